@@ -1,0 +1,53 @@
+"""In-tree build of libfks_hip.so (HIP kernels for gfx950 + the C-ABI host code).
+
+hipcc cross-compiles here without a GPU; the .so travels to the GPU box with the
+repository snapshot.  Every translation unit is compiled with -ffp-contract=off:
+bit-exact parity with the CPU oracle depends on the absence of fused multiply-adds.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+SOURCES = ["csrc/fks_kernels.hip", "csrc/fks_capi.cpp", "csrc/fks_env_builder.cpp"]
+HEADERS = ["csrc/fks_device.h", "../include/fks_capi.h", "../include/fks_portable_math.h"]
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
+
+
+def hipcc() -> str:
+    return shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+
+def build_command(output: str) -> list:
+    return [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
+            f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(PKG, 'csrc')}", "-x", "hip",
+            *[os.path.join(PKG, s) for s in SOURCES], "-o", output]
+
+
+def _stale(target: str) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    deps = [os.path.join(PKG, s) for s in SOURCES + HEADERS]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build_library(force: bool = False, verbose: bool = False) -> str:
+    target = os.path.join(PKG, "libfks_hip.so")
+    if not force and not _stale(target):
+        return target
+    tmp = target + ".tmp"
+    proc = subprocess.run(build_command(tmp), cwd=PKG, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + proc.stdout[-6000:])
+    if verbose:
+        print(proc.stdout)
+    os.replace(tmp, target)
+    return target
+
+
+if __name__ == "__main__":
+    print(build_library(force=True, verbose=True))

@@ -1,0 +1,724 @@
+/*
+ * fks_capi.cpp — host implementation of the C-ABI in include/fks_capi.h.
+ *
+ * A context mirrors one SimpleParticleContactSimulator (SPCS:371-1999): it owns
+ * device copies of the SDF and the surface-normal grid (copied once, as the
+ * reference copies them at construction SPCS:420), the flattened robot, the
+ * solver parameters (SPCS:345-369) and the counter-based RNG stream state.
+ * fks_forward_simulate replaces the OpenMP particle loop of
+ * ForwardSimulateRobots (SPCS:788-804) with one launch of the persistent
+ * simulation kernel.  No exceptions cross the ABI.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "fks_capi.h"
+#include "fks_device.h"
+#include "fks_portable_math.h"
+
+extern "C" __global__ void fks_simulate_particles(fksd::SimArgs args);
+extern "C" __global__ void fks_math_probe(const double* a, const double* b, double* out, uint64_t n);
+
+namespace {
+
+using fksd::GridDev;
+using fksd::JointDev;
+using fksd::RobotDev;
+
+inline double dot3(double a0, double a1, double a2, double b0, double b1, double b2) { return (a0 * b0 + a1 * b1) + a2 * b2; }
+
+void inverse34(const double* T, double* I) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) I[4 * i + j] = T[4 * j + i];
+    for (int i = 0; i < 3; ++i) I[4 * i + 3] = -dot3(I[4 * i + 0], I[4 * i + 1], I[4 * i + 2], T[3], T[7], T[11]);
+}
+
+GridDev make_grid(const fks_grid_geometry& g) {
+    GridDev d;
+    std::memcpy(d.org, g.origin, sizeof(d.org));
+    inverse34(d.org, d.inv);
+    d.res = g.resolution;
+    d.inv_res = 1.0 / g.resolution;
+    for (int a = 0; a < 3; ++a) d.n[a] = g.num_cells[a];
+    return d;
+}
+
+uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+uint32_t forward_steps(double time, double frequency) {
+    const double raw = time * frequency;
+    if (!(raw < 4294967295.0)) return 0xffffffffu;
+    const uint32_t steps = (raw > 0.0) ? (uint32_t)raw : 0u;
+    return steps > 1u ? steps : 1u;
+}
+
+template <typename T>
+hipError_t dev_upload(T** dptr, const T* host, size_t count) {
+    *dptr = nullptr;
+    if (count == 0) return hipSuccess;
+    hipError_t e = hipMalloc((void**)dptr, count * sizeof(T));
+    if (e != hipSuccess) return e;
+    return hipMemcpy(*dptr, host, count * sizeof(T), hipMemcpyHostToDevice);
+}
+
+bool valid_grid(const fks_grid_geometry& g) {
+    if (!(g.resolution > 0.0) || !std::isfinite(g.resolution)) return false;
+    for (int a = 0; a < 3; ++a)
+        if (g.num_cells[a] < 2 || g.num_cells[a] > 65535) return false;
+    const double cells = (double)g.num_cells[0] * (double)g.num_cells[1] * (double)g.num_cells[2];
+    return cells < 4294967295.0;
+}
+
+bool same_geometry(const fks_grid_geometry& a, const fks_grid_geometry& b) {
+    return std::memcmp(a.origin, b.origin, sizeof(a.origin)) == 0 && a.resolution == b.resolution &&
+           a.num_cells[0] == b.num_cells[0] && a.num_cells[1] == b.num_cells[1] && a.num_cells[2] == b.num_cells[2];
+}
+
+}  // namespace
+
+struct fks_context {
+    int device = 0;
+    std::string last_error;
+    int32_t debug_level = 0;
+    fks_solver_params params;
+    double frequency = 1.0;
+    uint64_t seed = 0;
+    uint64_t call_index = 0;
+    /* environment */
+    float* d_sdf = nullptr;
+    uint32_t* d_noff = nullptr;
+    double* d_nent = nullptr;
+    GridDev sdf_g, nrm_g, env_g;
+    float oob = 0.0f;
+    int32_t has_normals = 0;
+    /* robot */
+    bool has_robot = false;
+    RobotDev R;
+    std::vector<void*> robot_allocs;
+    /* launch resources */
+    double* d_scratch = nullptr;
+    uint64_t scratch_per_wave = 0;
+    uint32_t grid_waves = 0;
+    size_t lds_bytes = 0;
+    unsigned long long* d_counters = nullptr; /* kNumCounters + queue */
+    unsigned long long* h_counters = nullptr; /* pinned */
+    bool pending = false;
+    hipStream_t pending_stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::chrono::steady_clock::time_point call_start;
+    /* host-API staging */
+    double* d_starts = nullptr;
+    double* d_targets = nullptr;
+    double* d_out = nullptr;
+    uint8_t* d_coll = nullptr;
+    uint32_t* d_micro = nullptr;
+    uint32_t* d_res = nullptr;
+    uint32_t* d_err = nullptr;
+    size_t cap_particles = 0, cap_targets = 0;
+    fks_statistics stats;
+    fks_call_counters last;
+};
+
+template <typename T>
+static hipError_t ensure(T** p, size_t count) {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    return hipMalloc((void**)p, (count > 0 ? count : 1) * sizeof(T));
+}
+
+static fks_status fail(fks_context* ctx, fks_status st, const std::string& msg) {
+    if (ctx) ctx->last_error = msg;
+    return st;
+}
+static fks_status hip_fail(fks_context* ctx, hipError_t e, const char* where) {
+    return fail(ctx, FKS_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+#define HIP_TRY(ctx, expr)                                       \
+    do {                                                         \
+        hipError_t _e = (expr);                                  \
+        if (_e != hipSuccess) return hip_fail((ctx), _e, #expr); \
+    } while (0)
+
+static void free_robot(fks_context* ctx) {
+    for (void* p : ctx->robot_allocs) (void)hipFree(p);
+    ctx->robot_allocs.clear();
+    if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    ctx->d_scratch = nullptr;
+    ctx->has_robot = false;
+}
+
+static void free_staging(fks_context* ctx) {
+    void* ptrs[] = {ctx->d_starts, ctx->d_targets, ctx->d_out, ctx->d_coll, ctx->d_micro, ctx->d_res, ctx->d_err};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    ctx->d_starts = ctx->d_targets = ctx->d_out = nullptr;
+    ctx->d_coll = nullptr;
+    ctx->d_micro = ctx->d_res = ctx->d_err = nullptr;
+    ctx->cap_particles = ctx->cap_targets = 0;
+}
+
+extern "C" {
+
+int fks_abi_version(void) { return FKS_ABI_VERSION; }
+
+const char* fks_status_string(fks_status status) {
+    switch (status) {
+        case FKS_OK: return "ok";
+        case FKS_ERR_INVALID_ARGUMENT: return "invalid argument";
+        case FKS_ERR_HIP: return "HIP runtime error";
+        case FKS_ERR_NO_ROBOT: return "no robot set";
+        case FKS_ERR_OUT_OF_MEMORY: return "out of memory";
+        case FKS_ERR_UNSUPPORTED: return "unsupported";
+        case FKS_ERR_NO_DEVICE: return "no HIP device";
+        default: return "unknown status";
+    }
+}
+
+fks_status fks_default_solver_params(fks_solver_params* out) {
+    if (!out) return FKS_ERR_INVALID_ARGUMENT;
+    /* SimulatorSolverParameters() defaults, SPCS:357-368 */
+    out->forward_simulation_time = 1.0;
+    out->simulation_shortcut_distance = 0.0;
+    out->environment_collision_check_tolerance = 0.001;
+    out->resolve_correction_step_scaling_decay_rate = 0.5;
+    out->resolve_correction_initial_step_size = 1.0;
+    out->resolve_correction_min_step_scaling = 0.03125;
+    out->max_resolver_iterations = 25;
+    out->resolve_correction_step_scaling_decay_iterations = 5;
+    out->failed_resolves_end_motion = 1;
+    out->reserved = 0;
+    return FKS_OK;
+}
+
+fks_status fks_create(const fks_environment* env, const fks_solver_params* params, double simulation_controller_frequency,
+                      uint64_t prng_seed, int32_t debug_level, int32_t device, fks_context** out_ctx) {
+    if (!out_ctx) return FKS_ERR_INVALID_ARGUMENT;
+    *out_ctx = nullptr;
+    if (!env || !params || !env->sdf_values) return FKS_ERR_INVALID_ARGUMENT;
+    if (!valid_grid(env->sdf) || !valid_grid(env->collision_map) || !valid_grid(env->normals)) return FKS_ERR_INVALID_ARGUMENT;
+    if (!(simulation_controller_frequency != 0.0) || !std::isfinite(simulation_controller_frequency)) return FKS_ERR_INVALID_ARGUMENT;
+    if (params->resolve_correction_step_scaling_decay_iterations == 0) return FKS_ERR_INVALID_ARGUMENT;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return FKS_ERR_NO_DEVICE;
+    if (device < 0 || device >= count) return FKS_ERR_INVALID_ARGUMENT;
+    fks_context* ctx = new (std::nothrow) fks_context();
+    if (!ctx) return FKS_ERR_OUT_OF_MEMORY;
+    ctx->device = device;
+    ctx->params = *params;
+    ctx->frequency = simulation_controller_frequency;
+    ctx->seed = prng_seed;
+    ctx->debug_level = debug_level;
+    std::memset(&ctx->stats, 0, sizeof(ctx->stats));
+    std::memset(&ctx->last, 0, sizeof(ctx->last));
+    auto bail = [&](hipError_t e, const char* where) {
+        (void)where;
+        (void)e;
+        fks_destroy(ctx);
+        return FKS_ERR_HIP;
+    };
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return bail(e, "hipSetDevice");
+    ctx->sdf_g = make_grid(env->sdf);
+    ctx->nrm_g = make_grid(env->normals);
+    ctx->env_g = make_grid(env->collision_map);
+    ctx->oob = env->sdf_oob_value;
+    const size_t cells = (size_t)env->sdf.num_cells[0] * (size_t)env->sdf.num_cells[1] * (size_t)env->sdf.num_cells[2];
+    if ((e = dev_upload(&ctx->d_sdf, env->sdf_values, cells)) != hipSuccess) return bail(e, "sdf upload");
+    if (env->normal_offsets && env->normal_entries) {
+        const size_t ncells = (size_t)env->normals.num_cells[0] * (size_t)env->normals.num_cells[1] * (size_t)env->normals.num_cells[2];
+        const size_t entries = env->normal_offsets[ncells];
+        if ((e = dev_upload(&ctx->d_noff, env->normal_offsets, ncells + 1)) != hipSuccess) return bail(e, "normal offsets upload");
+        if (entries > 0 && (e = dev_upload(&ctx->d_nent, env->normal_entries, 6 * entries)) != hipSuccess)
+            return bail(e, "normal entries upload");
+        ctx->has_normals = 1;
+    }
+    if ((e = hipMalloc((void**)&ctx->d_counters, (fksd::kNumCounters + 2) * sizeof(unsigned long long))) != hipSuccess)
+        return bail(e, "counters");
+    if ((e = hipHostMalloc((void**)&ctx->h_counters, (fksd::kNumCounters + 2) * sizeof(unsigned long long), 0)) != hipSuccess)
+        return bail(e, "pinned counters");
+    if ((e = hipEventCreate(&ctx->ev0)) != hipSuccess) return bail(e, "event");
+    if ((e = hipEventCreate(&ctx->ev1)) != hipSuccess) return bail(e, "event");
+    (void)same_geometry;
+    *out_ctx = ctx;
+    return FKS_OK;
+}
+
+void fks_destroy(fks_context* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->pending && ctx->pending_stream) (void)hipStreamSynchronize(ctx->pending_stream);
+    (void)hipDeviceSynchronize();
+    free_robot(ctx);
+    free_staging(ctx);
+    if (ctx->d_sdf) (void)hipFree(ctx->d_sdf);
+    if (ctx->d_noff) (void)hipFree(ctx->d_noff);
+    if (ctx->d_nent) (void)hipFree(ctx->d_nent);
+    if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    delete ctx;
+}
+
+const char* fks_get_last_error(const fks_context* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+int32_t fks_config_width(const fks_context* ctx) { return (ctx && ctx->has_robot) ? ctx->R.W : 0; }
+
+fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    if (!d) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "null robot");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (ctx->pending && ctx->pending_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->pending_stream));
+    const int G = d->num_geometries;
+    if (G < 1 || G > fksd::kMaxGeoms || !d->geometry_link || !d->geometry_point_offset || !d->points || !d->controllers)
+        return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "robot geometries/controllers missing or more than 64 geometries");
+    const uint32_t P = d->geometry_point_offset[G];
+    if (d->geometry_point_offset[0] != 0 || P < 1 || P > 65535)
+        return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "robot needs 1..65535 points with offsets starting at 0");
+    for (int g = 0; g < G; ++g)
+        if (d->geometry_point_offset[g + 1] < d->geometry_point_offset[g])
+            return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "geometry offsets must be non-decreasing");
+    for (uint32_t i = 0; i < 4 * P; ++i)
+        if (!std::isfinite(d->points[i])) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "non-finite robot point");
+    RobotDev R;
+    std::memset(&R, 0, sizeof(R));
+    R.type = d->robot_type;
+    R.G = G;
+    R.P = (int32_t)P;
+    std::vector<JointDev> joints;
+    std::vector<int32_t> dof_joint;
+    std::vector<int32_t> link_parent_joint;
+    if (d->robot_type == FKS_ROBOT_LINKED) {
+        const int L = d->num_links, J = d->num_joints;
+        if (L < 1 || L > fksd::kMaxLinks || J < 0 || J > fksd::kMaxJoints || (J > 0 && !d->joints))
+            return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "linked robot needs 1..64 links and 0..64 joints");
+        std::vector<int> seen(L, 0);
+        seen[0] = 1;
+        link_parent_joint.assign(L, -1);
+        for (int j = 0; j < J; ++j) {
+            const fks_joint_desc& jd = d->joints[j];
+            if (jd.parent_link < 0 || jd.parent_link >= L || jd.child_link <= 0 || jd.child_link >= L)
+                return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "joint link index out of range");
+            if (!seen[jd.parent_link] || seen[jd.child_link])
+                return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "joints must be in topological order, one parent per link");
+            seen[jd.child_link] = 1;
+            link_parent_joint[jd.child_link] = j;
+            if (jd.type != FKS_JOINT_FIXED && jd.type != FKS_JOINT_REVOLUTE && jd.type != FKS_JOINT_CONTINUOUS &&
+                jd.type != FKS_JOINT_PRISMATIC)
+                return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "unknown joint type");
+            JointDev jv;
+            std::memset(&jv, 0, sizeof(jv));
+            jv.parent = jd.parent_link;
+            jv.child = jd.child_link;
+            jv.type = jd.type;
+            jv.dof = -1;
+            std::memcpy(jv.origin, jd.origin, sizeof(jv.origin));
+            std::memcpy(jv.axis, jd.axis, sizeof(jv.axis));
+            jv.lo = jd.limit_lower;
+            jv.hi = jd.limit_upper;
+            if (jd.type != FKS_JOINT_FIXED) {
+                jv.dof = (int32_t)dof_joint.size();
+                dof_joint.push_back(j);
+            }
+            joints.push_back(jv);
+        }
+        for (int l = 0; l < L; ++l)
+            if (!seen[l]) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "every link must be reached by a joint");
+        if ((int)dof_joint.size() != d->num_dofs || d->num_dofs < 1 || d->num_dofs > fksd::kMaxDofs)
+            return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "num_dofs must equal the number of non-fixed joints (1..64)");
+        for (int g = 0; g < G; ++g)
+            if (d->geometry_link[g] < 0 || d->geometry_link[g] >= L)
+                return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "geometry link index out of range");
+        R.L = L;
+        R.J = J;
+        R.D = d->num_dofs;
+        R.W = d->num_dofs;
+    } else if (d->robot_type == FKS_ROBOT_SE2 || d->robot_type == FKS_ROBOT_SE3) {
+        const int D = (d->robot_type == FKS_ROBOT_SE2) ? 3 : 6;
+        if (d->num_dofs != D || G != 1 || d->geometry_link[0] != 0)
+            return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "SE(2)/SE(3) robots have one geometry on link 0 and 3/6 dofs");
+        R.L = 1;
+        R.J = 0;
+        R.D = D;
+        R.W = (d->robot_type == FKS_ROBOT_SE2) ? 3 : 12;
+    } else {
+        return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "unknown robot type");
+    }
+    std::memcpy(R.base, d->base_transform, sizeof(R.base));
+    /* allowed self-collision masks (CheckIfSelfCollisionAllowed, symmetric, self allowed) */
+    std::vector<uint64_t> allowed(G, 0);
+    for (int g = 0; g < G; ++g) allowed[g] |= 1ull << g;
+    for (int k = 0; k < d->num_allowed_pairs; ++k) {
+        const int a = d->allowed_pairs[2 * k], b = d->allowed_pairs[2 * k + 1];
+        if (a < 0 || a >= G || b < 0 || b >= G) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "allowed pair out of range");
+        allowed[a] |= 1ull << b;
+        allowed[b] |= 1ull << a;
+    }
+    std::vector<int32_t> pairs;
+    for (int a = 0; a < G; ++a)
+        for (int b = a + 1; b < G; ++b)
+            if (!((allowed[a] >> b) & 1ull)) {
+                pairs.push_back(a);
+                pairs.push_back(b);
+            }
+    R.npairs = (int32_t)(pairs.size() / 2);
+    R.self_possible = !(G == 1 || (G == 2 && ((allowed[0] >> 1) & 1ull)));
+    /* per point geometry, per geometry local boxes and link masses (SPCS:1244-1255) */
+    std::vector<uint16_t> point_geom(P);
+    std::vector<double> box(7 * (size_t)G), mass(G);
+    for (int g = 0; g < G; ++g) {
+        const uint32_t b0 = d->geometry_point_offset[g], b1 = d->geometry_point_offset[g + 1];
+        double mn[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, mx[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+        bool w_one = true;
+        for (uint32_t i = b0; i < b1; ++i) {
+            point_geom[i] = (uint16_t)g;
+            for (int a = 0; a < 3; ++a) {
+                mn[a] = std::fmin(mn[a], d->points[4 * i + a]);
+                mx[a] = std::fmax(mx[a], d->points[4 * i + a]);
+            }
+            w_one = w_one && d->points[4 * i + 3] == 1.0;
+        }
+        if (b1 == b0) {
+            for (int a = 0; a < 3; ++a) mn[a] = mx[a] = 0.0;
+        }
+        for (int a = 0; a < 3; ++a) {
+            box[7 * g + a] = 0.5 * (mn[a] + mx[a]);
+            box[7 * g + 3 + a] = 0.5 * (mx[a] - mn[a]);
+        }
+        box[7 * g + 6] = w_one ? 1.0 : 0.0;
+    }
+    double previous_link_masses = 0.0;
+    for (int g = G - 1; g >= 0; --g) {
+        const double link_mass = (double)(d->geometry_point_offset[g + 1] - d->geometry_point_offset[g]);
+        mass[g] = link_mass + previous_link_masses;
+        previous_link_masses += link_mass;
+    }
+    /* dofs moving each link: joints whose child is an ancestor-or-self of the link */
+    std::vector<uint64_t> link_mask(R.L, 0);
+    if (d->robot_type == FKS_ROBOT_LINKED) {
+        for (int l = 0; l < R.L; ++l) {
+            int cur = l;
+            while (cur > 0) {
+                const int j = link_parent_joint[cur];
+                if (joints[j].dof >= 0) link_mask[l] |= 1ull << joints[j].dof;
+                cur = joints[j].parent;
+            }
+        }
+    }
+    std::vector<double> weights;
+    if (d->robot_type == FKS_ROBOT_LINKED) {
+        for (int k = 0; k < R.D; ++k) weights.push_back(d->distance_weights ? d->distance_weights[k] : 1.0);
+    } else {
+        weights.push_back(d->distance_weights ? d->distance_weights[0] : 1.0);
+        weights.push_back(d->distance_weights ? d->distance_weights[1] : 1.0);
+    }
+    free_robot(ctx);
+    auto up = [&](auto** dptr, const auto* host, size_t count) -> hipError_t {
+        hipError_t e = dev_upload(dptr, host, count);
+        if (*dptr) ctx->robot_allocs.push_back((void*)*dptr);
+        return e;
+    };
+    JointDev* dj = nullptr;
+    int32_t *dgl = nullptr, *ddj = nullptr, *dpairs = nullptr;
+    uint32_t* dgo = nullptr;
+    double *dpts = nullptr, *dbox = nullptr, *dmass = nullptr, *dw = nullptr;
+    uint16_t* dpg = nullptr;
+    uint64_t *dlm = nullptr, *dam = nullptr;
+    fks_dof_controller* dctrl = nullptr;
+    HIP_TRY(ctx, up(&dj, joints.data(), joints.size()));
+    HIP_TRY(ctx, up(&dgl, d->geometry_link, (size_t)G));
+    HIP_TRY(ctx, up(&dgo, d->geometry_point_offset, (size_t)G + 1));
+    HIP_TRY(ctx, up(&dpts, d->points, 4 * (size_t)P));
+    HIP_TRY(ctx, up(&dpg, point_geom.data(), (size_t)P));
+    HIP_TRY(ctx, up(&ddj, dof_joint.data(), dof_joint.size()));
+    HIP_TRY(ctx, up(&dlm, link_mask.data(), link_mask.size()));
+    HIP_TRY(ctx, up(&dpairs, pairs.data(), pairs.size()));
+    HIP_TRY(ctx, up(&dam, allowed.data(), allowed.size()));
+    HIP_TRY(ctx, up(&dbox, box.data(), box.size()));
+    HIP_TRY(ctx, up(&dmass, mass.data(), mass.size()));
+    HIP_TRY(ctx, up(&dctrl, d->controllers, (size_t)R.D));
+    HIP_TRY(ctx, up(&dw, weights.data(), weights.size()));
+    R.joints = dj;
+    R.geom_link = dgl;
+    R.geom_off = dgo;
+    R.points = dpts;
+    R.point_geom = dpg;
+    R.dof_joint = ddj;
+    R.link_dof_mask = dlm;
+    R.pairs = dpairs;
+    R.allowed_mask = dam;
+    R.geom_box = dbox;
+    R.geom_mass = dmass;
+    R.ctrl = dctrl;
+    R.weights = dw;
+    /* launch geometry: one wave per workgroup, as many resident waves as fit */
+    const fksd::LdsLayout L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G);
+    ctx->lds_bytes = (size_t)L.total * sizeof(double);
+    if (ctx->lds_bytes > 64 * 1024) return fail(ctx, FKS_ERR_UNSUPPORTED, "robot too large for the LDS layout");
+    int blocks_per_cu = 0;
+    HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, reinterpret_cast<const void*>(fks_simulate_particles),
+                                                              64, ctx->lds_bytes));
+    if (blocks_per_cu < 1) return fail(ctx, FKS_ERR_UNSUPPORTED, "kernel does not fit on a CU");
+    int cus = 0;
+    HIP_TRY(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    ctx->grid_waves = (uint32_t)(cus * blocks_per_cu);
+    ctx->scratch_per_wave = fksd::make_scratch_layout(3u * P, R.D, (int)P).total;
+    HIP_TRY(ctx, hipMalloc((void**)&ctx->d_scratch, (size_t)ctx->grid_waves * ctx->scratch_per_wave * sizeof(double)));
+    ctx->R = R;
+    ctx->has_robot = true;
+    return FKS_OK;
+}
+
+/* fold the counters of a finished launch into the statistics */
+static fks_status settle(fks_context* ctx) {
+    if (!ctx->pending) return FKS_OK;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->pending_stream));
+    ctx->pending = false;
+    const unsigned long long* c = ctx->h_counters;
+    ctx->stats.successful_resolves += c[fksd::kCntSuccessful];
+    ctx->stats.unsuccessful_resolves += c[fksd::kCntUnsuccessful];
+    ctx->stats.free_resolves += c[fksd::kCntFree];
+    ctx->stats.collision_resolves += c[fksd::kCntCollision];
+    ctx->stats.fallback_resolves += c[fksd::kCntFallback];
+    ctx->stats.unsuccessful_env_collision_resolves += c[fksd::kCntUnsuccessfulEnv];
+    ctx->stats.unsuccessful_self_collision_resolves += c[fksd::kCntUnsuccessfulSelf];
+    ctx->stats.recovered_unsuccessful_resolves += c[fksd::kCntRecovered];
+    ctx->last.controller_steps = c[fksd::kCntSteps];
+    ctx->last.microsteps = c[fksd::kCntMicrosteps];
+    ctx->last.resolver_iterations = c[fksd::kCntResolver];
+    ctx->last.sdf_bytes = c[fksd::kCntSdfBytes];
+    ctx->last.error_particles = c[fksd::kCntErrorParticles];
+    float ms = 0.0f;
+    HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->last.kernel_ms = (double)ms;
+    ctx->last.call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ctx->call_start).count();
+    return FKS_OK;
+}
+
+fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts, uint64_t n, const double* d_targets,
+                                       uint64_t num_targets, uint64_t first_particle_id, int32_t allow_contacts,
+                                       double* d_out_positions, uint8_t* d_out_collided, uint32_t* d_out_microsteps,
+                                       uint32_t* d_out_resolver_iterations, uint32_t* d_out_error_flags, void* stream,
+                                       int32_t synchronize) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    if (!ctx->has_robot) return fail(ctx, FKS_ERR_NO_ROBOT, "fks_set_robot has not been called");
+    if (n > 0 && (!d_starts || !d_targets || !d_out_positions))
+        return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "null device buffer");
+    if (n > 0 && num_targets != 1 && num_targets != n)
+        return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "targets must be 1 or n (SPCS:792)");
+    if (n > 0xffffffffull) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "at most 2^32-1 particles per call");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    fks_status st = settle(ctx);
+    if (st != FKS_OK) return st;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    ctx->call_start = std::chrono::steady_clock::now();
+    const uint64_t key = splitmix64(ctx->seed ^ splitmix64(ctx->call_index));
+    ctx->call_index++;
+    std::memset(&ctx->last, 0, sizeof(ctx->last));
+    ctx->last.particles = n;
+    fksd::SimArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.sdf_g = ctx->sdf_g;
+    a.nrm_g = ctx->nrm_g;
+    a.env_g = ctx->env_g;
+    a.sdf = ctx->d_sdf;
+    a.noff = ctx->d_noff;
+    a.nent = ctx->d_nent;
+    a.oob = ctx->oob;
+    a.has_normals = ctx->has_normals;
+    a.R = ctx->R;
+    a.S = ctx->params;
+    a.dt = 1.0 / ctx->frequency;
+    a.thr_env = 0.0 - (ctx->params.environment_collision_check_tolerance * ctx->sdf_g.res);
+    a.target_micro = ctx->env_g.res * 0.125;
+    a.allowed_micro = ctx->env_g.res * 1.0;
+    a.time_multiplier = 1.0 / a.dt;
+    a.T = forward_steps(ctx->params.forward_simulation_time, std::fabs(ctx->frequency));
+    a.key0 = (uint32_t)key;
+    a.key1 = (uint32_t)(key >> 32);
+    a.starts = d_starts;
+    a.targets = d_targets;
+    a.num_targets = num_targets;
+    a.n = n;
+    a.first_pid = first_particle_id;
+    a.allow_contacts = allow_contacts ? 1 : 0;
+    a.out_q = d_out_positions;
+    a.out_collided = d_out_collided;
+    a.out_micro = d_out_microsteps;
+    a.out_resolver = d_out_resolver_iterations;
+    a.out_err = d_out_error_flags;
+    a.counters = ctx->d_counters;
+    a.queue = ctx->d_counters + fksd::kNumCounters;
+    a.scratch = ctx->d_scratch;
+    a.scratch_per_wave = ctx->scratch_per_wave;
+    a.row_cap = 3u * (uint32_t)ctx->R.P;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, (fksd::kNumCounters + 2) * sizeof(unsigned long long), s));
+    const uint32_t grid = (uint32_t)((n < (uint64_t)ctx->grid_waves) ? (n > 0 ? n : 1) : ctx->grid_waves);
+    HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
+    hipLaunchKernelGGL(fks_simulate_particles, dim3(grid), dim3(64), ctx->lds_bytes, s, a);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_counters, ctx->d_counters, (fksd::kNumCounters + 2) * sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost, s));
+    ctx->pending = true;
+    ctx->pending_stream = s;
+    if (synchronize) return settle(ctx);
+    return FKS_OK;
+}
+
+static fks_status simulate_host(fks_context* ctx, const double* starts, uint64_t n, const double* targets, uint64_t num_targets,
+                                int32_t allow_contacts, double* out_positions, uint8_t* out_collided, uint32_t* out_microsteps,
+                                uint32_t* out_resolver_iterations, uint32_t* out_error_flags) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    if (!ctx->has_robot) return fail(ctx, FKS_ERR_NO_ROBOT, "fks_set_robot has not been called");
+    if (n > 0 && (!starts || !targets || !out_positions)) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "null host buffer");
+    if (n > 0 && num_targets != 1 && num_targets != n)
+        return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "targets must be 1 or n (SPCS:792)");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    fks_status st = settle(ctx);
+    if (st != FKS_OK) return st;
+    const size_t W = (size_t)ctx->R.W;
+    if (n > ctx->cap_particles) {
+        HIP_TRY(ctx, ensure(&ctx->d_starts, n * W));
+        HIP_TRY(ctx, ensure(&ctx->d_out, n * W));
+        HIP_TRY(ctx, ensure(&ctx->d_coll, n));
+        HIP_TRY(ctx, ensure(&ctx->d_micro, n));
+        HIP_TRY(ctx, ensure(&ctx->d_res, n));
+        HIP_TRY(ctx, ensure(&ctx->d_err, n));
+        ctx->cap_particles = n;
+    }
+    const uint64_t nt = (n > 0) ? num_targets : 0;
+    if (nt > ctx->cap_targets || !ctx->d_targets) {
+        HIP_TRY(ctx, ensure(&ctx->d_targets, (nt > 0 ? nt : 1) * W));
+        ctx->cap_targets = nt > 0 ? nt : 1;
+    }
+    if (n == 0) {
+        ctx->call_index++;
+        std::memset(&ctx->last, 0, sizeof(ctx->last));
+        return FKS_OK;
+    }
+    HIP_TRY(ctx, hipMemcpy(ctx->d_starts, starts, n * W * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_targets, targets, nt * W * sizeof(double), hipMemcpyHostToDevice));
+    st = fks_forward_simulate_device(ctx, ctx->d_starts, n, ctx->d_targets, nt, 0, allow_contacts, ctx->d_out, ctx->d_coll,
+                                     ctx->d_micro, ctx->d_res, ctx->d_err, nullptr, 1);
+    if (st != FKS_OK) return st;
+    HIP_TRY(ctx, hipMemcpy(out_positions, ctx->d_out, n * W * sizeof(double), hipMemcpyDeviceToHost));
+    if (out_collided) HIP_TRY(ctx, hipMemcpy(out_collided, ctx->d_coll, n, hipMemcpyDeviceToHost));
+    if (out_microsteps) HIP_TRY(ctx, hipMemcpy(out_microsteps, ctx->d_micro, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (out_resolver_iterations)
+        HIP_TRY(ctx, hipMemcpy(out_resolver_iterations, ctx->d_res, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (out_error_flags) HIP_TRY(ctx, hipMemcpy(out_error_flags, ctx->d_err, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    ctx->last.call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ctx->call_start).count();
+    return FKS_OK;
+}
+
+fks_status fks_forward_simulate(fks_context* ctx, const double* starts, uint64_t n, const double* targets, uint64_t num_targets,
+                                int32_t allow_contacts, double* out_positions, uint8_t* out_collided, uint32_t* out_microsteps,
+                                uint32_t* out_resolver_iterations, uint32_t* out_error_flags) {
+    return simulate_host(ctx, starts, n, targets, num_targets, allow_contacts, out_positions, out_collided, out_microsteps,
+                         out_resolver_iterations, out_error_flags);
+}
+
+/* ReverseSimulateRobots: ReverseSimulateMutableRobot == ForwardSimulateMutableRobot (SPCS:838-841) */
+fks_status fks_reverse_simulate(fks_context* ctx, const double* starts, uint64_t n, const double* targets, uint64_t num_targets,
+                                int32_t allow_contacts, double* out_positions, uint8_t* out_collided, uint32_t* out_microsteps,
+                                uint32_t* out_resolver_iterations, uint32_t* out_error_flags) {
+    return simulate_host(ctx, starts, n, targets, num_targets, allow_contacts, out_positions, out_collided, out_microsteps,
+                         out_resolver_iterations, out_error_flags);
+}
+
+fks_status fks_set_call_index(fks_context* ctx, uint64_t call_index) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    ctx->call_index = call_index;
+    return FKS_OK;
+}
+uint64_t fks_get_call_index(const fks_context* ctx) { return ctx ? ctx->call_index : 0; }
+
+fks_status fks_get_statistics(const fks_context* ctx, fks_statistics* out) {
+    if (!ctx || !out) return FKS_ERR_INVALID_ARGUMENT;
+    fks_status st = settle(const_cast<fks_context*>(ctx));
+    if (st != FKS_OK) return st;
+    *out = ctx->stats;
+    return FKS_OK;
+}
+fks_status fks_reset_statistics(fks_context* ctx) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    fks_status st = settle(ctx);
+    if (st != FKS_OK) return st;
+    std::memset(&ctx->stats, 0, sizeof(ctx->stats));
+    return FKS_OK;
+}
+fks_status fks_reset_generators(fks_context* ctx, uint64_t prng_seed) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    ctx->seed = prng_seed;
+    ctx->call_index = 0;
+    return FKS_OK;
+}
+int32_t fks_get_debug_level(const fks_context* ctx) { return ctx ? ctx->debug_level : 0; }
+int32_t fks_set_debug_level(fks_context* ctx, int32_t debug_level) {
+    if (!ctx) return 0;
+    ctx->debug_level = debug_level;
+    return ctx->debug_level;
+}
+fks_status fks_get_last_call_counters(const fks_context* ctx, fks_call_counters* out) {
+    if (!ctx || !out) return FKS_ERR_INVALID_ARGUMENT;
+    fks_status st = settle(const_cast<fks_context*>(ctx));
+    if (st != FKS_OK) return st;
+    *out = ctx->last;
+    return FKS_OK;
+}
+
+fks_status fks_selftest_math(int32_t device, uint64_t n, uint64_t* out_mismatches) {
+    if (!out_mismatches || n == 0 || n > (1ull << 26)) return FKS_ERR_INVALID_ARGUMENT;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return FKS_ERR_NO_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return FKS_ERR_HIP;
+    std::vector<double> a(n), b(n), host(8 * n), dev(8 * n);
+    uint64_t st = 0x1234567ull;
+    for (uint64_t i = 0; i < n; ++i) {
+        st = splitmix64(st);
+        a[i] = ((double)(st >> 11) * (1.0 / 9007199254740992.0) - 0.5) * 40.0;
+        st = splitmix64(st);
+        b[i] = ((double)(st >> 11) * (1.0 / 9007199254740992.0) - 0.5) * std::pow(10.0, (double)((st & 15) - 6));
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+        const double x = a[i], y = b[i];
+        host[8 * i + 0] = fks_math::sin(x);
+        host[8 * i + 1] = fks_math::cos(x);
+        host[8 * i + 2] = fks_math::log(fks_math::dabs(y) + 1e-300);
+        host[8 * i + 3] = fks_math::atan2(x, y);
+        host[8 * i + 4] = fks_math::dsqrt(fks_math::dabs(y));
+        host[8 * i + 5] = x / y;
+        host[8 * i + 6] = fks_math::enforce_continuous_revolute_bounds(x);
+        host[8 * i + 7] = (x * y + x) * y - x * x;
+    }
+    double *da = nullptr, *db = nullptr, *dout = nullptr;
+    if (dev_upload(&da, a.data(), n) != hipSuccess || dev_upload(&db, b.data(), n) != hipSuccess ||
+        hipMalloc((void**)&dout, 8 * n * sizeof(double)) != hipSuccess)
+        return FKS_ERR_HIP;
+    hipLaunchKernelGGL(fks_math_probe, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr, da, db, dout, n);
+    hipError_t e = hipMemcpy(dev.data(), dout, 8 * n * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(da);
+    (void)hipFree(db);
+    (void)hipFree(dout);
+    if (e != hipSuccess) return FKS_ERR_HIP;
+    uint64_t mism = 0;
+    for (uint64_t i = 0; i < 8 * n; ++i)
+        if (std::memcmp(&host[i], &dev[i], sizeof(double)) != 0) mism++;
+    *out_mismatches = mism;
+    return FKS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,212 @@
+/*
+ * Device-side data layout of the particle forward-simulation kernel (shared by
+ * the host launcher fks_capi.cpp and the kernels in fks_kernels.hip).
+ *
+ * HBM layout (all resident for the life of a context / robot):
+ *   SDF            float[nx*ny*nz], z fastest (arc_utilities VoxelGrid order)
+ *   normal grid    CSR: uint32 offsets[cells+1], 6 doubles per entry
+ *   robot          JointDev[J], per-geometry tables, points as double4 (x,y,z,w)
+ *                  in geometry-major order (the order of robot_link_geometries)
+ *   per-wave scratch  least-squares matrix (column-major, 3P rows x (D+1) cols),
+ *                  self-collision keys / corrections / flags
+ * LDS layout (one wavefront per workgroup): see LdsLayout below.
+ */
+#ifndef FKS_DEVICE_H
+#define FKS_DEVICE_H
+
+#include <stdint.h>
+
+#include "fks_capi.h"
+
+namespace fksd {
+
+constexpr int kWave = 64;
+constexpr int kMaxLinks = 64;
+constexpr int kMaxDofs = 64;
+constexpr int kMaxGeoms = 64;
+constexpr int kMaxJoints = 64;
+
+struct GridDev {
+    double org[12]; /* origin transform, 3x4 row-major */
+    double inv[12]; /* inverse origin */
+    double res, inv_res;
+    int64_t n[3];
+};
+
+struct JointDev {
+    int32_t parent, child, type, dof;
+    double origin[12];
+    double axis[3];
+    double lo, hi;
+};
+
+struct RobotDev {
+    int32_t type, L, J, G, D, P, W, npairs;
+    int32_t self_possible;
+    int32_t pad;
+    double base[12];
+    const JointDev* joints;
+    const int32_t* geom_link;
+    const uint32_t* geom_off;
+    const double* points;      /* 4 per point */
+    const uint16_t* point_geom;
+    const int32_t* dof_joint;   /* linked: joint index of dof d */
+    const uint64_t* link_dof_mask; /* per link: dofs whose joint child is an ancestor-or-self */
+    const int32_t* pairs;       /* disallowed geometry pairs, 2 per pair (a < b) */
+    const uint64_t* allowed_mask; /* per geometry: bit b set if self-collision with b allowed */
+    const double* geom_box;     /* per geometry: local centre xyz, half extent xyz, all_w_one */
+    const double* geom_mass;    /* per geometry: link mass + masses of all later geometries */
+    const fks_dof_controller* ctrl;
+    const double* weights;
+};
+
+struct SimArgs {
+    GridDev sdf_g, nrm_g, env_g;
+    const float* sdf;
+    const uint32_t* noff;
+    const double* nent;
+    float oob;
+    int32_t has_normals;
+    RobotDev R;
+    fks_solver_params S;
+    double dt;               /* simulation_controller_interval_ = 1/frequency  (SPCS:427)   */
+    double thr_env;          /* 0 - tolerance * sdf resolution (SPCS:923, threshold 0 SPCS:424) */
+    double target_micro;     /* GetResolution() * 0.125 (SPCS:1560) */
+    double allowed_micro;    /* GetResolution() * 1.0   (SPCS:1561) */
+    double time_multiplier;  /* 1.0 / time_interval     (SPCS:1027) */
+    uint32_t T;              /* forward simulation steps (SPCS:856) */
+    uint32_t key0, key1;
+    uint32_t pad0;
+    const double* starts;
+    const double* targets;
+    uint64_t num_targets;
+    uint64_t n;
+    uint64_t first_pid;
+    int32_t allow_contacts;
+    int32_t pad1;
+    double* out_q;
+    uint8_t* out_collided;
+    uint32_t* out_micro;
+    uint32_t* out_resolver;
+    uint32_t* out_err;
+    unsigned long long* counters; /* kCounter* */
+    unsigned long long* queue;
+    double* scratch;
+    uint64_t scratch_per_wave; /* doubles */
+    uint32_t row_cap;          /* 3 * P */
+    uint32_t pad2;
+};
+
+enum {
+    kCntSuccessful = 0,
+    kCntUnsuccessful,
+    kCntFree,
+    kCntCollision,
+    kCntFallback,
+    kCntUnsuccessfulEnv,
+    kCntUnsuccessfulSelf,
+    kCntRecovered,
+    kCntSteps,
+    kCntMicrosteps,
+    kCntResolver,
+    kCntSdfBytes,
+    kCntErrorParticles,
+    kNumCounters = 16
+};
+
+/* LDS carve-out (in doubles), identical on host and device */
+struct LdsLayout {
+    uint32_t Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u, ustep, x, real, axis_w,
+        orig_w, colsq, hcoef, box, misc, ints, total;
+};
+
+inline
+#if defined(__HIPCC__)
+    __host__ __device__
+#endif
+    LdsLayout make_lds_layout(int L, int J, int D, int W, int G) {
+    LdsLayout l;
+    uint32_t o = 0;
+    l.Tcur = o;
+    o += 12u * L;
+    l.Tprev = o;
+    o += 12u * L;
+    l.Ttmp = o;
+    o += 12u * L;
+    l.jm = o;
+    o += 12u * (J > 0 ? J : 1);
+    l.cfg = o;
+    o += W;
+    l.cfg_work = o;
+    o += W;
+    l.cfg_res = o;
+    o += W;
+    l.tgt = o;
+    o += W;
+    l.cfg_prev = o;
+    o += W;
+    l.cfg_tmp = o;
+    o += W;
+    l.cfg_act = o;
+    o += W;
+    l.u = o;
+    o += D;
+    l.ustep = o;
+    o += D;
+    l.x = o;
+    o += D;
+    l.real = o;
+    o += D;
+    l.axis_w = o;
+    o += 3u * D;
+    l.orig_w = o;
+    o += 3u * D;
+    l.colsq = o;
+    o += D;
+    l.hcoef = o;
+    o += D;
+    l.box = o;
+    o += 6u * G;
+    l.misc = o;
+    o += 32;
+    l.ints = o; /* int32 region: perm[64], transpositions[64], 16 spare words */
+    o += (2 * kMaxDofs + 16) / 2;
+    o = (o + 1u) & ~1u; /* 16-byte alignment */
+    l.total = o;
+    return l;
+}
+
+/* per-wave scratch layout (doubles) */
+struct ScratchLayout {
+    uint64_t J, b, keys, corr, flag, cand, list, dense, total;
+};
+inline
+#if defined(__HIPCC__)
+    __host__ __device__
+#endif
+    ScratchLayout make_scratch_layout(uint32_t row_cap, int D, int P) {
+    ScratchLayout l;
+    uint64_t o = 0;
+    l.J = o;
+    o += (uint64_t)row_cap * (uint64_t)(D > 0 ? D : 1);
+    l.b = o;
+    o += row_cap;
+    l.keys = o;
+    o += 3ull * (uint64_t)P;
+    l.corr = o;
+    o += 3ull * (uint64_t)P;
+    l.flag = o;
+    o += (uint64_t)P;
+    l.cand = o;
+    o += (uint64_t)P;
+    l.list = o;
+    o += (uint64_t)P;
+    l.dense = o;
+    o += 8192;
+    l.total = (o + 7) & ~7ull;
+    return l;
+}
+
+}  // namespace fksd
+
+#endif

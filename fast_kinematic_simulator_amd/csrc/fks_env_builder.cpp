@@ -1,0 +1,348 @@
+/*
+ * Environment preprocessing on the host: obstacles -> collision grid -> signed
+ * distance field -> surface-normal grid.  Restates
+ * src/fast_kinematic_simulator/simulator_environment_builder.cpp (SEB.cpp):
+ *   DiscretizeObstacle        SEB.cpp:21-46   (half-resolution sample lattice)
+ *   BuildEnvironment          SEB.cpp:49-160  (auto bounds + 3-cell border, or a fixed box)
+ *   ExtractSignedDistanceField SEB.cpp:473    (sdf_tools, absent: restated as an exact
+ *                                             Euclidean distance transform, Felzenszwalb &
+ *                                             Huttenlocher 2012, distance to the nearest
+ *                                             opposite cell centre; +inf out of bounds)
+ *   BuildSurfaceNormalsGrid   SEB.cpp:258-468 (SDF-gradient pass for d<0 cells, then the exact
+ *                                             cuboid face/edge/corner normals, last write wins)
+ * This is the input side of the hot path ("next" row f2 in SURVEY.md §8f); the
+ * GPU build of it is future work.  Output layout is the fks_environment CSR.
+ */
+#include <stdint.h>
+
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <new>
+#include <unordered_map>
+#include <vector>
+
+#include "fks_capi.h"
+#include "fks_portable_math.h"
+
+namespace {
+
+struct Mat34 {
+    double m[12];
+};
+
+inline double dot3(double a0, double a1, double a2, double b0, double b1, double b2) {
+    return (a0 * b0 + a1 * b1) + a2 * b2;
+}
+
+/* Isometry3d * Vector3d */
+inline void xform3(const double* T, const double p[3], double out[3]) {
+    for (int i = 0; i < 3; ++i) out[i] = dot3(T[4 * i + 0], T[4 * i + 1], T[4 * i + 2], p[0], p[1], p[2]) + T[4 * i + 3];
+}
+inline void rotate3(const double* T, const double v[3], double out[3]) {
+    for (int i = 0; i < 3; ++i) out[i] = dot3(T[4 * i + 0], T[4 * i + 1], T[4 * i + 2], v[0], v[1], v[2]);
+}
+inline void inverse34(const double* T, double* I) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) I[4 * i + j] = T[4 * j + i];
+    for (int i = 0; i < 3; ++i) I[4 * i + 3] = -dot3(I[4 * i + 0], I[4 * i + 1], I[4 * i + 2], T[3], T[7], T[11]);
+}
+
+struct Grid {
+    double origin[12], inv_origin[12];
+    double res, inv_res;
+    int64_t n[3];
+    bool index(const double p[3], int64_t idx[3]) const {
+        double g[3];
+        xform3(inv_origin, p, g);
+        for (int a = 0; a < 3; ++a) {
+            const double q = g[a] * inv_res;
+            if (!(q > -9.0e18 && q < 9.0e18)) return false;
+            idx[a] = (int64_t)q;
+            if (idx[a] < 0 || idx[a] >= n[a]) return false;
+        }
+        return true;
+    }
+    size_t linear(int64_t i, int64_t j, int64_t k) const { return ((size_t)i * (size_t)n[1] + (size_t)j) * (size_t)n[2] + (size_t)k; }
+    size_t cells() const { return (size_t)n[0] * (size_t)n[1] * (size_t)n[2]; }
+};
+
+/* 1-D squared distance transform (lower envelope of parabolas rooted at the
+ * finite samples), exact on integer grids */
+void edt_1d(const double* f, double* d, int64_t n, int64_t* v, double* z) {
+    const double INF = std::numeric_limits<double>::infinity();
+    int64_t k = -1;
+    for (int64_t q = 0; q < n; ++q) {
+        if (!(f[q] < INF)) continue;
+        if (k < 0) {
+            k = 0;
+            v[0] = q;
+            z[0] = -INF;
+            z[1] = INF;
+            continue;
+        }
+        double s = ((f[q] + (double)(q * q)) - (f[v[k]] + (double)(v[k] * v[k]))) / (2.0 * (double)(q - v[k]));
+        while (s <= z[k]) {
+            k--;
+            s = ((f[q] + (double)(q * q)) - (f[v[k]] + (double)(v[k] * v[k]))) / (2.0 * (double)(q - v[k]));
+        }
+        k++;
+        v[k] = q;
+        z[k] = s;
+        z[k + 1] = INF;
+    }
+    if (k < 0) {
+        for (int64_t q = 0; q < n; ++q) d[q] = INF;
+        return;
+    }
+    k = 0;
+    for (int64_t q = 0; q < n; ++q) {
+        while (z[k + 1] < (double)q) k++;
+        const double dq = (double)(q - v[k]);
+        d[q] = dq * dq + f[v[k]];
+    }
+}
+
+/* squared distance (in cells) from every cell to the nearest cell with seed[c] != 0 */
+std::vector<double> edt_3d(const std::vector<uint8_t>& seed, const int64_t n[3]) {
+    const double INF = std::numeric_limits<double>::infinity();
+    const size_t total = (size_t)n[0] * (size_t)n[1] * (size_t)n[2];
+    std::vector<double> D(total);
+    for (size_t c = 0; c < total; ++c) D[c] = seed[c] ? 0.0 : INF;
+    const int64_t maxn = std::max(n[0], std::max(n[1], n[2]));
+    std::vector<double> f((size_t)maxn), d((size_t)maxn), z((size_t)maxn + 1);
+    std::vector<int64_t> v((size_t)maxn);
+    const int64_t sx = n[1] * n[2], sy = n[2];
+    /* z */
+    for (int64_t i = 0; i < n[0]; ++i)
+        for (int64_t j = 0; j < n[1]; ++j) {
+            const size_t base = (size_t)(i * sx + j * sy);
+            for (int64_t k = 0; k < n[2]; ++k) f[(size_t)k] = D[base + (size_t)k];
+            edt_1d(f.data(), d.data(), n[2], v.data(), z.data());
+            for (int64_t k = 0; k < n[2]; ++k) D[base + (size_t)k] = d[(size_t)k];
+        }
+    /* y */
+    for (int64_t i = 0; i < n[0]; ++i)
+        for (int64_t k = 0; k < n[2]; ++k) {
+            const size_t base = (size_t)(i * sx + k);
+            for (int64_t j = 0; j < n[1]; ++j) f[(size_t)j] = D[base + (size_t)(j * sy)];
+            edt_1d(f.data(), d.data(), n[1], v.data(), z.data());
+            for (int64_t j = 0; j < n[1]; ++j) D[base + (size_t)(j * sy)] = d[(size_t)j];
+        }
+    /* x */
+    for (int64_t j = 0; j < n[1]; ++j)
+        for (int64_t k = 0; k < n[2]; ++k) {
+            const size_t base = (size_t)(j * sy + k);
+            for (int64_t i = 0; i < n[0]; ++i) f[(size_t)i] = D[base + (size_t)(i * sx)];
+            edt_1d(f.data(), d.data(), n[0], v.data(), z.data());
+            for (int64_t i = 0; i < n[0]; ++i) D[base + (size_t)(i * sx)] = d[(size_t)i];
+        }
+    return D;
+}
+
+struct Entry {
+    double e[6];
+};
+
+}  // namespace
+
+struct fks_env_handle {
+    fks_grid_geometry geometry;
+    std::vector<float> sdf;
+    std::vector<uint32_t> offsets;
+    std::vector<double> entries;
+    std::vector<uint8_t> occupancy;
+};
+
+extern "C" fks_status fks_env_build(const fks_obstacle* obstacles, int32_t num_obstacles, double resolution,
+                                    const double* grid_origin, const int64_t* num_cells, fks_env_handle** out) {
+    if (!out || !(resolution > 0.0) || num_obstacles < 0 || (num_obstacles > 0 && !obstacles)) return FKS_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    const double effective_resolution = resolution * 0.5;
+    /* DiscretizeObstacle + world placement (SEB.cpp:21-46, 78-127) */
+    std::vector<double> cells;  // xyz triples
+    std::vector<uint32_t> cell_ids;
+    double mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
+    bool init = false;
+    for (int32_t o = 0; o < num_obstacles; ++o) {
+        const fks_obstacle& ob = obstacles[o];
+        int32_t nc[3];
+        for (int a = 0; a < 3; ++a) nc[a] = (int32_t)(ob.extents[a] * 2.0 * (1.0 / effective_resolution));
+        for (int32_t xi = 0; xi < nc[0]; ++xi)
+            for (int32_t yi = 0; yi < nc[1]; ++yi)
+                for (int32_t zi = 0; zi < nc[2]; ++zi) {
+                    const double local[3] = {-(ob.extents[0] - (resolution * 0.5)) + (effective_resolution * xi),
+                                             -(ob.extents[1] - (resolution * 0.5)) + (effective_resolution * yi),
+                                             -(ob.extents[2] - (resolution * 0.5)) + (effective_resolution * zi)};
+                    double w[3];
+                    xform3(ob.pose, local, w);
+                    cells.insert(cells.end(), w, w + 3);
+                    cell_ids.push_back(ob.object_id);
+                    if (!init) {
+                        for (int a = 0; a < 3; ++a) mn[a] = mx[a] = w[a];
+                        init = true;
+                    } else {
+                        for (int a = 0; a < 3; ++a) {
+                            if (w[a] < mn[a]) mn[a] = w[a];
+                            else if (w[a] > mx[a]) mx[a] = w[a];
+                        }
+                    }
+                }
+    }
+    Grid grid;
+    grid.res = resolution;
+    grid.inv_res = 1.0 / resolution;
+    if (grid_origin && num_cells) {
+        std::memcpy(grid.origin, grid_origin, sizeof(grid.origin));
+        for (int a = 0; a < 3; ++a) grid.n[a] = num_cells[a];
+    } else {
+        /* SEB.cpp:128-149: minimum point keyed half a cell out, plus a 3-cell border */
+        if (!init) {
+            for (int a = 0; a < 3; ++a) {
+                mn[a] = 0.0;
+                mx[a] = 10.0;
+            }
+        } else {
+            for (int a = 0; a < 3; ++a) {
+                mn[a] -= resolution * 0.5;
+                mn[a] -= resolution * 3.0;
+                mx[a] += resolution * 3.0;
+            }
+        }
+        const double I[12] = {1, 0, 0, mn[0], 0, 1, 0, mn[1], 0, 0, 1, mn[2]};
+        std::memcpy(grid.origin, I, sizeof(I));
+        for (int a = 0; a < 3; ++a) grid.n[a] = (int64_t)std::ceil((mx[a] - mn[a]) / resolution);
+    }
+    for (int a = 0; a < 3; ++a)
+        if (grid.n[a] < 2 || grid.n[a] > 4096) return FKS_ERR_INVALID_ARGUMENT;
+    inverse34(grid.origin, grid.inv_origin);
+
+    fks_env_handle* env = new (std::nothrow) fks_env_handle();
+    if (!env) return FKS_ERR_OUT_OF_MEMORY;
+    try {
+        const size_t total = grid.cells();
+        env->occupancy.assign(total, 0);
+        for (size_t c = 0; c < cell_ids.size(); ++c) {
+            int64_t idx[3];
+            if (grid.index(&cells[3 * c], idx)) env->occupancy[grid.linear(idx[0], idx[1], idx[2])] = 1;
+        }
+        /* signed distance field: + distance to the nearest filled cell for free cells,
+         * - distance to the nearest free cell for filled cells (sdf_tools convention) */
+        std::vector<uint8_t> free_seed(total);
+        for (size_t c = 0; c < total; ++c) free_seed[c] = env->occupancy[c] ? 0 : 1;
+        const std::vector<double> to_filled = edt_3d(env->occupancy, grid.n);
+        const std::vector<double> to_free = edt_3d(free_seed, grid.n);
+        env->sdf.resize(total);
+        for (size_t c = 0; c < total; ++c) {
+            const double filled_distance = fks_math::dsqrt(to_filled[c]) * resolution;
+            const double free_distance = fks_math::dsqrt(to_free[c]) * resolution;
+            env->sdf[c] = (float)(filled_distance - free_distance);
+        }
+        auto sdf_at = [&](int64_t i, int64_t j, int64_t k) { return env->sdf[grid.linear(i, j, k)]; };
+        /* pass 2 first into a map (last write wins); pass 1 fills the rest */
+        std::unordered_map<size_t, std::vector<Entry>> surface;
+        for (int32_t o = 0; o < num_obstacles; ++o) {
+            const fks_obstacle& ob = obstacles[o];
+            int32_t nc[3];
+            for (int a = 0; a < 3; ++a) nc[a] = (int32_t)(ob.extents[a] * 2.0 * (1.0 / effective_resolution));
+            for (int32_t xi = 0; xi < nc[0]; ++xi)
+                for (int32_t yi = 0; yi < nc[1]; ++yi)
+                    for (int32_t zi = 0; zi < nc[2]; ++zi) {
+                        const int32_t id3[3] = {xi, yi, zi};
+                        bool boundary = false;
+                        for (int a = 0; a < 3; ++a) boundary = boundary || id3[a] == 0 || id3[a] == nc[a] - 1;
+                        if (!boundary) continue;
+                        const double local[3] = {-(ob.extents[0] - effective_resolution) + (effective_resolution * xi),
+                                                 -(ob.extents[1] - effective_resolution) + (effective_resolution * yi),
+                                                 -(ob.extents[2] - effective_resolution) + (effective_resolution * zi)};
+                        double w[3];
+                        xform3(ob.pose, local, w);
+                        int64_t idx[3];
+                        /* UpdateSurfaceNormalGridCell SEB.cpp:162-187 */
+                        if (!grid.index(w, idx)) continue; /* GetImmutable3d OOB = +inf, then insert fails */
+                        const float distance = sdf_at(idx[0], idx[1], idx[2]);
+                        if (!((double)distance > -(resolution * 1.5))) continue;
+                        std::vector<Entry> list;
+                        for (int a = 0; a < 3; ++a) {
+                            double normal[3] = {0, 0, 0}, entry[3] = {0, 0, 0};
+                            if (id3[a] == 0) {
+                                normal[a] = -1.0;
+                                entry[a] = 1.0;
+                            } else if (id3[a] == nc[a] - 1) {
+                                normal[a] = 1.0;
+                                entry[a] = -1.0;
+                            } else {
+                                continue;
+                            }
+                            double rn[3], re[3];
+                            rotate3(ob.pose, normal, rn);
+                            rotate3(ob.pose, entry, re);
+                            /* StoredSurfaceNormal: SafeNormal(normal), SafeNormal((entry, 0)) */
+                            Entry E;
+                            const double en = fks_math::dsqrt(((re[0] * re[0] + re[1] * re[1]) + re[2] * re[2]) + 0.0 * 0.0);
+                            for (int b = 0; b < 3; ++b) E.e[b] = (en > 2.220446049250313e-16) ? re[b] / en : re[b];
+                            const double nn = fks_math::dsqrt((rn[0] * rn[0] + rn[1] * rn[1]) + rn[2] * rn[2]);
+                            for (int b = 0; b < 3; ++b) E.e[3 + b] = (nn > 2.220446049250313e-16) ? rn[b] / nn : rn[b];
+                            list.push_back(E);
+                        }
+                        surface[grid.linear(idx[0], idx[1], idx[2])] = list;
+                    }
+        }
+        env->offsets.assign(total + 1, 0);
+        uint64_t count = 0;
+        for (int64_t i = 0; i < grid.n[0]; ++i)
+            for (int64_t j = 0; j < grid.n[1]; ++j)
+                for (int64_t k = 0; k < grid.n[2]; ++k) {
+                    const size_t c = grid.linear(i, j, k);
+                    env->offsets[c] = (uint32_t)count;
+                    const auto it = surface.find(c);
+                    if (it != surface.end()) {
+                        for (const Entry& E : it->second) env->entries.insert(env->entries.end(), E.e, E.e + 6);
+                        count += it->second.size();
+                    } else if (env->sdf[c] < 0.0f) {
+                        /* pass 1 (SEB.cpp:263-277): SDF gradient (edge gradients enabled), entry 0 */
+                        const int64_t id3[3] = {i, j, k};
+                        double g[3];
+                        for (int a = 0; a < 3; ++a) {
+                            int64_t lo[3] = {i, j, k}, hi[3] = {i, j, k};
+                            lo[a] = (id3[a] - 1 > 0) ? id3[a] - 1 : 0;
+                            hi[a] = (id3[a] + 1 < grid.n[a] - 1) ? id3[a] + 1 : grid.n[a] - 1;
+                            const double inv = 1.0 / (resolution * (double)(hi[a] - lo[a]));
+                            const float diff = sdf_at(hi[0], hi[1], hi[2]) - sdf_at(lo[0], lo[1], lo[2]);
+                            g[a] = (double)diff * inv;
+                        }
+                        const double gn = fks_math::dsqrt((g[0] * g[0] + g[1] * g[1]) + g[2] * g[2]);
+                        Entry E;
+                        for (int b = 0; b < 3; ++b) E.e[b] = 0.0;
+                        for (int b = 0; b < 3; ++b) E.e[3 + b] = (gn > 2.220446049250313e-16) ? g[b] / gn : g[b];
+                        env->entries.insert(env->entries.end(), E.e, E.e + 6);
+                        count += 1;
+                    }
+                    if (count > 0xffffffffull) throw std::bad_alloc();
+                }
+        env->offsets[total] = (uint32_t)count;
+    } catch (const std::bad_alloc&) {
+        delete env;
+        return FKS_ERR_OUT_OF_MEMORY;
+    }
+    std::memcpy(env->geometry.origin, grid.origin, sizeof(grid.origin));
+    env->geometry.resolution = resolution;
+    for (int a = 0; a < 3; ++a) env->geometry.num_cells[a] = grid.n[a];
+    *out = env;
+    return FKS_OK;
+}
+
+extern "C" fks_status fks_env_view(const fks_env_handle* env, fks_environment* out) {
+    if (!env || !out) return FKS_ERR_INVALID_ARGUMENT;
+    std::memset(out, 0, sizeof(*out));
+    out->collision_map = env->geometry;
+    out->sdf = env->geometry;
+    out->normals = env->geometry;
+    out->sdf_values = env->sdf.data();
+    out->sdf_oob_value = std::numeric_limits<float>::infinity();
+    out->normal_offsets = env->offsets.data();
+    out->normal_entries = env->entries.data();
+    return FKS_OK;
+}
+
+extern "C" void fks_env_free(fks_env_handle* env) { delete env; }

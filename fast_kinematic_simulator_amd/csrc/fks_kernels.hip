@@ -1,0 +1,1549 @@
+/*
+ * fks_kernels.hip — the particle forward-simulation hot path on CDNA4 (gfx950).
+ *
+ * One 64-lane wavefront simulates one particle at a time (workgroup = 1 wave,
+ * persistent grid, atomic particle queue for load balance across contact-heavy
+ * and free particles).  Inside a wave:
+ *   - DOF lanes (lane d < D): PID state, actuator clamp, truncated-normal
+ *     actuation noise (Philox4x32-10 counter RNG), joint-limit enforcement
+ *     (TNUVA:538-614, PID:122-135, UNC:70-90);
+ *   - FK: lane j < J builds joint j's motion matrix; the chain
+ *     T_child = (T_parent * origin_j) * motion_j is composed by 12 lanes, one
+ *     3x4 element each, link transforms kept in LDS (UpdateTransforms of the
+ *     arc_utilities linked model);
+ *   - link points are lane-strided (point i -> lane i % 64) for the SDF
+ *     collision check (SPCS:921-981), workspace-motion maxima (SPCS:1492-1544),
+ *     the per-point Jacobians / corrections (SPCS:1818-1939);
+ *   - the stacked least-squares solve (Eigen ColPivHouseholderQR, SPCS:1990-1998)
+ *     keeps rows lane-strided and reduces with a 64-lane xor butterfly — the
+ *     canonical summation order the CPU oracle reproduces bit for bit;
+ *   - self-collision (SPCS:1183-1275): per-geometry conservative cell-key boxes
+ *     (one lane per geometry) reject disallowed pairs; only overlapping pairs run
+ *     the exact key comparison, and true self-contacts run the impulse solve
+ *     (SPCS:983-1171) on one lane.
+ * All double arithmetic is IEEE (no contraction: built with -ffp-contract=off),
+ * transcendentals come from include/fks_portable_math.h, so results are
+ * bit-identical to the CPU oracle on the same inputs.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fks_capi.h"
+#include "fks_device.h"
+#include "fks_portable_math.h"
+
+namespace fksd {
+
+using fks_math::clamp;
+using fks_math::dabs;
+using fks_math::dmax;
+using fks_math::dmin;
+using fks_math::dsqrt;
+
+struct D3 {
+    double x, y, z;
+};
+struct D4 {
+    double x, y, z, w;
+};
+
+/* ---------------- geometry (same evaluation order as oracle_geometry.h) ---------------- */
+__device__ __forceinline__ double dot3(double a0, double a1, double a2, double b0, double b1, double b2) {
+    return (a0 * b0 + a1 * b1) + a2 * b2;
+}
+__device__ __forceinline__ D4 xform4(const double* T, const D4& p) {
+    D4 o;
+    o.x = dot3(T[0], T[1], T[2], p.x, p.y, p.z) + T[3] * p.w;
+    o.y = dot3(T[4], T[5], T[6], p.x, p.y, p.z) + T[7] * p.w;
+    o.z = dot3(T[8], T[9], T[10], p.x, p.y, p.z) + T[11] * p.w;
+    o.w = p.w;
+    return o;
+}
+__device__ __forceinline__ D3 xform3(const double* T, const D3& p) {
+    D3 o;
+    o.x = dot3(T[0], T[1], T[2], p.x, p.y, p.z) + T[3];
+    o.y = dot3(T[4], T[5], T[6], p.x, p.y, p.z) + T[7];
+    o.z = dot3(T[8], T[9], T[10], p.x, p.y, p.z) + T[11];
+    return o;
+}
+__device__ __forceinline__ D3 rotate(const double* T, const D3& v) {
+    D3 o;
+    o.x = dot3(T[0], T[1], T[2], v.x, v.y, v.z);
+    o.y = dot3(T[4], T[5], T[6], v.x, v.y, v.z);
+    o.z = dot3(T[8], T[9], T[10], v.x, v.y, v.z);
+    return o;
+}
+__device__ __forceinline__ D3 cross(const D3& a, const D3& b) {
+    D3 c;
+    c.x = a.y * b.z - a.z * b.y;
+    c.y = a.z * b.x - a.x * b.z;
+    c.z = a.x * b.y - a.y * b.x;
+    return c;
+}
+__device__ __forceinline__ double sqnorm4(const D4& v) { return ((v.x * v.x + v.y * v.y) + v.z * v.z) + v.w * v.w; }
+__device__ __forceinline__ double sqnorm3(const D3& v) { return (v.x * v.x + v.y * v.y) + v.z * v.z; }
+__device__ __forceinline__ D4 safe_normal4(const D4& v) {
+    const double n = dsqrt(sqnorm4(v));
+    if (n > 2.220446049250313e-16) return D4{v.x / n, v.y / n, v.z / n, v.w / n};
+    return v;
+}
+__device__ __forceinline__ D3 safe_normal3(const D3& v) {
+    const double n = dsqrt(sqnorm3(v));
+    if (n > 2.220446049250313e-16) return D3{v.x / n, v.y / n, v.z / n};
+    return v;
+}
+/* Eigen::AngleAxisd::toRotationMatrix into a 3x4 (translation untouched) */
+__device__ __forceinline__ void angle_axis34(double angle, double a0, double a1, double a2, double* M) {
+    const double s = fks_math::sin(angle);
+    const double c = fks_math::cos(angle);
+    const double sa0 = s * a0, sa1 = s * a1, sa2 = s * a2;
+    const double omc = 1.0 - c;
+    const double c1a0 = omc * a0, c1a1 = omc * a1, c1a2 = omc * a2;
+    double tmp = c1a0 * a1;
+    M[1] = tmp - sa2;
+    M[4] = tmp + sa2;
+    tmp = c1a0 * a2;
+    M[2] = tmp + sa1;
+    M[8] = tmp - sa1;
+    tmp = c1a1 * a2;
+    M[6] = tmp - sa0;
+    M[9] = tmp + sa0;
+    M[0] = c1a0 * a0 + c;
+    M[5] = c1a1 * a1 + c;
+    M[10] = c1a2 * a2 + c;
+}
+
+/* SE(3) exp/log of body twists: same closed forms as oracle_geometry.h */
+__device__ void se3_coeffs(double theta, double* A, double* B, double* C) {
+    if (theta < 1e-3) {
+        const double t2 = theta * theta;
+        *A = 1.0 - t2 / 6.0 + (t2 * t2) / 120.0;
+        *B = 0.5 - t2 / 24.0 + (t2 * t2) / 720.0;
+        *C = 1.0 / 6.0 - t2 / 120.0 + (t2 * t2) / 5040.0;
+    } else {
+        const double s = fks_math::sin(theta);
+        const double sh = fks_math::sin(0.5 * theta);
+        *A = s / theta;
+        *B = (2.0 * (sh * sh)) / (theta * theta);
+        *C = (theta - s) / ((theta * theta) * theta);
+    }
+}
+__device__ void exp_twist34(const double* tw, double* M) {
+    const D3 v{tw[0], tw[1], tw[2]};
+    const D3 w{tw[3], tw[4], tw[5]};
+    const double theta = dsqrt(sqnorm3(w));
+    double A, B, C;
+    se3_coeffs(theta, &A, &B, &C);
+    const double wv[3] = {w.x, w.y, w.z};
+    const double th2 = (w.x * w.x + w.y * w.y) + w.z * w.z;
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) {
+            double Wij = 0.0;
+            if (i == 0 && j == 1) Wij = -w.z;
+            if (i == 0 && j == 2) Wij = w.y;
+            if (i == 1 && j == 0) Wij = w.z;
+            if (i == 1 && j == 2) Wij = -w.x;
+            if (i == 2 && j == 0) Wij = -w.y;
+            if (i == 2 && j == 1) Wij = w.x;
+            const double W2ij = wv[i] * wv[j] - ((i == j) ? th2 : 0.0);
+            M[4 * i + j] = ((i == j) ? 1.0 : 0.0) + A * Wij + B * W2ij;
+        }
+    }
+    const D3 Wv = cross(w, v);
+    const D3 WWv = cross(w, Wv);
+    M[3] = (v.x + B * Wv.x) + C * WWv.x;
+    M[7] = (v.y + B * Wv.y) + C * WWv.y;
+    M[11] = (v.z + B * Wv.z) + C * WWv.z;
+}
+__device__ void log_twist34(const double* T, double* tw) {
+    const double R0 = T[0], R1 = T[1], R2 = T[2], R3 = T[4], R4 = T[5], R5 = T[6], R6 = T[8], R7 = T[9], R8 = T[10];
+    const double cos_arg = (((R0 + R4) + R8) - 1.0) * 0.5;
+    const D3 vee{(R7 - R5) * 0.5, (R2 - R6) * 0.5, (R3 - R1) * 0.5};
+    const double s = dsqrt(sqnorm3(vee));
+    const double theta = fks_math::atan2(s, cos_arg);
+    D3 w;
+    if (theta < 1e-3) {
+        const double f = 1.0 + (theta * theta) / 6.0;
+        w = D3{vee.x * f, vee.y * f, vee.z * f};
+    } else if (s < 1e-6 && cos_arg < 0.0) {
+        const double Rm[9] = {R0, R1, R2, R3, R4, R5, R6, R7, R8};
+        int k = 0;
+        if (Rm[4] > Rm[0]) k = 1;
+        if (Rm[8] > Rm[k * 4]) k = 2;
+        double ax[3];
+        ax[k] = dsqrt((Rm[k * 4] + 1.0) * 0.5);
+        for (int i = 0; i < 3; ++i)
+            if (i != k) ax[i] = (Rm[i * 3 + k] + Rm[k * 3 + i]) / (4.0 * ax[k]);
+        w = D3{ax[0] * theta, ax[1] * theta, ax[2] * theta};
+    } else {
+        const double f = theta / s;
+        w = D3{vee.x * f, vee.y * f, vee.z * f};
+    }
+    const double th = dsqrt(sqnorm3(w));
+    double A, B, C;
+    se3_coeffs(th, &A, &B, &C);
+    double D;
+    if (th < 1e-3) {
+        const double t2 = th * th;
+        D = 1.0 / 12.0 + t2 / 720.0;
+    } else {
+        D = (1.0 - A / (2.0 * B)) / (th * th);
+    }
+    const D3 t{T[3], T[7], T[11]};
+    const D3 Wt = cross(w, t);
+    const D3 WWt = cross(w, Wt);
+    tw[0] = (t.x - 0.5 * Wt.x) + D * WWt.x;
+    tw[1] = (t.y - 0.5 * Wt.y) + D * WWt.y;
+    tw[2] = (t.z - 0.5 * Wt.z) + D * WWt.z;
+    tw[3] = w.x;
+    tw[4] = w.y;
+    tw[5] = w.z;
+}
+/* C = A * B (3x4 row-major), Eigen Transform product order */
+__device__ __forceinline__ void compose34(const double* A, const double* B, double* C) {
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j)
+            C[4 * i + j] = dot3(A[4 * i + 0], A[4 * i + 1], A[4 * i + 2], B[j], B[4 + j], B[8 + j]);
+        C[4 * i + 3] = dot3(A[4 * i + 0], A[4 * i + 1], A[4 * i + 2], B[3], B[7], B[11]) + A[4 * i + 3];
+    }
+}
+__device__ __forceinline__ void inverse34(const double* T, double* I) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) I[4 * i + j] = T[4 * j + i];
+    for (int i = 0; i < 3; ++i) I[4 * i + 3] = -dot3(I[4 * i + 0], I[4 * i + 1], I[4 * i + 2], T[3], T[7], T[11]);
+}
+
+/* ---------------- wave primitives ---------------- */
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63u); }
+/* canonical 64-lane sum: xor butterfly over 32,16,8,4,2,1 (oracle canon_sum) */
+__device__ __forceinline__ double bfly_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_max_nonneg(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double o = __shfl_xor(v, off, 64);
+        v = (o > v) ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v |= (uint32_t)__shfl_xor((int)v, off, 64);
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += (uint64_t)__shfl_xor((long long)v, off, 64);
+    return v;
+}
+__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
+__device__ __forceinline__ void wsync() { __syncthreads(); }
+
+/* ---------------- RNG (same spec as oracle_rng.h) ---------------- */
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(M0, c[0]), lo0 = M0 * c[0];
+        const uint32_t hi1 = __umulhi(M1, c[2]), lo1 = M1 * c[2];
+        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0;
+        c[1] = lo1;
+        c[2] = n2;
+        c[3] = lo0;
+        k0 += W0;
+        k1 += W1;
+    }
+}
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+    const uint64_t bits = (((uint64_t)a << 32) | (uint64_t)b) >> 11;
+    return (double)bits * (1.0 / 9007199254740992.0);
+}
+/* truncated normal TN(0, 0.5) on [-1, 1]: TYPE_1 accept-reject over polar normals */
+__device__ double tn_sample(uint32_t k0, uint32_t k1, uint64_t particle, uint32_t step, uint32_t micro, uint32_t dof,
+                            uint32_t* err) {
+    const double mean = 0.0, stddev = 0.5, lo = -2.0, hi = 2.0;
+    for (uint32_t attempt = 0; attempt < 64; ++attempt) {
+        uint32_t c[4] = {(uint32_t)particle, step, micro,
+                         ((uint32_t)(particle >> 32) << 16) | ((dof & 0xffu) << 8) | attempt};
+        philox4x32_10(c, k0, k1);
+        const double x = 2.0 * u53(c[0], c[1]) - 1.0;
+        const double y = 2.0 * u53(c[2], c[3]) - 1.0;
+        const double r2 = x * x + y * y;
+        if (r2 > 1.0 || r2 == 0.0) continue;
+        const double mult = dsqrt(-2.0 * fks_math::log(r2) / r2);
+        const double n1 = (y * mult) * 1.0 + 0.0;
+        const double n2 = (x * mult) * 1.0 + 0.0;
+        if ((n1 <= hi) && (n1 >= lo)) return mean + stddev * n1;
+        if ((n2 <= hi) && (n2 >= lo)) return mean + stddev * n2;
+    }
+    *err |= FKS_PARTICLE_ERR_RNG_EXHAUSTED;
+    return 0.0;
+}
+
+/* ---------------- grids ---------------- */
+/* VoxelGrid LocationToGridIndex4d + IndexInBounds: trunc toward zero of
+ * (inverse_origin * p) * (1/res); indices beyond int32 are out of bounds anyway */
+__device__ __forceinline__ bool grid_index(const GridDev& g, const D4& p, int32_t idx[3]) {
+    const D4 q = xform4(g.inv, p);
+    const double v[3] = {q.x * g.inv_res, q.y * g.inv_res, q.z * g.inv_res};
+    bool ok = true;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const bool fin = (v[a] > -2147483648.0) && (v[a] < 2147483647.0);
+        idx[a] = fin ? (int32_t)v[a] : -1;
+        ok = ok && fin && idx[a] >= 0 && (int64_t)idx[a] < g.n[a];
+    }
+    return ok;
+}
+__device__ __forceinline__ uint32_t grid_linear(const GridDev& g, int32_t i, int32_t j, int32_t k) {
+    return ((uint32_t)i * (uint32_t)g.n[1] + (uint32_t)j) * (uint32_t)g.n[2] + (uint32_t)k;
+}
+
+struct Sim {
+    const SimArgs* A;
+    double* lds;
+    int32_t* ldsi;
+    LdsLayout L;
+    double* scratch;
+    int lane;
+    uint64_t pid;
+    uint32_t step;
+    uint32_t err;          /* per-lane error bits, OR-reduced at decision points */
+    uint64_t lane_bytes;   /* per-lane algorithmic SDF bytes */
+    uint64_t micro_count, resolver_count, step_count;
+    uint32_t stats[8];
+    double pid_integral, pid_last; /* DOF lanes */
+    bool self_nonempty;
+};
+
+/* sdf_tools EstimateDistance4d (same spec as oracle SDF::EstimateDistance4d) */
+__device__ double estimate_distance(const SimArgs& A, const D4& p, bool* inb, uint64_t* bytes) {
+    int32_t idx[3];
+    if (!grid_index(A.sdf_g, p, idx)) {
+        *inb = false;
+        return (double)A.oob;
+    }
+    *inb = true;
+    *bytes += 28;
+    const GridDev& g = A.sdf_g;
+    double grad[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        int32_t lo[3] = {idx[0], idx[1], idx[2]}, hi[3] = {idx[0], idx[1], idx[2]};
+        lo[a] = (idx[a] - 1 > 0) ? idx[a] - 1 : 0;
+        hi[a] = ((int64_t)idx[a] + 1 < g.n[a] - 1) ? idx[a] + 1 : (int32_t)(g.n[a] - 1);
+        const double inv = 1.0 / (g.res * (double)(hi[a] - lo[a]));
+        const float diff = A.sdf[grid_linear(g, hi[0], hi[1], hi[2])] - A.sdf[grid_linear(g, lo[0], lo[1], lo[2])];
+        grad[a] = (double)diff * inv;
+    }
+    const D3 c = xform3(g.org, D3{g.res * ((double)idx[0] + 0.5), g.res * ((double)idx[1] + 0.5), g.res * ((double)idx[2] + 0.5)});
+    const double dx = p.x - c.x, dy = p.y - c.y, dz = p.z - c.z;
+    const double nominal = (double)A.sdf[grid_linear(g, idx[0], idx[1], idx[2])];
+    const double corrected = (nominal >= 0.0) ? nominal - (g.res * 0.5) : nominal + (g.res * 0.5);
+    const double adjustment = (dx * grad[0] + dy * grad[1]) + dz * grad[2];
+    const double estimate = corrected + adjustment;
+    if ((corrected >= 0.0) == (estimate >= 0.0)) return estimate;
+    if (corrected >= 0.0) return g.res * 0.0625;
+    return g.res * -0.0625;
+}
+
+/* SurfaceNormalGrid::LookupSurfaceNormal(Vector4d, Vector4d) + GetBestSurfaceNormal */
+__device__ bool lookup_normal(const SimArgs& A, const D4& loc, const D4& dir, D3* out, uint32_t* err, uint64_t* bytes) {
+    *out = D3{0.0, 0.0, 0.0};
+    int32_t idx[3];
+    if (!A.has_normals || !grid_index(A.nrm_g, loc, idx)) return false;
+    const uint32_t lin = grid_linear(A.nrm_g, idx[0], idx[1], idx[2]);
+    const uint32_t begin = A.noff[lin], end = A.noff[lin + 1];
+    *bytes += 8;
+    if (begin == end) return true;
+    *bytes += 48ull * (uint64_t)(end - begin);
+    const double direction_norm = dsqrt(sqnorm4(dir));
+    if (!(direction_norm > 0.0)) {
+        *err |= FKS_PARTICLE_ERR_ZERO_DIRECTION;
+        return true;
+    }
+    const double ux = dir.x / direction_norm, uy = dir.y / direction_norm, uz = dir.z / direction_norm;
+    int64_t best = -1;
+    double best_dot = -__builtin_huge_val();
+    for (uint32_t e = begin; e < end; ++e) {
+        const double* ent = A.nent + 6ull * e;
+        const double dot = (ent[0] * ux + ent[1] * uy) + ent[2] * uz;
+        if (dot > best_dot) {
+            best_dot = dot;
+            best = (int64_t)e;
+        }
+    }
+    if (best < 0) {
+        *err |= FKS_PARTICLE_ERR_ZERO_DIRECTION;
+        return true;
+    }
+    const double* ent = A.nent + 6ull * (uint64_t)best;
+    *out = D3{ent[3], ent[4], ent[5]};
+    return true;
+}
+
+__device__ __forceinline__ D4 load_point(const RobotDev& R, int i) {
+    const double2* p2 = reinterpret_cast<const double2*>(R.points + 4ull * (uint64_t)i);
+    const double2 a = p2[0], b = p2[1];
+    return D4{a.x, a.y, b.x, b.y};
+}
+
+/* ---------------- forward kinematics: cfg (LDS) -> link transforms T (LDS) ---------------- */
+__device__ void fk(Sim& s, const double* cfg, double* T) {
+    const RobotDev& R = s.A->R;
+    const int ln = s.lane;
+    if (R.type == FKS_ROBOT_LINKED) {
+        double* jm = s.lds + s.L.jm;
+        if (ln < R.J) {
+            const JointDev& jd = R.joints[ln];
+            if (jd.type == FKS_JOINT_REVOLUTE || jd.type == FKS_JOINT_CONTINUOUS) {
+                double M[12];
+                angle_axis34(cfg[jd.dof], jd.axis[0], jd.axis[1], jd.axis[2], M);
+                M[3] = 0.0;
+                M[7] = 0.0;
+                M[11] = 0.0;
+                for (int e = 0; e < 12; ++e) jm[12 * ln + e] = M[e];
+            } else if (jd.type == FKS_JOINT_PRISMATIC) {
+                const double v = cfg[jd.dof];
+                const double M[12] = {1.0, 0.0, 0.0, jd.axis[0] * v, 0.0, 1.0, 0.0, jd.axis[1] * v, 0.0, 0.0, 1.0, jd.axis[2] * v};
+                for (int e = 0; e < 12; ++e) jm[12 * ln + e] = M[e];
+            }
+        }
+        if (ln < 12) T[ln] = R.base[ln];
+        wsync();
+        const int r = ln >> 2, c = ln & 3;
+        for (int j = 0; j < R.J; ++j) {
+            const JointDev& jd = R.joints[j];
+            const int parent = jd.parent, child = jd.child, type = jd.type;
+            double Ae = 0.0;
+            if (ln < 12) {
+                const double* Tp = T + 12 * parent;
+                const double* O = jd.origin;
+                if (c < 3)
+                    Ae = dot3(Tp[4 * r], Tp[4 * r + 1], Tp[4 * r + 2], O[c], O[4 + c], O[8 + c]);
+                else
+                    Ae = dot3(Tp[4 * r], Tp[4 * r + 1], Tp[4 * r + 2], O[3], O[7], O[11]) + Tp[4 * r + 3];
+            }
+            const int rb = ln & ~3;
+            const double a0 = __shfl(Ae, rb + 0, 64), a1 = __shfl(Ae, rb + 1, 64), a2 = __shfl(Ae, rb + 2, 64),
+                         a3 = __shfl(Ae, rb + 3, 64);
+            if (ln < 12) {
+                double out;
+                if (type == FKS_JOINT_FIXED) {
+                    out = Ae;
+                } else {
+                    const double* M = jm + 12 * j;
+                    if (c < 3)
+                        out = dot3(a0, a1, a2, M[c], M[4 + c], M[8 + c]);
+                    else
+                        out = dot3(a0, a1, a2, M[3], M[7], M[11]) + a3;
+                }
+                T[12 * child + ln] = out;
+            }
+            wsync();
+        }
+    } else if (R.type == FKS_ROBOT_SE2) {
+        double M[12];
+        angle_axis34(cfg[2], 0.0, 0.0, 1.0, M);
+        M[3] = cfg[0];
+        M[7] = cfg[1];
+        M[11] = 0.0;
+        if (ln < 12) T[ln] = M[ln];
+        wsync();
+    } else {
+        if (ln < 12) T[ln] = cfg[ln];
+        wsync();
+    }
+}
+
+/* ---------------- robot control-input application (TNUVA ApplyControlInput) ----------------
+ * cfg_out = apply(cfg_in, input) with clamp (+ noise if noisy).  Lane d < D owns dof d. */
+__device__ void apply_input(Sim& s, const double* cfg_in, const double* input, double* cfg_out, bool noisy, uint32_t micro) {
+    const SimArgs& A = *s.A;
+    const RobotDev& R = A.R;
+    const int ln = s.lane;
+    if (R.type == FKS_ROBOT_LINKED) {
+        if (ln < R.D) {
+            const fks_dof_controller& ct = R.ctrl[ln];
+            const double vmax = dabs(ct.velocity_limit);
+            double real = clamp(input[ln], -vmax, vmax);
+            if (noisy) {
+                const double prop = dabs(ct.max_actuator_proportional_noise) * dabs(real);
+                const double floor_noise = dabs(ct.max_actuator_minimum_noise) * vmax;
+                const double bound = dmax(prop, floor_noise);
+                real = real + tn_sample(A.key0, A.key1, s.pid, s.step, micro, (uint32_t)ln, &s.err) * bound;
+            }
+            const JointDev& jd = R.joints[R.dof_joint[ln]];
+            const double raw = cfg_in[ln] + real;
+            double v;
+            if (jd.type == FKS_JOINT_CONTINUOUS) {
+                v = fks_math::enforce_continuous_revolute_bounds(raw);
+                v = fks_math::enforce_continuous_revolute_bounds(v);
+            } else {
+                v = clamp(raw, jd.lo, jd.hi);
+                v = clamp(v, jd.lo, jd.hi);
+            }
+            cfg_out[ln] = v;
+        }
+        wsync();
+    } else if (R.type == FKS_ROBOT_SE2) {
+        if (ln < 3) {
+            const fks_dof_controller& ct = R.ctrl[ln];
+            const double vmax = dabs(ct.velocity_limit);
+            double real = clamp(input[ln], -vmax, vmax);
+            if (noisy) {
+                const double prop = dabs(ct.max_actuator_proportional_noise) * dabs(real);
+                const double floor_noise = dabs(ct.max_actuator_minimum_noise) * vmax;
+                const double bound = dmax(prop, floor_noise);
+                real = real + tn_sample(A.key0, A.key1, s.pid, s.step, micro, (uint32_t)ln, &s.err) * bound;
+            }
+            double v = cfg_in[ln] + real;
+            if (ln == 2) v = fks_math::enforce_continuous_revolute_bounds(v);
+            cfg_out[ln] = v;
+        }
+        wsync();
+    } else {
+        double* tw = s.lds + s.L.misc; /* 6 doubles */
+        if (ln < 6) {
+            const fks_dof_controller& ct = R.ctrl[ln];
+            const double vmax = dabs(ct.velocity_limit);
+            double real = clamp(input[ln], -vmax, vmax);
+            if (noisy) {
+                const double prop = dabs(ct.max_actuator_proportional_noise) * dabs(real);
+                const double floor_noise = dabs(ct.max_actuator_minimum_noise) * vmax;
+                const double bound = dmax(prop, floor_noise);
+                real = real + tn_sample(A.key0, A.key1, s.pid, s.step, micro, (uint32_t)ln, &s.err) * bound;
+            }
+            tw[ln] = real;
+        }
+        wsync();
+        double M[12], twr[6], P[12];
+        for (int k = 0; k < 6; ++k) twr[k] = tw[k];
+        for (int k = 0; k < 12; ++k) P[k] = cfg_in[k];
+        exp_twist34(twr, M);
+        double C[12];
+        compose34(P, M, C);
+        wsync();
+        if (ln < 12) cfg_out[ln] = C[ln];
+        wsync();
+    }
+}
+
+/* GenerateControlAction (TNUVA:179-198, 384-412, 598-614): lane d < D returns u_d */
+__device__ double control_action(Sim& s, const double* cfg, const double* target) {
+    const SimArgs& A = *s.A;
+    const RobotDev& R = A.R;
+    const int ln = s.lane;
+    double err = 0.0;
+    if (R.type == FKS_ROBOT_LINKED) {
+        if (ln < R.D) {
+            const JointDev& jd = R.joints[R.dof_joint[ln]];
+            if (jd.type == FKS_JOINT_CONTINUOUS)
+                err = fks_math::enforce_continuous_revolute_bounds(target[ln] - cfg[ln]);
+            else
+                err = target[ln] - cfg[ln];
+        }
+    } else if (R.type == FKS_ROBOT_SE2) {
+        if (ln < 2) err = target[ln] - cfg[ln];
+        if (ln == 2) err = fks_math::enforce_continuous_revolute_bounds(target[2] - cfg[2]);
+    } else {
+        double P[12], Pi[12], Tg[12], Dm[12], tw[6];
+        for (int k = 0; k < 12; ++k) {
+            P[k] = cfg[k];
+            Tg[k] = target[k];
+        }
+        inverse34(P, Pi);
+        compose34(Pi, Tg, Dm);
+        log_twist34(Dm, tw);
+        double e = tw[0];
+        for (int k = 1; k < 6; ++k)
+            if (ln == k) e = tw[k];
+        if (ln < 6) err = e;
+    }
+    double u = 0.0;
+    if (ln < R.D) {
+        const fks_dof_controller& ct = R.ctrl[ln];
+        /* SimplePIDController::ComputeFeedbackTerm (PID:122-135), gains made positive (PID:104-113) */
+        const double kp = dabs(ct.kp), ki = dabs(ct.ki), kd = dabs(ct.kd), iclamp = dabs(ct.integral_clamp);
+        const double timestep = A.dt;
+        const double timestep_error_integral = ((err * 0.5) + (s.pid_last * 0.5)) * timestep;
+        const double new_error_integral = s.pid_integral + timestep_error_integral;
+        s.pid_integral = dmax(-iclamp, dmin(iclamp, new_error_integral));
+        const double error_derivative = (err - s.pid_last) / timestep;
+        s.pid_last = err;
+        const double term = (err * kp) + (s.pid_integral * ki) + (error_derivative * kd);
+        const double vmax = dabs(ct.velocity_limit);
+        u = clamp(term, -vmax, vmax);
+    }
+    return u;
+}
+
+/* configuration distance for the simulation shortcut (SPCS:898) */
+__device__ double config_distance(Sim& s, const double* cfg, const double* target) {
+    const RobotDev& R = s.A->R;
+    if (R.type == FKS_ROBOT_LINKED) {
+        double sum = 0.0;
+        for (int k = 0; k < R.D; ++k) {
+            const JointDev& jd = R.joints[R.dof_joint[k]];
+            const double sd = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(target[k] - cfg[k])
+                                                                : target[k] - cfg[k];
+            const double d = R.weights[k] * dabs(sd);
+            sum = sum + d * d;
+        }
+        return dsqrt(sum);
+    } else if (R.type == FKS_ROBOT_SE2) {
+        const double dx = target[0] - cfg[0];
+        const double dy = target[1] - cfg[1];
+        const double dr = fks_math::enforce_continuous_revolute_bounds(target[2] - cfg[2]);
+        return R.weights[0] * dsqrt(dx * dx + dy * dy) + R.weights[1] * dabs(dr);
+    } else {
+        double P[12], Pi[12], Tg[12], Dm[12], tw[6];
+        for (int k = 0; k < 12; ++k) {
+            P[k] = cfg[k];
+            Tg[k] = target[k];
+        }
+        const double dx = Tg[3] - P[3], dy = Tg[7] - P[7], dz = Tg[11] - P[11];
+        inverse34(P, Pi);
+        compose34(Pi, Tg, Dm);
+        log_twist34(Dm, tw);
+        const double angle = dsqrt((tw[3] * tw[3] + tw[4] * tw[4]) + tw[5] * tw[5]);
+        return R.weights[0] * dsqrt((dx * dx + dy * dy) + dz * dz) + R.weights[1] * angle;
+    }
+}
+
+/* EstimateMaxControlInputWorkspaceMotion over two transform sets (SPCS:1492-1527) */
+__device__ double max_point_motion(Sim& s, const double* TA, const double* TB) {
+    const RobotDev& R = s.A->R;
+    double m = 0.0;
+    for (int i = s.lane; i < R.P; i += kWave) {
+        const D4 p = load_point(R, i);
+        const int link = R.geom_link[R.point_geom[i]];
+        const D4 a = xform4(TA + 12 * link, p), b = xform4(TB + 12 * link, p);
+        const double sq = sqnorm4(D4{b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w});
+        if (sq > m) m = sq;
+    }
+    return dsqrt(wave_max_nonneg(m));
+}
+
+/* CheckEnvironmentCollision (SPCS:921-981) with threshold 0: evaluated one
+ * 64-point round at a time, stopping after the round holding the first colliding
+ * point; algorithmic bytes are counted up to that point, as the reference reads */
+__device__ bool env_collision(Sim& s, const double* T) {
+    const SimArgs& A = *s.A;
+    const RobotDev& R = A.R;
+    const double thr = A.thr_env;
+    const double thr2 = thr - A.sdf_g.res;
+    for (int base = 0; base < R.P; base += kWave) {
+        const int i = base + s.lane;
+        bool col = false;
+        uint64_t b = 0;
+        if (i < R.P) {
+            const D4 p = load_point(R, i);
+            const int link = R.geom_link[R.point_geom[i]];
+            const D4 x = xform4(T + 12 * link, p);
+            int32_t idx[3];
+            float d = A.oob;
+            if (grid_index(A.sdf_g, x, idx)) {
+                d = A.sdf[grid_linear(A.sdf_g, idx[0], idx[1], idx[2])];
+                b += 4;
+            }
+            if ((double)d < thr) {
+                if ((double)d < thr2) {
+                    col = true;
+                } else {
+                    bool inb;
+                    const double est = estimate_distance(A, x, &inb, &b);
+                    if (est < thr) col = true;
+                }
+            }
+        }
+        const uint64_t m = __ballot(col);
+        if (m) {
+            const int first = __ffsll((unsigned long long)m) - 1;
+            if (s.lane <= first) s.lane_bytes += b;
+            return true;
+        }
+        s.lane_bytes += b;
+    }
+    return false;
+}
+
+/* ---------------- self-collision (SPCS:983-1275) ---------------- */
+/* dense helpers on one lane (oracle Dense matmul / Gauss-Jordan inverse) */
+__device__ void dense_matmul(const double* A, int ar, int ac, const double* B, int bc, double* C) {
+    for (int i = 0; i < ar; ++i)
+        for (int j = 0; j < bc; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k < ac; ++k) acc = acc + A[i * ac + k] * B[k * bc + j];
+            C[i * bc + j] = acc;
+        }
+}
+__device__ void dense_transpose(const double* A, int r, int c, double* T) {
+    for (int i = 0; i < r; ++i)
+        for (int j = 0; j < c; ++j) T[j * r + i] = A[i * c + j];
+}
+__device__ void dense_inverse(const double* A, int n, double* aug, double* inv) {
+    const int w = 2 * n;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < w; ++j) aug[i * w + j] = (j < n) ? A[i * n + j] : ((j - n == i) ? 1.0 : 0.0);
+    for (int c = 0; c < n; ++c) {
+        int p = c;
+        double best = dabs(aug[c * w + c]);
+        for (int r = c + 1; r < n; ++r)
+            if (dabs(aug[r * w + c]) > best) {
+                best = dabs(aug[r * w + c]);
+                p = r;
+            }
+        if (p != c)
+            for (int j = 0; j < w; ++j) {
+                const double t = aug[c * w + j];
+                aug[c * w + j] = aug[p * w + j];
+                aug[p * w + j] = t;
+            }
+        const double piv = aug[c * w + c];
+        for (int j = 0; j < w; ++j) aug[c * w + j] = aug[c * w + j] / piv;
+        for (int r = 0; r < n; ++r) {
+            if (r == c) continue;
+            const double f = aug[r * w + c];
+            for (int j = 0; j < w; ++j) aug[r * w + j] = aug[r * w + j] - f * aug[c * w + j];
+        }
+    }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) inv[i * n + j] = aug[i * w + n + j];
+}
+
+/* ExtractSelfCollidingPoints for one cell on lane 0.  members: point indices of
+ * the cell in ascending order.  Writes corrections + flags into scratch; returns
+ * true if the cell is a colliding cell (link_collisions.size() >= 2). */
+__device__ bool extract_cell(Sim& s, const double* Tp, const double* Tc, const int32_t* members, int nm, uint32_t* cells) {
+    const SimArgs& A = *s.A;
+    const RobotDev& R = A.R;
+    const ScratchLayout SL = make_scratch_layout(A.row_cap, R.D, R.P);
+    double* corr = s.scratch + SL.corr;
+    double* flag = s.scratch + SL.flag;
+    double* dense = s.scratch + SL.dense;
+    if (nm <= 1) return false;
+    /* by_link: geometries present (ascending), ranges into members */
+    int geo[kMaxGeoms];
+    int gbeg[kMaxGeoms], gend[kMaxGeoms];
+    int ng = 0;
+    for (int m = 0; m < nm; ++m) {
+        const int g = R.point_geom[members[m]];
+        if (ng == 0 || geo[ng - 1] != g) {
+            if (ng == kMaxGeoms) break;
+            geo[ng] = g;
+            gbeg[ng] = m;
+            ng++;
+        }
+        gend[ng - 1] = m + 1;
+    }
+    if (ng < 2) return false;
+    /* link_collisions: for each present geometry, the present geometries it may not touch */
+    uint64_t present = 0;
+    for (int a = 0; a < ng; ++a) present |= 1ull << geo[a];
+    int ncollide_links = 0;
+    for (int a = 0; a < ng; ++a) {
+        const uint64_t disallowed = present & ~R.allowed_mask[geo[a]] & ~(1ull << geo[a]);
+        if (disallowed) ncollide_links++;
+    }
+    if (ncollide_links < 2) return false;
+    (*cells)++;
+    if (*cells > FKS_MAX_SELF_CELLS || ng > FKS_MAX_SELF_LINKS) {
+        s.err |= FKS_PARTICLE_ERR_SELF_CAPACITY;
+        return true;
+    }
+    const double tm = A.time_multiplier;
+    D4 mom[FKS_MAX_SELF_LINKS];
+    for (int a = 0; a < ng; ++a) {
+        const uint64_t disallowed = present & ~R.allowed_mask[geo[a]] & ~(1ull << geo[a]);
+        mom[a] = D4{0.0, 0.0, 0.0, 0.0};
+        if (!disallowed) continue;
+        const int link = R.geom_link[geo[a]];
+        for (int m = gbeg[a]; m < gend[a]; ++m) {
+            const D4 p = load_point(R, members[m]);
+            const D4 pv = xform4(Tp + 12 * link, p), cv = xform4(Tc + 12 * link, p);
+            const D4 vel{(cv.x - pv.x) * tm, (cv.y - pv.y) * tm, (cv.z - pv.z) * tm, (cv.w - pv.w) * tm};
+            mom[a] = D4{mom[a].x + vel.x, mom[a].y + vel.y, mom[a].z + vel.z, mom[a].w + vel.w};
+        }
+    }
+    for (int a = 0; a < ng; ++a) {
+        const uint64_t disallowed = present & ~R.allowed_mask[geo[a]] & ~(1ull << geo[a]);
+        if (!disallowed) continue;
+        int others[FKS_MAX_SELF_LINKS];
+        int n = 0;
+        for (int b = 0; b < ng; ++b)
+            if ((disallowed >> geo[b]) & 1ull) others[n++] = b;
+        const int link = R.geom_link[geo[a]];
+        const D4 link_loc = xform4(Tp + 12 * link, load_point(R, members[gbeg[a]]));
+        const double cnt = (double)(gend[a] - gbeg[a]);
+        const D4 link_vel{mom[a].x / cnt, mom[a].y / cnt, mom[a].z / cnt, mom[a].w / cnt};
+        const int rows = (n + 1) * 3, ccols = n * 3;
+        double* C = dense;                     /* rows x ccols */
+        double* N = C + rows * ccols;          /* ccols x n */
+        double* M = N + ccols * n;             /* rows x rows */
+        double* V = M + rows * rows;           /* rows */
+        double* Nt = V + rows;                 /* n x ccols */
+        double* Ct = Nt + n * ccols;           /* ccols x rows */
+        double* Minv = Ct + ccols * rows;      /* rows x rows */
+        double* T1 = Minv + rows * rows;       /* work */
+        double* T2 = T1 + rows * rows;
+        double* aug = T2 + rows * rows;
+        for (int k = 0; k < rows * ccols; ++k) C[k] = 0.0;
+        for (int l = 1; l <= n; ++l)
+            for (int d = 0; d < 3; ++d) {
+                C[d * ccols + (l - 1) * 3 + d] = -1.0;
+                C[(l * 3 + d) * ccols + (l - 1) * 3 + d] = 1.0;
+            }
+        for (int k = 0; k < ccols * n; ++k) N[k] = 0.0;
+        for (int c = 0; c < n; ++c) {
+            const int ob = others[c];
+            const int olink = R.geom_link[geo[ob]];
+            const D4 oloc = xform4(Tp + 12 * olink, load_point(R, members[gbeg[ob]]));
+            const D4 cn = safe_normal4(D4{oloc.x - link_loc.x, oloc.y - link_loc.y, oloc.z - link_loc.z, oloc.w - link_loc.w});
+            N[(c * 3 + 0) * n + c] = cn.x;
+            N[(c * 3 + 1) * n + c] = cn.y;
+            N[(c * 3 + 2) * n + c] = cn.z;
+        }
+        for (int k = 0; k < rows * rows; ++k) M[k] = 0.0;
+        const double lm = R.geom_mass[geo[a]];
+        for (int d = 0; d < 3; ++d) M[d * rows + d] = lm;
+        for (int l = 1; l <= n; ++l) {
+            const double om = R.geom_mass[geo[others[l - 1]]];
+            for (int d = 0; d < 3; ++d) M[(l * 3 + d) * rows + (l * 3 + d)] = om;
+        }
+        V[0] = link_vel.x;
+        V[1] = link_vel.y;
+        V[2] = link_vel.z;
+        for (int l = 1; l <= n; ++l) {
+            const int ob = others[l - 1];
+            const double oc = (double)(gend[ob] - gbeg[ob]);
+            V[l * 3 + 0] = mom[ob].x / oc;
+            V[l * 3 + 1] = mom[ob].y / oc;
+            V[l * 3 + 2] = mom[ob].z / oc;
+        }
+        dense_transpose(N, ccols, n, Nt);
+        dense_transpose(C, rows, ccols, Ct);
+        dense_inverse(M, rows, aug, Minv);
+        /* A = Nt*Ct*Minv*C*N (left to right) */
+        dense_matmul(Nt, n, ccols, Ct, rows, T1);     /* n x rows */
+        dense_matmul(T1, n, rows, Minv, rows, T2);    /* n x rows */
+        dense_matmul(T2, n, rows, C, ccols, T1);      /* n x ccols */
+        dense_matmul(T1, n, ccols, N, n, T2);         /* n x n */
+        double* Ainv = T1 + rows * rows;              /* beyond T1 usage: reuse aug tail */
+        Ainv = aug + 2 * rows * rows;
+        dense_inverse(T2, n, aug, Ainv);
+        /* impulses = Ainv*Nt*Ct*V */
+        dense_matmul(Ainv, n, n, Nt, ccols, T1);      /* n x ccols */
+        dense_matmul(T1, n, ccols, Ct, rows, T2);     /* n x rows */
+        double* imp = Ainv + n * n;
+        dense_matmul(T2, n, rows, V, 1, imp);         /* n x 1 */
+        /* dv = (Minv*C*N*imp) * -1 */
+        dense_matmul(Minv, rows, rows, C, ccols, T1); /* rows x ccols */
+        dense_matmul(T1, rows, ccols, N, n, T2);      /* rows x n */
+        double* dv = imp + n;
+        dense_matmul(T2, rows, n, imp, 1, dv);        /* rows x 1 */
+        const D3 corr3{dv[0] * -1.0, dv[1] * -1.0, dv[2] * -1.0};
+        const double np = cnt;
+        for (int m = gbeg[a]; m < gend[a]; ++m) {
+            const D3 pc{corr3.x / np, corr3.y / np, corr3.z / np};
+            if (pc.x != pc.x || pc.y != pc.y || pc.z != pc.z) s.err |= FKS_PARTICLE_ERR_SELF_SINGULAR;
+            const int pi = members[m];
+            corr[3 * pi + 0] = pc.x;
+            corr[3 * pi + 1] = pc.y;
+            corr[3 * pi + 2] = pc.z;
+            flag[pi] = 1.0;
+        }
+    }
+    return true;
+}
+
+/* CollectSelfCollisions: returns whether the self-collision map is non-empty */
+__device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
+    const SimArgs& A = *s.A;
+    const RobotDev& R = A.R;
+    const int ln = s.lane;
+    if (!R.self_possible) return false;
+    double* box = s.lds + s.L.box;
+    bool bad = false;
+    if (ln < R.G) {
+        const double* gb = R.geom_box + 7 * ln;
+        const int link = R.geom_link[ln];
+        const double* T = Tc + 12 * link;
+        double lo[3], hi[3];
+        if (gb[6] != 0.0) {
+            const D3 wc = xform3(T, D3{gb[0], gb[1], gb[2]});
+            double wh[3];
+            for (int i = 0; i < 3; ++i)
+                wh[i] = (dabs(T[4 * i]) * gb[3] + dabs(T[4 * i + 1]) * gb[4]) + dabs(T[4 * i + 2]) * gb[5];
+            const D3 gc = xform3(A.env_g.inv, wc);
+            const double gcv[3] = {gc.x, gc.y, gc.z};
+            for (int i = 0; i < 3; ++i) {
+                const double* Ir = A.env_g.inv + 4 * i;
+                const double gh = (dabs(Ir[0]) * wh[0] + dabs(Ir[1]) * wh[1]) + dabs(Ir[2]) * wh[2];
+                const double margin = 1e-6 + 1e-9 * (dabs(gcv[i]) + gh);
+                const double l = (gcv[i] - gh - margin) / A.env_g.res;
+                const double h = (gcv[i] + gh + margin) / A.env_g.res;
+                if (!(l > -1e18 && l < 1e18 && h > -1e18 && h < 1e18)) bad = true;
+                lo[i] = __builtin_trunc(l);
+                hi[i] = __builtin_trunc(h);
+            }
+        } else {
+            bad = true;
+        }
+        if (bad) {
+            for (int i = 0; i < 3; ++i) {
+                lo[i] = -__builtin_huge_val();
+                hi[i] = __builtin_huge_val();
+            }
+        }
+        for (int i = 0; i < 3; ++i) {
+            box[6 * ln + i] = lo[i];
+            box[6 * ln + 3 + i] = hi[i];
+        }
+    }
+    wsync();
+    bool any = false;
+    for (int k = ln; k < R.npairs; k += kWave) {
+        const int a = R.pairs[2 * k], b = R.pairs[2 * k + 1];
+        bool ov = true;
+        for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
+        any = any || ov;
+    }
+    if (!wave_any(any || bad)) return false;
+
+    /* exact path: extended cell keys of every point (SPCS:1173-1181: division, trunc) */
+    const ScratchLayout SL = make_scratch_layout(A.row_cap, R.D, R.P);
+    int64_t* keys = reinterpret_cast<int64_t*>(s.scratch + SL.keys);
+    double* flag = s.scratch + SL.flag;
+    double* cand = s.scratch + SL.cand;
+    int32_t* list = reinterpret_cast<int32_t*>(s.scratch + SL.list);
+    for (int i = ln; i < R.P; i += kWave) {
+        const D4 p = load_point(R, i);
+        const int link = R.geom_link[R.point_geom[i]];
+        const D4 x = xform4(Tc + 12 * link, p);
+        const D4 g = xform4(A.env_g.inv, x);
+        const double q[3] = {g.x / A.env_g.res, g.y / A.env_g.res, g.z / A.env_g.res};
+        for (int a = 0; a < 3; ++a) {
+            int64_t k;
+            if (q[a] != q[a] || q[a] == __builtin_huge_val() || q[a] == -__builtin_huge_val()) {
+                s.err |= FKS_PARTICLE_ERR_KEY_RANGE;
+                k = 0;
+            } else if (q[a] >= 9.0e18) {
+                k = (int64_t)9000000000000000000ll;
+            } else if (q[a] <= -9.0e18) {
+                k = -(int64_t)9000000000000000000ll;
+            } else {
+                k = (int64_t)q[a];
+            }
+            keys[3 * i + a] = k;
+        }
+        flag[i] = 0.0;
+        cand[i] = 0.0;
+    }
+    wsync();
+    /* exact candidate marking over pairs whose boxes overlap */
+    for (int k = 0; k < R.npairs; ++k) {
+        const int a = R.pairs[2 * k], b = R.pairs[2 * k + 1];
+        bool ov = true;
+        for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
+        if (!ov) continue;
+        const int a0 = (int)R.geom_off[a], a1 = (int)R.geom_off[a + 1];
+        const int b0 = (int)R.geom_off[b], b1 = (int)R.geom_off[b + 1];
+        for (int i = a0 + ln; i < a1; i += kWave) {
+            const int64_t kx = keys[3 * i], ky = keys[3 * i + 1], kz = keys[3 * i + 2];
+            bool hit = false;
+            for (int j = b0; j < b1 && !hit; ++j) hit = (keys[3 * j] == kx) && (keys[3 * j + 1] == ky) && (keys[3 * j + 2] == kz);
+            if (hit) cand[i] = 1.0;
+        }
+    }
+    wsync();
+    /* process each candidate cell once */
+    uint32_t* ui = reinterpret_cast<uint32_t*>(s.ldsi + 2 * kMaxDofs); /* spare int words */
+    if (ln == 0) {
+        ui[0] = 0; /* colliding cells */
+        ui[1] = 0; /* any corrected point */
+    }
+    wsync();
+    for (int base = 0; base < R.P; base += kWave) {
+        const int i0 = base + ln;
+        uint64_t m = __ballot(i0 < R.P && cand[i0] != 0.0);
+        while (m) {
+            const int bit = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1ull;
+            const int ci = base + bit;
+            if (cand[ci] == 0.0) continue; /* already consumed by an earlier cell (uniform read) */
+            const int64_t kx = keys[3 * ci], ky = keys[3 * ci + 1], kz = keys[3 * ci + 2];
+            /* members of the cell in point order */
+            int count = 0;
+            for (int b2 = 0; b2 < R.P; b2 += kWave) {
+                const int j = b2 + ln;
+                const bool in = j < R.P && keys[3 * j] == kx && keys[3 * j + 1] == ky && keys[3 * j + 2] == kz;
+                const uint64_t mm = __ballot(in);
+                if (in) {
+                    const int rank = __popcll(mm & ((1ull << ln) - 1ull));
+                    list[count + rank] = j;
+                    cand[j] = 0.0;
+                }
+                count += __popcll(mm);
+            }
+            wsync();
+            if (ln == 0) {
+                uint32_t cells = ui[0];
+                extract_cell(s, Tp, Tc, list, count, &cells);
+                ui[0] = cells;
+            }
+            wsync();
+        }
+    }
+    bool nonempty = false;
+    for (int i = ln; i < R.P; i += kWave) nonempty = nonempty || (flag[i] != 0.0);
+    s.err = wave_or(s.err);
+    return wave_any(nonempty);
+}
+
+/* CheckCollision (SPCS:1418-1436) */
+__device__ bool check_collision(Sim& s, const double* Tp, const double* Tc) {
+    const bool env = env_collision(s, Tc);
+    const bool self = self_collisions(s, Tp, Tc);
+    s.self_nonempty = self;
+    return env || self;
+}
+
+/* world joint axes/origins per dof for the Jacobian (linked robots) */
+__device__ void joint_frames(Sim& s, const double* Tc) {
+    const RobotDev& R = s.A->R;
+    const int ln = s.lane;
+    if (R.type == FKS_ROBOT_LINKED && ln < R.D) {
+        const JointDev& jd = R.joints[R.dof_joint[ln]];
+        const double* Tch = Tc + 12 * jd.child;
+        const D3 aw = rotate(Tch, D3{jd.axis[0], jd.axis[1], jd.axis[2]});
+        double* axw = s.lds + s.L.axis_w;
+        double* orw = s.lds + s.L.orig_w;
+        axw[3 * ln + 0] = aw.x;
+        axw[3 * ln + 1] = aw.y;
+        axw[3 * ln + 2] = aw.z;
+        orw[3 * ln + 0] = Tch[3];
+        orw[3 * ln + 1] = Tch[7];
+        orw[3 * ln + 2] = Tch[11];
+    }
+    wsync();
+}
+
+/* CollectPointCorrectionsAndJacobians (SPCS:1818-1939): rows written to scratch, returns R */
+__device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* Tc, const double* cfg) {
+    const SimArgs& A = *s.A;
+    const RobotDev& R = A.R;
+    const int ln = s.lane;
+    const int D = R.D;
+    const ScratchLayout SL = make_scratch_layout(A.row_cap, R.D, R.P);
+    double* J = s.scratch + SL.J;
+    double* bv = s.scratch + SL.b;
+    const double* corr = s.scratch + SL.corr;
+    const double* flag = s.scratch + SL.flag;
+    const uint32_t rc = A.row_cap;
+    joint_frames(s, Tc);
+    const double* axw = s.lds + s.L.axis_w;
+    const double* orw = s.lds + s.L.orig_w;
+    uint32_t rows = 0;
+    for (int base = 0; base < R.P; base += kWave) {
+        const int i = base + ln;
+        bool has = false;
+        D3 pcorr{0.0, 0.0, 0.0};
+        D4 xc{0.0, 0.0, 0.0, 0.0};
+        int link = 0;
+        if (i < R.P) {
+            const D4 p = load_point(R, i);
+            link = R.geom_link[R.point_geom[i]];
+            xc = xform4(Tc + 12 * link, p);
+            const bool has_self = s.self_nonempty && flag[i] != 0.0;
+            bool inb;
+            const double est = estimate_distance(A, xc, &inb, &s.lane_bytes);
+            const bool has_env = (est < 0.0) && inb;
+            D3 ecorr{0.0, 0.0, 0.0};
+            if (has_env) {
+                const D4 xp = xform4(Tp + 12 * link, p);
+                const D4 motion{xc.x - xp.x, xc.y - xp.y, xc.z - xp.z, xc.w - xp.w};
+                const D4 nm = safe_normal4(motion);
+                D3 raw;
+                const bool ok = lookup_normal(A, xc, nm, &raw, &s.err, &s.lane_bytes);
+                if (!ok) s.err |= FKS_PARTICLE_ERR_NORMAL_OOB;
+                const D3 g = safe_normal3(raw);
+                const double pen = dabs(0.0 - est);
+                ecorr = D3{g.x * pen, g.y * pen, g.z * pen};
+            }
+            has = has_self || has_env;
+            if (has_self) pcorr = D3{pcorr.x + corr[3 * i], pcorr.y + corr[3 * i + 1], pcorr.z + corr[3 * i + 2]};
+            if (has_env) pcorr = D3{pcorr.x + ecorr.x, pcorr.y + ecorr.y, pcorr.z + ecorr.z};
+        }
+        const uint64_t m = __ballot(has);
+        if (has) {
+            const uint32_t row = (rows + (uint32_t)__popcll(m & ((1ull << ln) - 1ull))) * 3u;
+            bv[row + 0] = pcorr.x;
+            bv[row + 1] = pcorr.y;
+            bv[row + 2] = pcorr.z;
+            if (R.type == FKS_ROBOT_LINKED) {
+                const uint64_t mask = R.link_dof_mask[link];
+                for (int d = 0; d < D; ++d) {
+                    D3 col{0.0, 0.0, 0.0};
+                    if ((mask >> d) & 1ull) {
+                        const D3 aw{axw[3 * d], axw[3 * d + 1], axw[3 * d + 2]};
+                        const int jt = R.joints[R.dof_joint[d]].type;
+                        if (jt == FKS_JOINT_PRISMATIC) {
+                            col = aw;
+                        } else {
+                            col = cross(aw, D3{xc.x - orw[3 * d], xc.y - orw[3 * d + 1], xc.z - orw[3 * d + 2]});
+                        }
+                        col = D3{0.0 + col.x, 0.0 + col.y, 0.0 + col.z};
+                    }
+                    J[(uint64_t)d * rc + row + 0] = col.x;
+                    J[(uint64_t)d * rc + row + 1] = col.y;
+                    J[(uint64_t)d * rc + row + 2] = col.z;
+                }
+            } else if (R.type == FKS_ROBOT_SE2) {
+                J[0 * rc + row + 0] = 0.0 + 1.0;
+                J[0 * rc + row + 1] = 0.0;
+                J[0 * rc + row + 2] = 0.0;
+                J[1 * rc + row + 0] = 0.0;
+                J[1 * rc + row + 1] = 0.0 + 1.0;
+                J[1 * rc + row + 2] = 0.0;
+                const D3 c2 = cross(D3{0.0, 0.0, 1.0}, D3{xc.x - cfg[0], xc.y - cfg[1], xc.z - 0.0});
+                J[2 * rc + row + 0] = 0.0 + c2.x;
+                J[2 * rc + row + 1] = 0.0 + c2.y;
+                J[2 * rc + row + 2] = 0.0 + c2.z;
+            } else {
+                const D3 d{xc.x - cfg[3], xc.y - cfg[7], xc.z - cfg[11]};
+                for (int a = 0; a < 3; ++a) {
+                    const D3 axis{cfg[a], cfg[4 + a], cfg[8 + a]};
+                    J[(uint64_t)a * rc + row + 0] = 0.0 + axis.x;
+                    J[(uint64_t)a * rc + row + 1] = 0.0 + axis.y;
+                    J[(uint64_t)a * rc + row + 2] = 0.0 + axis.z;
+                    const D3 c = cross(axis, d);
+                    J[(uint64_t)(3 + a) * rc + row + 0] = 0.0 + c.x;
+                    J[(uint64_t)(3 + a) * rc + row + 1] = 0.0 + c.y;
+                    J[(uint64_t)(3 + a) * rc + row + 2] = 0.0 + c.z;
+                }
+            }
+        }
+        rows += (uint32_t)__popcll(m);
+    }
+    wsync();
+    return rows * 3u;
+}
+
+/* ColPivHouseholderQR::solve (Eigen 3.2 / 3.3-beta1), rows lane-strided; x -> LDS */
+__device__ void qr_solve(Sim& s, uint32_t Rn, double* x) {
+    const SimArgs& A = *s.A;
+    const int D = A.R.D;
+    const int ln = s.lane;
+    const uint32_t rc = A.row_cap;
+    const ScratchLayout SL = make_scratch_layout(A.row_cap, A.R.D, A.R.P);
+    double* Jm = s.scratch + SL.J;
+    double* c = s.scratch + SL.b;
+    double* colsq = s.lds + s.L.colsq;
+    double* hco = s.lds + s.L.hcoef;
+    int32_t* perm = s.ldsi;
+    int32_t* transp = s.ldsi + kMaxDofs;
+    auto col = [&](int k) { return Jm + (uint64_t)k * rc; };
+    /* canonical tail squared norm of column k over rows [begin, Rn) */
+    auto tail_sq = [&](int k, uint32_t begin) {
+        double acc = 0.0;
+        const double* ck = col(k);
+        for (uint32_t r = (uint32_t)ln; r < Rn; r += kWave)
+            if (r >= begin) acc = acc + ck[r] * ck[r];
+        return bfly_sum(acc);
+    };
+    if (ln < D) x[ln] = 0.0;
+    if (D == 0) {
+        wsync();
+        return;
+    }
+    for (int k = 0; k < D; ++k) {
+        const double v = tail_sq(k, 0);
+        if (ln == 0) colsq[k] = v;
+    }
+    wsync();
+    double maxsq = colsq[0];
+    for (int k = 1; k < D; ++k)
+        if (colsq[k] > maxsq) maxsq = colsq[k];
+    const double eps = 2.220446049250313e-16;
+    const double threshold_helper = maxsq * (eps * eps) / (double)Rn;
+    const int size = ((int)Rn < D) ? (int)Rn : D;
+    int nz = size;
+    for (int k = 0; k < size; ++k) {
+        int biggest = k;
+        double bsq = colsq[k];
+        for (int c2 = k + 1; c2 < D; ++c2)
+            if (colsq[c2] > bsq) {
+                bsq = colsq[c2];
+                biggest = c2;
+            }
+        bsq = tail_sq(biggest, (uint32_t)k);
+        if (nz == size && bsq < threshold_helper * (double)(Rn - (uint32_t)k)) nz = k;
+        wsync();
+        if (ln == 0) {
+            colsq[biggest] = bsq;
+            transp[k] = biggest;
+        }
+        if (k != biggest) {
+            double* ck = col(k);
+            double* cb = col(biggest);
+            for (uint32_t r = (uint32_t)ln; r < Rn; r += kWave) {
+                const double t = ck[r];
+                ck[r] = cb[r];
+                cb[r] = t;
+            }
+            if (ln == 0) {
+                const double t = colsq[k];
+                colsq[k] = colsq[biggest];
+                colsq[biggest] = t;
+            }
+        }
+        wsync();
+        double* ck = col(k);
+        const double c0 = ck[k];
+        const double tail = (Rn - (uint32_t)k == 1u) ? 0.0 : tail_sq(k, (uint32_t)k + 1u);
+        double tau, beta;
+        if (tail <= 2.2250738585072014e-308) {
+            tau = 0.0;
+            beta = c0;
+            for (uint32_t r = (uint32_t)ln; r < Rn; r += kWave)
+                if (r > (uint32_t)k) ck[r] = 0.0;
+        } else {
+            beta = dsqrt(c0 * c0 + tail);
+            if (c0 >= 0.0) beta = -beta;
+            const double denom = c0 - beta;
+            for (uint32_t r = (uint32_t)ln; r < Rn; r += kWave)
+                if (r > (uint32_t)k) ck[r] = ck[r] / denom;
+            tau = (beta - c0) / beta;
+        }
+        wsync();
+        if (ln == 0) {
+            hco[k] = tau;
+            ck[k] = beta;
+        }
+        wsync();
+        if (Rn - (uint32_t)k == 1u) {
+            if (ln == 0)
+                for (int j = k + 1; j < D; ++j) col(j)[k] = col(j)[k] * (1.0 - tau);
+        } else if (tau != 0.0) {
+            for (int j = k + 1; j < D; ++j) {
+                double* cj = col(j);
+                double acc = 0.0;
+                for (uint32_t r = (uint32_t)ln; r < Rn; r += kWave)
+                    if (r > (uint32_t)k) acc = acc + ck[r] * cj[r];
+                double tmp = bfly_sum(acc);
+                tmp = tmp + cj[k];
+                wsync();
+                if (ln == 0) cj[k] = cj[k] - tau * tmp;
+                for (uint32_t r = (uint32_t)ln; r < Rn; r += kWave)
+                    if (r > (uint32_t)k) cj[r] = cj[r] - (tau * ck[r]) * tmp;
+                wsync();
+            }
+        }
+        wsync();
+        if (ln == 0)
+            for (int j = k + 1; j < D; ++j) colsq[j] = colsq[j] - col(j)[k] * col(j)[k];
+        wsync();
+    }
+    if (ln == 0) {
+        for (int i = 0; i < D; ++i) perm[i] = i;
+        for (int k = 0; k < size; ++k) {
+            const int t = perm[k];
+            perm[k] = perm[transp[k]];
+            perm[transp[k]] = t;
+        }
+    }
+    wsync();
+    if (nz == 0) return;
+    for (int k = 0; k < nz; ++k) {
+        const double tau = hco[k];
+        const double* ck = col(k);
+        if (Rn - (uint32_t)k == 1u) {
+            wsync();
+            if (ln == 0) c[k] = c[k] * (1.0 - tau);
+            wsync();
+        } else if (tau != 0.0) {
+            double acc = 0.0;
+            for (uint32_t r = (uint32_t)ln; r < Rn; r += kWave)
+                if (r > (uint32_t)k) acc = acc + ck[r] * c[r];
+            double tmp = bfly_sum(acc);
+            tmp = tmp + c[k];
+            wsync();
+            if (ln == 0) c[k] = c[k] - tau * tmp;
+            for (uint32_t r = (uint32_t)ln; r < Rn; r += kWave)
+                if (r > (uint32_t)k) c[r] = c[r] - (tau * ck[r]) * tmp;
+            wsync();
+        }
+    }
+    /* column-oriented back substitution on the nz x nz upper triangle */
+    for (int ii = nz - 1; ii >= 0; --ii) {
+        const double ci = c[ii];
+        if (ci != 0.0) {
+            const double* cc = col(ii);
+            const double v = ci / cc[ii];
+            wsync();
+            if (ln == 0) c[ii] = v;
+            if (ln < ii) c[ln] = c[ln] - v * cc[ln];
+            wsync();
+        }
+    }
+    if (ln < nz) x[perm[ln]] = c[ln];
+    wsync();
+}
+
+/* one controller step: ResolveForwardSimulation (SPCS:1546-1816).
+ * returns 0 ok, 1 error; sets collided/failed; result config in res_cfg */
+__device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg, bool allow_contacts, bool* out_collided,
+                            bool* out_failed, double*& Tcur, double*& Tprev) {
+    const SimArgs& A = *s.A;
+    const RobotDev& R = A.R;
+    const int ln = s.lane;
+    const int W = R.W, D = R.D;
+    double* u = s.lds + s.L.u;
+    double* ustep = s.lds + s.L.ustep;
+    double* cfg_tmp = s.lds + s.L.cfg_tmp;
+    double* cfg_prev = s.lds + s.L.cfg_prev;
+    double* cfg_act = s.lds + s.L.cfg_act;
+    double* x = s.lds + s.L.x;
+    double* real = s.lds + s.L.real;
+    double* Ttmp = s.lds + s.L.Ttmp;
+    double* cfg = s.lds + s.L.cfg_work; /* robot(immutable_robot->Clone()) SPCS:1548 */
+    *out_collided = false;
+    *out_failed = false;
+    if (ln < W) cfg[ln] = particle_cfg[ln];
+    wsync();
+    /* real_control_input = u * dt (SPCS:1549), already in u */
+    fk(s, cfg, Tcur);
+    apply_input(s, cfg, u, cfg_tmp, false, 0);
+    fk(s, cfg_tmp, Ttmp);
+    const double computed_step_motion = max_point_motion(s, Tcur, Ttmp);
+    const double raw_steps = __builtin_ceil(computed_step_motion / A.target_micro);
+    if (!(raw_steps <= 1048576.0)) {
+        s.err |= FKS_PARTICLE_ERR_MICROSTEP_CAP;
+        return 1;
+    }
+    uint32_t M = (uint32_t)raw_steps;
+    if (M < 1u) M = 1u;
+    if (ln < D) ustep[ln] = u[ln] / (double)M;
+    wsync();
+    apply_input(s, cfg, ustep, cfg_tmp, false, 0);
+    fk(s, cfg_tmp, Ttmp);
+    const double micro_motion = max_point_motion(s, Tcur, Ttmp);
+    if (micro_motion > A.allowed_micro) {
+        s.err |= FKS_PARTICLE_ERR_MICROSTEP_MOTION;
+        return 1;
+    }
+    bool collided = false;
+    for (uint32_t micro = 0; micro < M; ++micro) {
+        s.micro_count++;
+        if (ln < W) cfg_prev[ln] = cfg[ln];
+        {
+            double* t = Tprev;
+            Tprev = Tcur;
+            Tcur = t;
+        }
+        wsync();
+        apply_input(s, cfg_prev, ustep, cfg, true, micro);
+        s.err = wave_or(s.err);
+        if (s.err) {
+            if (ln < W) res_cfg[ln] = cfg_prev[ln];
+            wsync();
+            return 1;
+        }
+        fk(s, cfg, Tcur);
+        bool in_collision = check_collision(s, Tprev, Tcur);
+        if (s.err) return 1;
+        if (in_collision) collided = true;
+        if (in_collision && allow_contacts) {
+            if (ln < W) cfg_act[ln] = cfg[ln];
+            wsync();
+            uint32_t iters = 0;
+            double scaling = A.S.resolve_correction_initial_step_size;
+            while (in_collision) {
+                s.resolver_count++;
+                const uint32_t Rn = collect_corrections(s, Tprev, Tcur, cfg_act);
+                s.err = wave_or(s.err);
+                if (s.err) return 1;
+                qr_solve(s, Rn, x);
+                apply_input(s, cfg_act, x, cfg_tmp, false, 0);
+                fk(s, cfg_tmp, Ttmp);
+                const double est = max_point_motion(s, Tcur, Ttmp);
+                const double step_fraction = dmax(est / A.allowed_micro, 1.0);
+                if (ln < D) real[ln] = (x[ln] / step_fraction) * dabs(scaling);
+                wsync();
+                apply_input(s, cfg_act, real, cfg_tmp, false, 0);
+                if (ln < W) cfg_act[ln] = cfg_tmp[ln];
+                wsync();
+                fk(s, cfg_act, Tcur);
+                in_collision = check_collision(s, Tprev, Tcur);
+                if (s.err) return 1;
+                iters++;
+                if (iters > A.S.max_resolver_iterations) {
+                    s.stats[kCntUnsuccessful]++;
+                    if (s.self_nonempty)
+                        s.stats[kCntUnsuccessfulSelf]++;
+                    else
+                        s.stats[kCntUnsuccessfulEnv]++;
+                    if (ln < W) res_cfg[ln] = cfg_prev[ln];
+                    wsync();
+                    *out_collided = true;
+                    *out_failed = true;
+                    return 0;
+                }
+                if ((iters % A.S.resolve_correction_step_scaling_decay_iterations) == 0u) {
+                    if (scaling >= 0.0) {
+                        scaling = scaling * A.S.resolve_correction_step_scaling_decay_rate;
+                        if (scaling < A.S.resolve_correction_min_step_scaling) scaling = -A.S.resolve_correction_min_step_scaling;
+                    } else {
+                        scaling = -A.S.resolve_correction_min_step_scaling;
+                    }
+                }
+            }
+            if (ln < W) cfg[ln] = cfg_act[ln];
+            wsync();
+        } else if (in_collision && !allow_contacts) {
+            s.stats[kCntSuccessful]++;
+            if (ln < W) res_cfg[ln] = cfg_prev[ln];
+            wsync();
+            *out_collided = true;
+            return 0;
+        }
+    }
+    s.stats[kCntSuccessful]++;
+    if (collided)
+        s.stats[kCntCollision]++;
+    else
+        s.stats[kCntFree]++;
+    if (ln < W) res_cfg[ln] = cfg[ln];
+    wsync();
+    *out_collided = collided;
+    return 0;
+}
+
+}  // namespace fksd
+
+using namespace fksd;
+
+extern "C" __global__ void __launch_bounds__(64) fks_simulate_particles(SimArgs args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    const SimArgs& A = args;
+    const RobotDev& R = A.R;
+    Sim s;
+    s.A = &args;
+    s.lds = lds_mem;
+    s.L = make_lds_layout(R.L, R.J, R.D, R.W, R.G);
+    s.ldsi = reinterpret_cast<int32_t*>(lds_mem + s.L.ints);
+    s.scratch = A.scratch + (uint64_t)blockIdx.x * A.scratch_per_wave;
+    s.lane = lane_id();
+    const int ln = s.lane;
+    const int W = R.W, D = R.D;
+    double* cfg = s.lds + s.L.cfg;
+    double* res_cfg = s.lds + s.L.cfg_res;
+    double* u = s.lds + s.L.u;
+    unsigned long long* next_particle = reinterpret_cast<unsigned long long*>(s.lds + s.L.misc + 31);
+    while (true) {
+        if (ln == 0) *next_particle = atomicAdd(A.queue, 1ull);
+        wsync();
+        const uint64_t local = *next_particle;
+        wsync();
+        if (local >= A.n) break;
+        s.pid = A.first_pid + local;
+        s.err = 0;
+        s.lane_bytes = 0;
+        s.micro_count = 0;
+        s.resolver_count = 0;
+        s.step_count = 0;
+        for (int k = 0; k < 8; ++k) s.stats[k] = 0;
+        s.pid_integral = 0.0;
+        s.pid_last = 0.0;
+        s.self_nonempty = false;
+        const double* start = A.starts + local * (uint64_t)W;
+        const double* target = (A.num_targets == A.n) ? A.targets + local * (uint64_t)W : A.targets;
+        /* ResetPosition(start): SetPosition enforces joint limits / angle wrap */
+        if (R.type == FKS_ROBOT_LINKED) {
+            if (ln < D) {
+                const JointDev& jd = R.joints[R.dof_joint[ln]];
+                cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(start[ln])
+                                                            : clamp(start[ln], jd.lo, jd.hi);
+            }
+        } else if (R.type == FKS_ROBOT_SE2) {
+            if (ln < 3) cfg[ln] = (ln == 2) ? fks_math::enforce_continuous_revolute_bounds(start[2]) : start[ln];
+        } else {
+            if (ln < 12) cfg[ln] = start[ln];
+        }
+        wsync();
+        double* Tcur = s.lds + s.L.Tcur;
+        double* Tprev = s.lds + s.L.Tprev;
+        bool collided = false;
+        bool any_failed = false;
+        /* ForwardSimulateMutableRobot (SPCS:843-919) */
+        for (uint32_t step = 0; step < A.T; ++step) {
+            s.step = step;
+            s.step_count++;
+            double* tgt_lds = s.lds + s.L.tgt;
+            const double uc = control_action(s, cfg, target);
+            if (ln < D) u[ln] = uc * A.dt;
+            wsync();
+            bool rc = false, rf = false;
+            const int status = resolve_step(s, cfg, res_cfg, A.allow_contacts != 0, &rc, &rf, Tcur, Tprev);
+            s.err = wave_or(s.err);
+            if (status != 0 || s.err) break;
+            if (A.allow_contacts || !rc) {
+                if (ln < W) cfg[ln] = res_cfg[ln];
+                wsync();
+                if (rc) collided = true;
+                if (rf) {
+                    if (A.S.failed_resolves_end_motion) break;
+                    any_failed = true;
+                } else if (any_failed) {
+                    s.stats[kCntRecovered]++;
+                }
+                if (A.S.simulation_shortcut_distance > 0.0 || A.S.simulation_shortcut_distance != A.S.simulation_shortcut_distance) {
+                    if (ln < W) tgt_lds[ln] = target[ln];
+                    wsync();
+                    const double dist = config_distance(s, cfg, tgt_lds);
+                    wsync();
+                    if (dist < A.S.simulation_shortcut_distance) break;
+                }
+            } else {
+                break;
+            }
+        }
+        /* outputs */
+        if (ln < W) A.out_q[local * (uint64_t)W + ln] = cfg[ln];
+        const uint64_t bytes = wave_sum_u64(s.lane_bytes);
+        if (ln == 0) {
+            if (A.out_collided) A.out_collided[local] = collided ? 1 : 0;
+            if (A.out_micro) A.out_micro[local] = (uint32_t)s.micro_count;
+            if (A.out_resolver) A.out_resolver[local] = (uint32_t)s.resolver_count;
+            if (A.out_err) A.out_err[local] = s.err;
+            for (int k = 0; k < 8; ++k)
+                if (s.stats[k]) atomicAdd(A.counters + k, (unsigned long long)s.stats[k]);
+            atomicAdd(A.counters + kCntSteps, (unsigned long long)s.step_count);
+            atomicAdd(A.counters + kCntMicrosteps, (unsigned long long)s.micro_count);
+            atomicAdd(A.counters + kCntResolver, (unsigned long long)s.resolver_count);
+            atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes);
+            if (s.err) atomicAdd(A.counters + kCntErrorParticles, 1ull);
+        }
+        wsync();
+    }
+}
+
+/* device self-test of the portable libm (fks_selftest_math) */
+extern "C" __global__ void fks_math_probe(const double* a, const double* b, double* out, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double x = a[i], y = b[i];
+    out[8 * i + 0] = fks_math::sin(x);
+    out[8 * i + 1] = fks_math::cos(x);
+    out[8 * i + 2] = fks_math::log(fks_math::dabs(y) + 1e-300);
+    out[8 * i + 3] = fks_math::atan2(x, y);
+    out[8 * i + 4] = fks_math::dsqrt(fks_math::dabs(y));
+    out[8 * i + 5] = x / y;
+    out[8 * i + 6] = fks_math::enforce_continuous_revolute_bounds(x);
+    out[8 * i + 7] = (x * y + x) * y - x * x;
+}

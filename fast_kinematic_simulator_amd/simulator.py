@@ -1,0 +1,218 @@
+"""Host-side mirror of the reference simulator interface over the C-ABI.
+
+Mirrors ``simple_particle_contact_simulator::SimpleParticleContactSimulator``
+(SPCS:371-1999) as seen through ``uncertainty_planning_core``'s
+``SimulatorInterface`` and the ``fast_kinematic_simulator`` factories
+(FKS.hpp:11-22, FKS.cpp:4-71).  Batch calls run on the GPU through
+``libfks_hip.so``; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, fields
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+from . import _capi
+from .environment import SimulatorEnvironment
+from .robots import RobotDescription
+
+
+@dataclass
+class SimulatorSolverParameters:
+    """SimulatorSolverParameters with the defaults of SPCS:357-368."""
+
+    forward_simulation_time: float = 1.0
+    simulation_shortcut_distance: float = 0.0
+    environment_collision_check_tolerance: float = 0.001
+    resolve_correction_step_scaling_decay_rate: float = 0.5
+    resolve_correction_initial_step_size: float = 1.0
+    resolve_correction_min_step_scaling: float = 0.03125
+    max_resolver_iterations: int = 25
+    resolve_correction_step_scaling_decay_iterations: int = 5
+    failed_resolves_end_motion: bool = True
+
+    def to_c(self) -> _capi.SolverParams:
+        p = _capi.SolverParams()
+        for f in fields(self):
+            v = getattr(self, f.name)
+            setattr(p, f.name, int(v) if isinstance(v, (bool, int)) and not isinstance(v, float) else v)
+        return p
+
+
+def get_default_solver_parameters() -> SimulatorSolverParameters:
+    """fast_kinematic_simulator::GetDefaultSolverParameters (FKS.hpp:13-16)."""
+    return SimulatorSolverParameters()
+
+
+@dataclass
+class SimulationResult:
+    """simple_simulator_interface::SimulationResult(reached, target, collided, true) (SPCS:918)."""
+
+    result_config: np.ndarray
+    target_config: np.ndarray
+    did_contact: bool
+    outcome_is_valid: bool = True
+    microsteps: int = 0
+    resolver_iterations: int = 0
+    error_flags: int = 0
+
+
+class HipParticleContactSimulator:
+    """SimpleParticleContactSimulator on one MI355X.  The stacked-Jacobian resolver
+    is always used, as the factories hard-wire (FKS.cpp:22,45,68)."""
+
+    def __init__(self, environment: SimulatorEnvironment, solver_config: SimulatorSolverParameters,
+                 simulation_controller_frequency: float, prng_seed: int, debug_level: int = 0, device: int = 0):
+        self._lib = _capi.lib()
+        self.environment = environment
+        self.solver_config = solver_config
+        self.simulation_controller_frequency = float(simulation_controller_frequency)
+        self.prng_seed = int(prng_seed)
+        env_c, self._env_keep = environment.to_c()
+        params = solver_config.to_c()
+        ctx = ctypes.c_void_p()
+        st = self._lib.fks_create(ctypes.byref(env_c), ctypes.byref(params), self.simulation_controller_frequency,
+                                  ctypes.c_uint64(self.prng_seed & 0xFFFFFFFFFFFFFFFF), int(debug_level), int(device),
+                                  ctypes.byref(ctx))
+        _capi.check(st, None, "fks_create")
+        self._ctx = ctx
+        self._robot_key = None
+        self._robot = None
+
+    # ---- lifetime ----
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.fks_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- reference interface ----
+    def get_debug_level(self) -> int:
+        return int(self._lib.fks_get_debug_level(self._ctx))
+
+    def set_debug_level(self, debug_level: int) -> int:
+        return int(self._lib.fks_set_debug_level(self._ctx, int(debug_level)))
+
+    def get_statistics(self) -> dict:
+        s = _capi.Statistics()
+        _capi.check(self._lib.fks_get_statistics(self._ctx, ctypes.byref(s)), self._ctx, "fks_get_statistics")
+        return s.as_dict()
+
+    def reset_statistics(self):
+        _capi.check(self._lib.fks_reset_statistics(self._ctx), self._ctx, "fks_reset_statistics")
+
+    def reset_generators(self, prng_seed: int):
+        _capi.check(self._lib.fks_reset_generators(self._ctx, ctypes.c_uint64(int(prng_seed))), self._ctx, "reset")
+
+    def set_call_index(self, call_index: int):
+        _capi.check(self._lib.fks_set_call_index(self._ctx, ctypes.c_uint64(int(call_index))), self._ctx, "call index")
+
+    def get_call_index(self) -> int:
+        return int(self._lib.fks_get_call_index(self._ctx))
+
+    def last_call_counters(self) -> dict:
+        c = _capi.CallCounters()
+        _capi.check(self._lib.fks_get_last_call_counters(self._ctx, ctypes.byref(c)), self._ctx, "counters")
+        return c.as_dict()
+
+    def set_robot(self, robot: RobotDescription):
+        key = id(robot)
+        if self._robot_key == key and self._robot is robot:
+            return
+        desc, keep = robot.to_c()
+        _capi.check(self._lib.fks_set_robot(self._ctx, ctypes.byref(desc)), self._ctx, "fks_set_robot")
+        del keep
+        self._robot_key = key
+        self._robot = robot
+
+    def forward_simulate_arrays(self, robot: RobotDescription, start_positions, target_positions, allow_contacts: bool,
+                                reverse: bool = False) -> dict:
+        """Batch call with numpy arrays: starts (n, W), targets (1 or n, W)."""
+        self.set_robot(robot)
+        W = robot.config_width
+        starts = np.ascontiguousarray(np.asarray(start_positions, dtype=np.float64).reshape(-1, W))
+        targets = np.ascontiguousarray(np.asarray(target_positions, dtype=np.float64).reshape(-1, W))
+        n = starts.shape[0]
+        if n > 0 and targets.shape[0] not in (1, n):
+            raise ValueError("target_positions must hold 1 or len(start_positions) configurations (SPCS:792)")
+        out = np.zeros((n, W), dtype=np.float64)
+        collided = np.zeros(n, dtype=np.uint8)
+        micro = np.zeros(n, dtype=np.uint32)
+        resolver = np.zeros(n, dtype=np.uint32)
+        errors = np.zeros(n, dtype=np.uint32)
+        fn = self._lib.fks_reverse_simulate if reverse else self._lib.fks_forward_simulate
+        st = fn(self._ctx, _capi.as_ptr(starts, ctypes.c_double), n, _capi.as_ptr(targets, ctypes.c_double),
+                targets.shape[0], 1 if allow_contacts else 0, _capi.as_ptr(out, ctypes.c_double),
+                _capi.as_ptr(collided, ctypes.c_uint8), _capi.as_ptr(micro, ctypes.c_uint32),
+                _capi.as_ptr(resolver, ctypes.c_uint32), _capi.as_ptr(errors, ctypes.c_uint32))
+        _capi.check(st, self._ctx, "fks_forward_simulate")
+        return {"positions": out, "collided": collided.astype(bool), "microsteps": micro, "resolver_iterations": resolver,
+                "error_flags": errors}
+
+    def forward_simulate_robots(self, immutable_robot: RobotDescription, start_positions: Sequence, target_positions: Sequence,
+                                allow_contacts: bool, display_fn: Optional[Callable] = None) -> List[SimulationResult]:
+        """ForwardSimulateRobots (SPCS:788-804).  display_fn is accepted for interface
+        parity; the batch path never draws (SPCS:801 passes enable_tracing=false)."""
+        return self._results(immutable_robot, start_positions, target_positions, allow_contacts, reverse=False)
+
+    def reverse_simulate_robots(self, immutable_robot: RobotDescription, start_positions: Sequence, target_positions: Sequence,
+                                allow_contacts: bool, display_fn: Optional[Callable] = None) -> List[SimulationResult]:
+        """ReverseSimulateRobots (SPCS:806-822) == forward simulation (SPCS:838-841)."""
+        return self._results(immutable_robot, start_positions, target_positions, allow_contacts, reverse=True)
+
+    def forward_simulate_robot(self, immutable_robot: RobotDescription, start_position, target_position,
+                               allow_contacts: bool) -> SimulationResult:
+        """ForwardSimulateRobot (SPCS:824-829) as a batch of one."""
+        return self._results(immutable_robot, [start_position], [target_position], allow_contacts, reverse=False)[0]
+
+    def _results(self, robot, starts, targets, allow_contacts, reverse):
+        W = robot.config_width
+        tarr = np.asarray(targets, dtype=np.float64).reshape(-1, W)
+        r = self.forward_simulate_arrays(robot, starts, tarr, allow_contacts, reverse=reverse)
+        n = r["positions"].shape[0]
+        out = []
+        for i in range(n):
+            tgt = tarr[i] if tarr.shape[0] == n else tarr[0]
+            out.append(SimulationResult(r["positions"][i].copy(), tgt.copy(), bool(r["collided"][i]), True,
+                                        int(r["microsteps"][i]), int(r["resolver_iterations"][i]), int(r["error_flags"][i])))
+        return out
+
+    def forward_simulate_device(self, robot: RobotDescription, d_starts, n: int, d_targets, num_targets: int,
+                                first_particle_id: int, allow_contacts: bool, d_out_positions, d_out_collided=0,
+                                d_out_microsteps=0, d_out_resolver_iterations=0, d_out_error_flags=0, stream=0,
+                                synchronize=False):
+        """fks_forward_simulate_device: every buffer is a device pointer (int), e.g.
+        torch_tensor.data_ptr(); `stream` a hipStream_t handle (int)."""
+        self.set_robot(robot)
+        st = self._lib.fks_forward_simulate_device(
+            self._ctx, ctypes.c_void_p(d_starts), n, ctypes.c_void_p(d_targets), num_targets, first_particle_id,
+            1 if allow_contacts else 0, ctypes.c_void_p(d_out_positions), ctypes.c_void_p(d_out_collided or None),
+            ctypes.c_void_p(d_out_microsteps or None), ctypes.c_void_p(d_out_resolver_iterations or None),
+            ctypes.c_void_p(d_out_error_flags or None), ctypes.c_void_p(stream or None), 1 if synchronize else 0)
+        _capi.check(st, self._ctx, "fks_forward_simulate_device")
+
+
+def _make(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level, device=0):
+    return HipParticleContactSimulator(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level, device)
+
+
+def make_se2_simulator(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level=0, device=0):
+    """fast_kinematic_simulator::MakeSE2Simulator (FKS.cpp:4-25)."""
+    return _make(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level, device)
+
+
+def make_se3_simulator(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level=0, device=0):
+    """fast_kinematic_simulator::MakeSE3Simulator (FKS.cpp:27-48)."""
+    return _make(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level, device)
+
+
+def make_linked_simulator(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level=0, device=0):
+    """fast_kinematic_simulator::MakeLinkedSimulator (FKS.cpp:50-71)."""
+    return _make(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level, device)

@@ -1,0 +1,283 @@
+"""Synthetic workloads for the five configurations of BASELINE.json / SURVEY.md §8(d).
+
+Each workload is a robot + environment + particle batch + solver parameters.
+Sizes are the BASELINE ones; ``scale`` shrinks the particle count (and nothing
+else) for parity tests.  All random choices are seeded.
+
+cfg1  SE(2) 3-DOF planar robot, 64 points, 64^3 grid @ 0.0625 m, 32 particles x 50 steps
+cfg2  UR5-style 6-DOF arm, 7 links x 64 points, 128^3 @ 0.02 m, 4096 x 100
+cfg3  7-DOF arm (iiwa-like), 8 links x 64 points, 256^3 @ 0.01 m, 65536 x 200   <- headline
+cfg4  SE(3) free flyer, 256 points, 256^3 @ 0.01 m, 1M x 100 (8 GPUs)
+cfg5  dual-arm 14-DOF (Baxter-like), 17 links x 64 points, 512^3 @ 0.005 m, 1M x 200 (8 GPUs)
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+
+from . import _capi
+from .environment import ObstacleConfig, SimulatorEnvironment, build_complete_environment
+from .robots import (ControllerConfig, Joint, RobotDescription, make_linked_robot, make_se2_robot, make_se3_robot,
+                     rotation_from_axis_angle, se3_pose, transform34)
+from .simulator import SimulatorSolverParameters
+
+
+@dataclass
+class Workload:
+    name: str
+    description: str
+    robot: RobotDescription
+    env_builder: Callable[[], SimulatorEnvironment]
+    starts: np.ndarray
+    targets: np.ndarray
+    solver: SimulatorSolverParameters
+    controller_frequency: float
+    seed: int
+    allow_contacts: bool = True
+    grid_cells: int = 0
+    resolution: float = 0.0
+    _env: Optional[SimulatorEnvironment] = field(default=None, repr=False)
+
+    @property
+    def num_particles(self) -> int:
+        return int(self.starts.shape[0])
+
+    @property
+    def steps(self) -> int:
+        return max(int(self.solver.forward_simulation_time * self.controller_frequency), 1)
+
+    def environment(self) -> SimulatorEnvironment:
+        if self._env is None:
+            self._env = self.env_builder()
+        return self._env
+
+
+def cylinder_points(length: float, radius: float, n: int = 64, rings: int = 16, z0: float = 0.0) -> np.ndarray:
+    """n points on rings around the local z axis from z0 to z0+length."""
+    per = n // rings
+    pts = []
+    for r in range(rings):
+        z = z0 + length * (r + 0.5) / rings
+        for k in range(per):
+            a = 2.0 * np.pi * (k + 0.5 * (r % 2)) / per
+            pts.append([radius * np.cos(a), radius * np.sin(a), z, 1.0])
+    return np.array(pts, dtype=np.float64)
+
+
+def box(object_id, center, half, rotation=None) -> ObstacleConfig:
+    return ObstacleConfig(object_id, transform34(center, rotation), list(half))
+
+
+def grid_origin(lo) -> np.ndarray:
+    return transform34(lo)
+
+
+# ---------------------------------------------------------------- cfg1: SE(2)
+def _cfg1_env():
+    rng = np.random.default_rng(1)
+    obstacles = []
+    for i in range(12):
+        c = [rng.uniform(0.5, 3.5), rng.uniform(0.5, 3.5), 0.0]
+        h = [rng.uniform(0.08, 0.25), rng.uniform(0.08, 0.25), 1.0]
+        obstacles.append(box(i + 1, c, h, rotation_from_axis_angle([0, 0, 1], rng.uniform(0, np.pi))))
+    return build_complete_environment(obstacles, 0.0625, origin=grid_origin([0.0, 0.0, -2.0]), num_cells=(64, 64, 64))
+
+
+def _se2_points(x, y, th, pts):
+    c, s = np.cos(th), np.sin(th)
+    return np.stack([c * pts[:, 0] - s * pts[:, 1] + x, s * pts[:, 0] + c * pts[:, 1] + y, pts[:, 2]], axis=1)
+
+
+def cfg1(scale: float = 1.0) -> Workload:
+    res = 0.0625
+    g = np.arange(8) * (res * 0.5) - 3.5 * res * 0.5
+    pts = np.array([[x, y, 0.0, 1.0] for x in g for y in g])
+    tr = ControllerConfig(kp=1.0, ki=0.1, kd=0.01, integral_clamp=1.0, velocity_limit=0.5,
+                          max_actuator_proportional_noise=0.2, max_actuator_minimum_noise=0.05)
+    robot = make_se2_robot(pts, tr, tr, name="se2_planar_box")
+    env = _cfg1_env()
+    rng = np.random.default_rng(2)
+    n = max(1, int(round(32 * scale)))
+    starts = []
+    while len(starts) < n:
+        q = np.array([rng.uniform(0.4, 3.6), rng.uniform(0.4, 3.6), rng.uniform(-np.pi, np.pi)])
+        if np.all(env.nearest(_se2_points(q[0], q[1], q[2], pts)) > 2 * res):
+            starts.append(q)
+    target = np.array([[2.0, 2.0, 0.5]])
+    solver = SimulatorSolverParameters(forward_simulation_time=1.0)
+    wl = Workload("cfg1", "SE(2) 3-DOF planar robot, 64^3 grid, 32 particles x 50 steps", robot, lambda: env,
+                  np.array(starts), target, solver, 50.0, 11, True, 64, res)
+    wl._env = env
+    return wl
+
+
+# ---------------------------------------------------------------- arms
+def _arm_controllers(d, vmax=1.0):
+    # the actuator noise floor is min_noise * vmax per applied input (UNC:80-86), i.e. per
+    # microstep: keep it at ~10% of a typical microstep joint delta (vmax*dt/M ~ 1e-3 rad)
+    return [ControllerConfig(kp=10.0, ki=1.0, kd=0.1, integral_clamp=0.5, velocity_limit=vmax, acceleration_limit=vmax * 10,
+                             max_actuator_proportional_noise=0.2, max_actuator_minimum_noise=0.0002) for _ in range(d)]
+
+
+def serial_arm(segments, axes, radii, base_height, base_radius, limits=np.pi, name="arm",
+               base_transform=None) -> RobotDescription:
+    """Serial revolute chain: joint i sits at the end of segment i-1 (segment 0 = base),
+    link i spans segment i along its local +z."""
+    n = len(axes)
+    joints = []
+    geoms = [(0, cylinder_points(base_height, base_radius, 64, 16))]
+    for i in range(n):
+        offset = base_height if i == 0 else segments[i - 1]
+        joints.append(Joint(parent=i, child=i + 1, type=_capi.JOINT_REVOLUTE, origin=transform34([0, 0, offset]),
+                            axis=tuple(axes[i]), lower=-limits, upper=limits))
+        geoms.append((i + 1, cylinder_points(segments[i], radii[i], 64, 16, z0=0.0)))
+    allowed = [(i, i + 1) for i in range(n)] + [(i, i + 2) for i in range(n - 1)]
+    return make_linked_robot(base_transform if base_transform is not None else transform34([0, 0, 0.03]), n + 1, joints, geoms,
+                             allowed, _arm_controllers(n), [1.0] * n, name=name)
+
+
+def _cfg2_env():
+    obstacles = [box(1, [0.0, 0.0, -0.05], [0.9, 0.9, 0.05]),           # table, top at z = 0
+                 box(2, [0.45, 0.25, 0.25], [0.06, 0.06, 0.25]),        # post
+                 box(3, [0.35, -0.35, 0.12], [0.10, 0.08, 0.12]),       # block
+                 box(4, [-0.3, 0.4, 0.35], [0.05, 0.05, 0.35])]         # pillar
+    return build_complete_environment(obstacles, 0.02, origin=grid_origin([-1.28, -1.28, -0.4]), num_cells=(128, 128, 128))
+
+
+def cfg2(scale: float = 1.0) -> Workload:
+    segs = [0.43, 0.39, 0.11, 0.09, 0.08, 0.06]
+    axes = [[0, 0, 1], [0, 1, 0], [0, 1, 0], [0, 1, 0], [0, 0, 1], [0, 1, 0]]
+    robot = serial_arm(segs, axes, [0.055, 0.05, 0.045, 0.04, 0.04, 0.035], 0.09, 0.07, name="ur5_style")
+    nominal = np.array([0.0, 0.9, 1.2, 0.4, 0.0, 0.3])
+    rng = np.random.default_rng(3)
+    n = max(1, int(round(4096 * scale)))
+    starts = nominal + rng.uniform(-0.05, 0.05, size=(n, 6))
+    target = np.array([[0.9, 1.1, 0.8, 0.6, 0.5, -0.3]])
+    solver = SimulatorSolverParameters(forward_simulation_time=1.0)
+    return Workload("cfg2", "UR5-style 6-DOF arm, 128^3 SDF, 4096 particles x 100 steps", robot, _cfg2_env, starts, target,
+                    solver, 100.0, 12, True, 128, 0.02)
+
+
+def _cfg3_env():
+    rng = np.random.default_rng(4)
+    obstacles = [box(1, [0.0, 0.0, -0.05], [1.1, 1.1, 0.05])]            # table, top at z = 0
+    pillars = [[0.55, 0.35], [0.25, 0.62], [-0.45, 0.45], [0.6, -0.3], [-0.2, -0.6]]
+    for i, (x, y) in enumerate(pillars):
+        h = rng.uniform(0.3, 0.5)
+        obstacles.append(box(2 + i, [x, y, h / 2], [0.05, 0.05, h / 2]))
+    return build_complete_environment(obstacles, 0.01, origin=grid_origin([-1.28, -1.28, -0.3]), num_cells=(256, 256, 256))
+
+
+def iiwa_style_arm() -> RobotDescription:
+    segs = [0.14, 0.2, 0.2, 0.2, 0.2, 0.08, 0.126]
+    axes = [[0, 0, 1], [0, 1, 0], [0, 0, 1], [0, -1, 0], [0, 0, 1], [0, 1, 0], [0, 0, 1]]
+    radii = [0.06, 0.06, 0.055, 0.055, 0.05, 0.045, 0.04]
+    return serial_arm(segs, axes, radii, 0.2, 0.08, limits=2.9, name="iiwa_style_7dof")
+
+
+CFG3_NOMINAL = np.array([0.0, 0.6, 0.0, -1.2, 0.0, 0.6, 0.0])
+CFG3_TARGET = np.array([1.1, 0.9, 0.3, -0.7, 0.4, 1.0, 0.5])
+
+
+def cfg3(scale: float = 1.0) -> Workload:
+    robot = iiwa_style_arm()
+    rng = np.random.default_rng(4)
+    n = max(1, int(round(65536 * scale)))
+    starts = CFG3_NOMINAL + rng.uniform(-0.05, 0.05, size=(n, 7))
+    solver = SimulatorSolverParameters(forward_simulation_time=2.0)
+    return Workload("cfg3", "7-DOF linked arm, 256^3 SDF, 65536 particles x 200 steps", robot, _cfg3_env, starts,
+                    CFG3_TARGET[None, :].copy(), solver, 100.0, 13, True, 256, 0.01)
+
+
+# ---------------------------------------------------------------- cfg4: SE(3)
+def _cfg4_env():
+    rng = np.random.default_rng(5)
+    obstacles = []
+    for i in range(24):
+        c = [rng.uniform(-0.9, 0.9), rng.uniform(-0.9, 0.9), rng.uniform(-0.9, 0.9)]
+        if np.linalg.norm(c) < 0.35:
+            continue
+        h = [rng.uniform(0.04, 0.15) for _ in range(3)]
+        obstacles.append(box(i + 1, c, h, rotation_from_axis_angle(rng.normal(size=3), rng.uniform(0, np.pi))))
+    return build_complete_environment(obstacles, 0.01, origin=grid_origin([-1.28, -1.28, -1.28]), num_cells=(256, 256, 256))
+
+
+def cfg4(scale: float = 1.0) -> Workload:
+    g = (np.arange(8) - 3.5) * 0.02
+    gz = (np.arange(4) - 1.5) * 0.02
+    pts = np.array([[x, y, z, 1.0] for x in g for y in g for z in gz])
+    tr = ControllerConfig(kp=4.0, ki=0.4, kd=0.04, integral_clamp=0.5, velocity_limit=0.5,
+                          max_actuator_proportional_noise=0.2, max_actuator_minimum_noise=0.0005)
+    rot = ControllerConfig(kp=4.0, ki=0.4, kd=0.04, integral_clamp=0.5, velocity_limit=1.0,
+                           max_actuator_proportional_noise=0.2, max_actuator_minimum_noise=0.0005)
+    robot = make_se3_robot(pts, tr, rot, name="se3_free_flyer")
+    rng = np.random.default_rng(5)
+    n = max(1, int(round(1048576 * scale)))
+    starts = np.zeros((n, 12))
+    for i in range(n):
+        R = rotation_from_axis_angle(rng.normal(size=3), rng.uniform(0, 0.1))
+        starts[i] = se3_pose(rng.uniform(-0.03, 0.03, size=3), R)
+    target = se3_pose([0.45, 0.3, -0.2], rotation_from_axis_angle([0.3, 1.0, 0.2], 0.8))[None, :]
+    solver = SimulatorSolverParameters(forward_simulation_time=1.0)
+    return Workload("cfg4", "SE(3) free-flying rigid body, 256^3 SDF, 1M particles x 100 steps", robot, _cfg4_env, starts,
+                    target, solver, 100.0, 14, True, 256, 0.01)
+
+
+# ---------------------------------------------------------------- cfg5: dual arm
+def dual_arm_robot() -> RobotDescription:
+    """Baxter-like: torso (link 0) carrying two 7-DOF arms on fixed shoulder mounts;
+    17 links (torso, 2 mounts, 2 x 7 arm links), 14 dofs."""
+    joints = []
+    geoms = [(0, cylinder_points(0.5, 0.12, 64, 16))]
+    segs = [0.12, 0.25, 0.12, 0.25, 0.12, 0.15, 0.1]
+    axes = [[0, 0, 1], [0, 1, 0], [1, 0, 0], [0, 1, 0], [1, 0, 0], [0, 1, 0], [1, 0, 0]]
+    radii = [0.06, 0.055, 0.05, 0.05, 0.045, 0.04, 0.035]
+    link = 1
+    allowed = []
+    for side, y in ((0, 0.26), (1, -0.26)):
+        mount = link
+        rot = rotation_from_axis_angle([1, 0, 0], -np.pi / 2 if side == 0 else np.pi / 2)
+        joints.append(Joint(parent=0, child=mount, type=_capi.JOINT_FIXED, origin=transform34([0.06, y, 0.5], rot)))
+        geoms.append((mount, cylinder_points(0.08, 0.07, 64, 16)))
+        allowed.append((0, mount))
+        prev = mount
+        link += 1
+        for i in range(7):
+            off = 0.08 if i == 0 else segs[i - 1]
+            joints.append(Joint(parent=prev, child=link, type=_capi.JOINT_REVOLUTE, origin=transform34([0, 0, off]),
+                                axis=tuple(axes[i]), lower=-2.9, upper=2.9))
+            geoms.append((link, cylinder_points(segs[i], radii[i], 64, 16)))
+            allowed.append((prev, link))
+            if i == 0:
+                allowed.append((0, link))
+            else:
+                allowed.append((prev - 1 if prev - 1 >= mount else 0, link))
+            prev = link
+            link += 1
+    # geometry indices equal link indices here (one geometry per link, in link order)
+    return make_linked_robot(transform34([0, 0, 0]), link, joints, geoms, allowed, _arm_controllers(14), [1.0] * 14,
+                             name="dual_arm_14dof")
+
+
+def _cfg5_env():
+    obstacles = [box(1, [0.6, 0.0, 0.35], [0.35, 0.7, 0.05]),
+                 box(2, [0.7, 0.35, 0.48], [0.1, 0.1, 0.08]),
+                 box(3, [0.7, -0.35, 0.48], [0.1, 0.1, 0.08])]
+    return build_complete_environment(obstacles, 0.005, origin=grid_origin([-0.48, -1.28, -0.2]), num_cells=(512, 512, 512))
+
+
+def cfg5(scale: float = 1.0) -> Workload:
+    robot = dual_arm_robot()
+    nominal = np.array([0.3, 0.5, 0.0, 0.8, 0.0, 0.4, 0.0] * 2)
+    target = nominal + np.array([0.5, 0.3, 0.2, -0.3, 0.3, 0.2, 0.1, -0.5, 0.3, -0.2, -0.3, -0.3, 0.2, -0.1])
+    rng = np.random.default_rng(6)
+    n = max(1, int(round(1048576 * scale)))
+    starts = nominal + rng.uniform(-0.05, 0.05, size=(n, 14))
+    solver = SimulatorSolverParameters(forward_simulation_time=2.0)
+    return Workload("cfg5", "dual-arm 14-DOF linked model, 512^3 SDF, 1M particles x 200 steps", robot, _cfg5_env, starts,
+                    target[None, :], solver, 100.0, 15, True, 512, 0.005)
+
+
+WORKLOADS: Dict[str, Callable[..., Workload]] = {"cfg1": cfg1, "cfg2": cfg2, "cfg3": cfg3, "cfg4": cfg4, "cfg5": cfg5}

@@ -1,0 +1,296 @@
+/*
+ * fks_capi.h — C-ABI of the MI355X-native particle forward-simulation path.
+ *
+ * This is the drop-in boundary that replaces the OpenMP particle loop of
+ * simple_particle_contact_simulator::SimpleParticleContactSimulator
+ * (reference: include/fast_kinematic_simulator/simple_particle_contact_simulator.hpp,
+ * abbreviated SPCS below).  Plain C types only: no C++, no torch, no HIP types
+ * cross this header.  A C++ host wrapper that re-implements the
+ * uncertainty_planning_core SimulatorInterface on top of these entry points is in
+ * include/fast_kinematic_simulator_amd/hip_particle_contact_simulator.hpp and the
+ * Python mirror is fast_kinematic_simulator_amd/simulator.py.
+ *
+ * Entry point  ->  reference interface it replaces
+ *   fks_default_solver_params  -> fast_kinematic_simulator::GetDefaultSolverParameters   (FKS.hpp:13-16)
+ *   fks_create + fks_set_robot -> fast_kinematic_simulator::Make{SE2,SE3,Linked}Simulator (FKS.cpp:4-71),
+ *                                 SimpleParticleContactSimulator ctor (SPCS:420-444)
+ *   fks_forward_simulate       -> SimpleParticleContactSimulator::ForwardSimulateRobots (SPCS:788-804)
+ *   fks_reverse_simulate       -> SimpleParticleContactSimulator::ReverseSimulateRobots (SPCS:806-822)
+ *   fks_forward_simulate_device-> same as fks_forward_simulate, inputs/outputs already in HBM
+ *   fks_get_statistics         -> SimpleParticleContactSimulator::GetStatistics          (SPCS:488-500)
+ *   fks_reset_statistics       -> SimpleParticleContactSimulator::ResetStatistics        (SPCS:502-512)
+ *   fks_reset_generators       -> SimpleParticleContactSimulator::ResetGenerators        (SPCS:457-471)
+ *   fks_get/set_debug_level    -> Get/SetDebugLevel                                       (SPCS:446-455)
+ *   fks_env_build              -> simulator_environment_builder::BuildCompleteEnvironment
+ *                                 (src/.../simulator_environment_builder.cpp:470-476; CPU preprocessing)
+ *
+ * Errors: every call returns fks_status; fks_get_last_error() gives the text.
+ * Nothing throws across the ABI.  Per-particle problems that the reference
+ * handles with assert() (SPCS:1570-1575, 1882, GetBestSurfaceNormal SPCS:113-114)
+ * are reported as FKS_PARTICLE_ERR_* bits and that particle stops simulating.
+ *
+ * Threading: a context is single-caller and stream-ordered (the reference's
+ * simulator object is not safe for concurrent calls either, SPCS:846-850).
+ */
+#ifndef FKS_CAPI_H
+#define FKS_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FKS_ABI_VERSION 1
+
+typedef enum {
+    FKS_OK = 0,
+    FKS_ERR_INVALID_ARGUMENT = 1,
+    FKS_ERR_HIP = 2,
+    FKS_ERR_NO_ROBOT = 3,
+    FKS_ERR_OUT_OF_MEMORY = 4,
+    FKS_ERR_UNSUPPORTED = 5,
+    FKS_ERR_NO_DEVICE = 6
+} fks_status;
+
+typedef enum { FKS_ROBOT_LINKED = 0, FKS_ROBOT_SE2 = 1, FKS_ROBOT_SE3 = 2 } fks_robot_type;
+
+/* arc_utilities simple_linked_robot_model::SimpleJointModel::JOINT_TYPE values */
+typedef enum {
+    FKS_JOINT_FIXED = 0,
+    FKS_JOINT_REVOLUTE = 1,
+    FKS_JOINT_CONTINUOUS = 2,
+    FKS_JOINT_PRISMATIC = 4
+} fks_joint_type;
+
+/* per-particle error bits (replace the reference's asserts) */
+#define FKS_PARTICLE_ERR_MICROSTEP_MOTION 0x1u   /* SPCS:1570-1575 computed microstep motion > allowed  */
+#define FKS_PARTICLE_ERR_NORMAL_OOB 0x2u         /* SPCS:1882 surface normal lookup out of bounds        */
+#define FKS_PARTICLE_ERR_ZERO_DIRECTION 0x4u     /* SPCS:113-114 best-normal query with zero motion      */
+#define FKS_PARTICLE_ERR_RNG_EXHAUSTED 0x8u      /* truncated-normal rejection exceeded its draw budget  */
+#define FKS_PARTICLE_ERR_SELF_CAPACITY 0x10u     /* > FKS_MAX_SELF_CELLS colliding cells or
+                                                    > FKS_MAX_SELF_LINKS links in one colliding cell     */
+#define FKS_PARTICLE_ERR_KEY_RANGE 0x20u         /* non-finite point in the self-collision grid          */
+#define FKS_PARTICLE_ERR_MICROSTEP_CAP 0x40u     /* microsteps per controller step exceeded 2^20         */
+#define FKS_PARTICLE_ERR_SELF_SINGULAR 0x80u     /* NaN self-collision correction (assert SPCS:1151-1153) */
+
+/* capacities of the self-collision impulse solve (both the HIP path and the oracle
+ * flag FKS_PARTICLE_ERR_SELF_CAPACITY beyond them) */
+#define FKS_MAX_SELF_CELLS 64
+#define FKS_MAX_SELF_LINKS 8
+
+/* SimulatorSolverParameters (SPCS:345-369); booleans widened to uint32 */
+typedef struct {
+    double forward_simulation_time;
+    double simulation_shortcut_distance;
+    double environment_collision_check_tolerance;
+    double resolve_correction_step_scaling_decay_rate;
+    double resolve_correction_initial_step_size;
+    double resolve_correction_min_step_scaling;
+    uint32_t max_resolver_iterations;
+    uint32_t resolve_correction_step_scaling_decay_iterations;
+    uint32_t failed_resolves_end_motion;
+    uint32_t reserved;
+} fks_solver_params;
+
+/* A VoxelGrid geometry (arc_utilities VoxelGrid): origin transform as a 3x4
+ * row-major [R | t], cubic cells, cell counts; storage index
+ * (x * ny + y) * nz + z (z fastest). */
+typedef struct {
+    double origin[12];
+    double resolution;
+    int64_t num_cells[3];
+} fks_grid_geometry;
+
+/* The three inputs the reference simulator copies at construction (SPCS:379-381):
+ * environment_ (collision map: only its geometry is used on the path: GetResolution
+ * SPCS:524-527 and GetInverseOriginTransform SPCS:1176), environment_sdf_
+ * (float distance per cell, oob_value returned outside, SEB.cpp:473 uses +inf) and
+ * surface_normals_grid_ (SPCS:44-343, stored as CSR: cell c owns entries
+ * [normal_offsets[c], normal_offsets[c+1]); each entry is 6 doubles: the
+ * SafeNormal'ed entry direction xyz (its w is always 0) then the SafeNormal'ed
+ * normal xyz, in insertion order).  Arrays are read during fks_create/fks_env
+ * upload only; the caller keeps ownership. */
+typedef struct {
+    fks_grid_geometry collision_map;
+    fks_grid_geometry sdf;
+    const float* sdf_values;
+    float sdf_oob_value;
+    uint32_t reserved;
+    fks_grid_geometry normals;
+    const uint32_t* normal_offsets; /* num_cells+1 entries */
+    const double* normal_entries;   /* 6 * normal_offsets[num_cells] doubles */
+} fks_environment;
+
+/* TnuvaLinkedRobot::LINKED_ROBOT_CONFIG (TNUVA:420-457); SE2/SE3 use one per axis */
+typedef struct {
+    double kp;
+    double ki;
+    double kd;
+    double integral_clamp;
+    double velocity_limit;
+    double acceleration_limit;
+    double max_sensor_noise;
+    double max_actuator_proportional_noise;
+    double max_actuator_minimum_noise;
+} fks_dof_controller;
+
+/* simple_linked_robot_model::RobotJoint */
+typedef struct {
+    int32_t parent_link;
+    int32_t child_link;
+    int32_t type; /* fks_joint_type */
+    int32_t reserved;
+    double origin[12]; /* parent link frame -> joint frame, 3x4 row-major */
+    double axis[3];
+    double limit_lower;
+    double limit_upper;
+} fks_joint_desc;
+
+/* Flattened robot.  Geometries are the robot_link_geometries vector
+ * (GetLinkGeometries): geometry g belongs to link geometry_link[g] and owns
+ * points [geometry_point_offset[g], geometry_point_offset[g+1]) of `points`
+ * (x, y, z, w per point: PointSphereGeometry POINTS with w = 1).  Allowed
+ * self-collision pairs are given as geometry indices (the indices that
+ * CheckIfSelfCollisionAllowed receives at SPCS:1008,1193).
+ *  linked: num_dofs = number of non-fixed joints, configuration = joint values
+ *  SE2:    num_dofs = 3, configuration = (x, y, theta), controllers = x, y, theta
+ *  SE3:    num_dofs = 6, configuration = 3x4 row-major pose (12 doubles),
+ *          controllers = x, y, z, rx, ry, rz (twist order, TNUVA:352-358)
+ * distance_weights: linked -> one weight per dof; SE2/SE3 -> [position, rotation]. */
+typedef struct {
+    int32_t robot_type; /* fks_robot_type */
+    int32_t num_links;
+    int32_t num_joints;
+    int32_t num_geometries;
+    int32_t num_dofs;
+    int32_t num_allowed_pairs;
+    double base_transform[12];
+    const fks_joint_desc* joints;
+    const int32_t* geometry_link;
+    const uint32_t* geometry_point_offset;
+    const double* points;
+    const int32_t* allowed_pairs;
+    const fks_dof_controller* controllers;
+    const double* distance_weights;
+} fks_robot_desc;
+
+/* SimpleParticleContactSimulator statistics counters (SPCS:392-400, 488-500) */
+typedef struct {
+    uint64_t successful_resolves;
+    uint64_t unsuccessful_resolves;
+    uint64_t free_resolves;
+    uint64_t collision_resolves;
+    uint64_t fallback_resolves;
+    uint64_t unsuccessful_env_collision_resolves;
+    uint64_t unsuccessful_self_collision_resolves;
+    uint64_t recovered_unsuccessful_resolves;
+} fks_statistics;
+
+/* Work/traffic counters of the last forward/reverse call (all particles). */
+typedef struct {
+    uint64_t particles;
+    uint64_t controller_steps;
+    uint64_t microsteps;          /* executions of the microstep loop body, SPCS:1590-1796 */
+    uint64_t resolver_iterations; /* executions of the resolver loop body, SPCS:1625-1762 */
+    uint64_t sdf_bytes;           /* algorithmic SDF/normal-grid bytes the reference would read */
+    uint64_t error_particles;
+    double kernel_ms;             /* device time of the simulation kernel (HIP events) */
+    double call_ms;               /* host wall time of the whole call */
+} fks_call_counters;
+
+typedef struct fks_context fks_context;
+
+int fks_abi_version(void);
+const char* fks_status_string(fks_status status);
+
+/* GetDefaultSolverParameters (FKS.hpp:13-16) */
+fks_status fks_default_solver_params(fks_solver_params* out);
+
+/* Make{SE2,SE3,Linked}Simulator (FKS.cpp:4-71): copies env to device `device`.
+ * The stacked-Jacobian resolver is always used (FKS.cpp:22,45,68 pass false). */
+fks_status fks_create(const fks_environment* env, const fks_solver_params* params,
+                      double simulation_controller_frequency, uint64_t prng_seed,
+                      int32_t debug_level, int32_t device, fks_context** out_ctx);
+void fks_destroy(fks_context* ctx);
+const char* fks_get_last_error(const fks_context* ctx);
+
+/* Upload/replace the robot every particle is a clone of (the immutable_robot
+ * argument of ForwardSimulateRobots, SPCS:788).  Cached until replaced. */
+fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* robot);
+/* configuration width in doubles for the current robot (linked D, SE2 3, SE3 12) */
+int32_t fks_config_width(const fks_context* ctx);
+
+/* ForwardSimulateRobots (SPCS:788): host buffers.  starts: n*W doubles;
+ * targets: num_targets*W doubles with num_targets == 1 or n (SPCS:792).
+ * Outputs (n entries each, any may be NULL except out_positions):
+ * reached configuration, collided flag (SimulationResult), microsteps,
+ * resolver iterations and FKS_PARTICLE_ERR_* bits per particle. */
+fks_status fks_forward_simulate(fks_context* ctx, const double* starts, uint64_t n,
+                                const double* targets, uint64_t num_targets,
+                                int32_t allow_contacts, double* out_positions,
+                                uint8_t* out_collided, uint32_t* out_microsteps,
+                                uint32_t* out_resolver_iterations, uint32_t* out_error_flags);
+/* ReverseSimulateRobots (SPCS:806): identical semantics (SPCS:838-841). */
+fks_status fks_reverse_simulate(fks_context* ctx, const double* starts, uint64_t n,
+                                const double* targets, uint64_t num_targets,
+                                int32_t allow_contacts, double* out_positions,
+                                uint8_t* out_collided, uint32_t* out_microsteps,
+                                uint32_t* out_resolver_iterations, uint32_t* out_error_flags);
+
+/* Same call with every buffer already in device memory of the context's GPU.
+ * first_particle_id: global id of particle 0 of this shard (the RNG stream is
+ * keyed by global id, so sharding across GPUs does not change results).
+ * stream: a hipStream_t (NULL = default stream); the call returns once the
+ * work is enqueued unless `synchronize` is non-zero. */
+fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts, uint64_t n,
+                                       const double* d_targets, uint64_t num_targets,
+                                       uint64_t first_particle_id, int32_t allow_contacts,
+                                       double* d_out_positions, uint8_t* d_out_collided,
+                                       uint32_t* d_out_microsteps,
+                                       uint32_t* d_out_resolver_iterations,
+                                       uint32_t* d_out_error_flags, void* stream,
+                                       int32_t synchronize);
+
+/* Each forward/reverse call consumes one RNG "call index" (the reference's
+ * per-thread std::mt19937_64 streams advance across calls, SPCS:850).  Ranks
+ * that shard one logical call must use the same index: set it explicitly. */
+fks_status fks_set_call_index(fks_context* ctx, uint64_t call_index);
+uint64_t fks_get_call_index(const fks_context* ctx);
+
+fks_status fks_get_statistics(const fks_context* ctx, fks_statistics* out);
+fks_status fks_reset_statistics(fks_context* ctx);
+fks_status fks_reset_generators(fks_context* ctx, uint64_t prng_seed);
+int32_t fks_get_debug_level(const fks_context* ctx);
+int32_t fks_set_debug_level(fks_context* ctx, int32_t debug_level);
+fks_status fks_get_last_call_counters(const fks_context* ctx, fks_call_counters* out);
+
+/* ---- environment preprocessing (CPU; reference SEB.cpp:21-476) ---- */
+/* OBSTACLE_CONFIG (SEB.hpp): pose as 3x4 row-major, half extents, object id > 0 */
+typedef struct {
+    double pose[12];
+    double extents[3];
+    uint32_t object_id;
+    uint32_t reserved;
+} fks_obstacle;
+
+typedef struct fks_env_handle fks_env_handle;
+
+/* BuildCompleteEnvironment(obstacles, resolution).  If `grid_origin` and
+ * `num_cells` are non-NULL the grid is that box (a fixed-size grid, e.g. 256^3);
+ * otherwise it is sized to the obstacles plus a 3-cell border (SEB.cpp:128-149). */
+fks_status fks_env_build(const fks_obstacle* obstacles, int32_t num_obstacles,
+                         double resolution, const double* grid_origin,
+                         const int64_t* num_cells, fks_env_handle** out);
+/* Fill a view whose pointers stay valid until fks_env_free. */
+fks_status fks_env_view(const fks_env_handle* env, fks_environment* out);
+void fks_env_free(fks_env_handle* env);
+
+/* Device self-test of the portable libm against the host (bit equality). */
+fks_status fks_selftest_math(int32_t device, uint64_t n, uint64_t* out_mismatches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FKS_CAPI_H */

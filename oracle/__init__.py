@@ -1,0 +1,186 @@
+"""TEST INFRASTRUCTURE ONLY — Python binding of the CPU oracle (oracle/_build/liboracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this package; it is the checker and the reported CPU baseline, never the thing
+measured or shipped.  The product (fast_kinematic_simulator_amd) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_double, c_int32, c_uint8, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+RNG_COUNTER, RNG_REFERENCE = 0, 1
+_LIB = None
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with its Makefile (g++, OpenMP)."""
+    cmd = ["make", "-C", HERE] + (["-B"] if force else [])
+    subprocess.run(cmd, check=True, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    return LIB_PATH
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        from fast_kinematic_simulator_amd import _capi as C  # struct layouts only (the ABI types)
+
+        L = ctypes.CDLL(LIB_PATH)
+        L.oracle_forward_simulate.restype = c_int32
+        L.oracle_forward_simulate.argtypes = [
+            POINTER(C.Environment), POINTER(C.SolverParams), c_double, c_uint64, c_uint64, POINTER(C.RobotDesc),
+            POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_uint64, c_int32, c_int32, c_int32, POINTER(c_double),
+            POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32), POINTER(C.Statistics),
+            POINTER(C.CallCounters)]
+        L.oracle_philox4x32_10.restype = None
+        L.oracle_philox4x32_10.argtypes = [POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]
+        L.oracle_pid_sequence.restype = None
+        L.oracle_pid_sequence.argtypes = [c_double, c_double, c_double, c_double, POINTER(c_double), POINTER(c_double), c_int32,
+                                          POINTER(c_double)]
+        L.oracle_counter_truncated_normal.restype = c_double
+        L.oracle_counter_truncated_normal.argtypes = [c_uint64, c_uint64, c_uint64, c_uint32, c_uint32, c_uint32, POINTER(c_uint32)]
+        L.oracle_qr_solve.restype = None
+        L.oracle_qr_solve.argtypes = [POINTER(c_double), c_uint64, c_uint64, POINTER(c_double), POINTER(c_double)]
+        L.oracle_estimate_distance.restype = None
+        L.oracle_estimate_distance.argtypes = [POINTER(C.Environment), POINTER(c_double), c_uint64, POINTER(c_double),
+                                               POINTER(c_uint8), POINTER(ctypes.c_float)]
+        L.oracle_link_transforms.restype = c_int32
+        L.oracle_link_transforms.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), POINTER(c_double)]
+        L.oracle_point_jacobian.restype = c_int32
+        L.oracle_point_jacobian.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), c_int32, POINTER(c_double), POINTER(c_double)]
+        L.oracle_se3_exp.restype = None
+        L.oracle_se3_exp.argtypes = [POINTER(c_double), POINTER(c_double)]
+        L.oracle_se3_log.restype = None
+        L.oracle_se3_log.argtypes = [POINTER(c_double), POINTER(c_double)]
+        L.oracle_max_threads.restype = c_int32
+        L.oracle_portable_math.restype = None
+        L.oracle_portable_math.argtypes = [c_int32, POINTER(c_double), POINTER(c_double), c_uint64, POINTER(c_double)]
+        _LIB = L
+    return _LIB
+
+
+def _p(a, t):
+    return a.ctypes.data_as(POINTER(t))
+
+
+def forward_simulate(env, robot, solver, frequency, seed, starts, targets, allow_contacts=True, call_index=0,
+                     first_particle_id=0, rng_mode=RNG_COUNTER, threads=0):
+    """ForwardSimulateRobots on the CPU oracle.  Returns a dict like the HIP path."""
+    L = lib()
+    from fast_kinematic_simulator_amd import _capi as C
+
+    W = robot.config_width
+    starts = np.ascontiguousarray(np.asarray(starts, dtype=np.float64).reshape(-1, W))
+    targets = np.ascontiguousarray(np.asarray(targets, dtype=np.float64).reshape(-1, W))
+    n = starts.shape[0]
+    env_c, keep_env = env.to_c()
+    desc, keep_robot = robot.to_c()
+    params = solver.to_c()
+    out = np.zeros((n, W))
+    coll = np.zeros(n, dtype=np.uint8)
+    micro = np.zeros(n, dtype=np.uint32)
+    res = np.zeros(n, dtype=np.uint32)
+    err = np.zeros(n, dtype=np.uint32)
+    stats = C.Statistics()
+    cc = C.CallCounters()
+    st = L.oracle_forward_simulate(ctypes.byref(env_c), ctypes.byref(params), float(frequency), c_uint64(int(seed)),
+                                   c_uint64(int(call_index)), ctypes.byref(desc), _p(starts, c_double), n,
+                                   _p(targets, c_double), targets.shape[0], int(first_particle_id), 1 if allow_contacts else 0,
+                                   int(rng_mode), int(threads), _p(out, c_double), _p(coll, c_uint8), _p(micro, c_uint32),
+                                   _p(res, c_uint32), _p(err, c_uint32), ctypes.byref(stats), ctypes.byref(cc))
+    del keep_env, keep_robot
+    if st != 0:
+        raise RuntimeError(f"oracle_forward_simulate failed ({st})")
+    return {"positions": out, "collided": coll.astype(bool), "microsteps": micro, "resolver_iterations": res, "error_flags": err,
+            "statistics": stats.as_dict(), "counters": cc.as_dict()}
+
+
+def philox(ctr, key):
+    L = lib()
+    c = np.array(ctr, dtype=np.uint32)
+    k = np.array(key, dtype=np.uint32)
+    o = np.zeros(4, dtype=np.uint32)
+    L.oracle_philox4x32_10(_p(c, c_uint32), _p(k, c_uint32), _p(o, c_uint32))
+    return [int(v) for v in o]
+
+
+def pid_sequence(kp, ki, kd, iclamp, errors, dts):
+    L = lib()
+    e = np.ascontiguousarray(errors, dtype=np.float64)
+    d = np.ascontiguousarray(dts, dtype=np.float64)
+    o = np.zeros(len(e))
+    L.oracle_pid_sequence(kp, ki, kd, iclamp, _p(e, c_double), _p(d, c_double), len(e), _p(o, c_double))
+    return o
+
+
+def truncated_normal(seed, call_index, particle, step, micro, dof):
+    err = c_uint32(0)
+    v = lib().oracle_counter_truncated_normal(seed, call_index, particle, step, micro, dof, ctypes.byref(err))
+    return v, err.value
+
+
+def qr_solve(J, b):
+    J = np.ascontiguousarray(J, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(J.shape[1])
+    lib().oracle_qr_solve(_p(J, c_double), J.shape[0], J.shape[1], _p(b, c_double), _p(x, c_double))
+    return x
+
+
+def estimate_distance(env, points):
+    pts = np.ascontiguousarray(np.asarray(points, dtype=np.float64).reshape(-1, 4))
+    env_c, keep = env.to_c()
+    d = np.zeros(len(pts))
+    inb = np.zeros(len(pts), dtype=np.uint8)
+    near = np.zeros(len(pts), dtype=np.float32)
+    lib().oracle_estimate_distance(ctypes.byref(env_c), _p(pts, c_double), len(pts), _p(d, c_double), _p(inb, c_uint8),
+                                   _p(near, ctypes.c_float))
+    return d, inb.astype(bool), near
+
+
+def link_transforms(robot, config):
+    desc, keep = robot.to_c()
+    cfg = np.ascontiguousarray(config, dtype=np.float64)
+    out = np.zeros((len(robot.geometry_points), 12))
+    lib().oracle_link_transforms(ctypes.byref(desc), _p(cfg, c_double), _p(out, c_double))
+    return out
+
+
+def point_jacobian(robot, config, geometry, point):
+    desc, keep = robot.to_c()
+    cfg = np.ascontiguousarray(config, dtype=np.float64)
+    p = np.ascontiguousarray(point, dtype=np.float64)
+    out = np.zeros(3 * robot.num_dofs)
+    lib().oracle_point_jacobian(ctypes.byref(desc), _p(cfg, c_double), int(geometry), _p(p, c_double), _p(out, c_double))
+    return out.reshape(3, robot.num_dofs)
+
+
+def se3_exp(twist):
+    t = np.ascontiguousarray(twist, dtype=np.float64)
+    o = np.zeros(12)
+    lib().oracle_se3_exp(_p(t, c_double), _p(o, c_double))
+    return o
+
+
+def se3_log(pose):
+    p = np.ascontiguousarray(pose, dtype=np.float64)
+    o = np.zeros(6)
+    lib().oracle_se3_log(_p(p, c_double), _p(o, c_double))
+    return o
+
+
+def portable_math(fn, x, y=None):
+    """fn: 0 sin, 1 cos, 2 log, 3 atan, 4 atan2(x, y), 5 wrap (include/fks_portable_math.h)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y if y is not None else np.zeros_like(x), dtype=np.float64)
+    o = np.zeros_like(x)
+    lib().oracle_portable_math(int(fn), _p(x, c_double), _p(y, c_double), len(x), _p(o, c_double))
+    return o

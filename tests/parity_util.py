@@ -1,0 +1,52 @@
+"""Helpers shared by the parity tests: run the HIP path and the CPU oracle on the
+same inputs and compare every output field exactly."""
+import numpy as np
+
+
+def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, first_particle_id=0, sim=None):
+    import oracle
+    from fast_kinematic_simulator_amd import make_linked_simulator
+
+    env = wl.environment()
+    starts = wl.starts if starts is None else starts
+    targets = wl.targets if targets is None else targets
+    allow = wl.allow_contacts if allow_contacts is None else allow_contacts
+    own = sim is None
+    if own:
+        sim = make_linked_simulator(env, wl.solver, wl.controller_frequency, wl.seed)
+    sim.set_call_index(call_index)
+    g = sim.forward_simulate_arrays(wl.robot, starts, targets, allow)
+    g["statistics"] = sim.get_statistics()
+    g["counters"] = sim.last_call_counters()
+    if own:
+        sim.close()
+    o = oracle.forward_simulate(env, wl.robot, wl.solver, wl.controller_frequency, wl.seed, starts, targets, allow,
+                                call_index=call_index, first_particle_id=first_particle_id)
+    return g, o
+
+
+def mismatch_report(g, o, limit=5):
+    lines = []
+    n = len(o["microsteps"])
+    bad = np.zeros(n, dtype=bool)
+    for k in ("collided", "microsteps", "resolver_iterations", "error_flags"):
+        bad |= np.asarray(g[k]) != np.asarray(o[k])
+    bad |= np.any(g["positions"] != o["positions"], axis=1)
+    idx = np.nonzero(bad)[0]
+    lines.append(f"{len(idx)} / {n} particles differ")
+    for i in idx[:limit]:
+        lines.append(f"  particle {i}: micro {g['microsteps'][i]} vs {o['microsteps'][i]}, resolver "
+                     f"{g['resolver_iterations'][i]} vs {o['resolver_iterations'][i]}, collided {g['collided'][i]} vs "
+                     f"{o['collided'][i]}, err {g['error_flags'][i]} vs {o['error_flags'][i]}, max|dq| "
+                     f"{np.max(np.abs(g['positions'][i] - o['positions'][i])):.3e}")
+    return "\n".join(lines)
+
+
+def assert_identical(g, o):
+    report = mismatch_report(g, o)
+    assert np.array_equal(g["collided"], o["collided"]), report
+    assert np.array_equal(g["microsteps"], o["microsteps"]), report
+    assert np.array_equal(g["resolver_iterations"], o["resolver_iterations"]), report
+    assert np.array_equal(g["error_flags"], o["error_flags"]), report
+    # joint states: bit-exact in practice; the contract (BASELINE.json) is 1e-6
+    assert np.array_equal(g["positions"], o["positions"]), report + f"\nmax |dq| {np.max(np.abs(g['positions'] - o['positions']))}"
