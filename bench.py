@@ -1,0 +1,229 @@
+"""Benchmark of the particle forward-simulation hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+A "step" is one ForwardSimulateRobots batch (SPCS:788) of the headline workload
+cfg3 (7-DOF arm, 256^3 SDF @ 1 cm, 65,536 particles x 200 controller steps) per GPU,
+inputs already resident in HBM, followed by the RCCL gather of every particle's
+outcome (reached configuration, collided flag, microstep / resolver counts, error
+bits) to rank 0.  value = particle-microsteps executed by all ranks / max-over-ranks
+wall time of the K timed steps (weak scaling: each GPU owns 65,536 particles; RNG
+streams are keyed by global particle id so shards are independent).
+
+Also reported: the dominant kernel's roofline (algorithmic SDF bytes per launch / the
+launch's HIP-event duration, against the 8 TB/s HBM peak) and the CPU baseline (the
+oracle, a C++ restatement of the reference's OpenMP path, timed on this host on a
+bounded prefix of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "particle-microsteps/sec, 7-DOF arm vs 256³ SDF, at 1/2/4/8 MI355X"
+UNIT = "particle-microsteps/s"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s spec)
+PARTICLES_PER_GPU = 65536
+
+
+def log(msg):
+    print(msg, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(wl, sample_particles: int, threads: int):
+    """The oracle in reference-RNG mode (per-OpenMP-thread mt19937_64, SPCS:431-441,
+    #pragma omp parallel for over particles, SPCS:795) on a prefix of the batch."""
+    import oracle
+
+    env = wl.environment()
+    starts = wl.starts[:sample_particles]
+    t0 = time.perf_counter()
+    r = oracle.forward_simulate(env, wl.robot, wl.solver, wl.controller_frequency, wl.seed, starts, wl.targets, True,
+                                rng_mode=oracle.RNG_REFERENCE, threads=threads)
+    dt = time.perf_counter() - t0
+    micro = int(r["counters"]["microsteps"])
+    return {"value": micro / dt, "unit": UNIT, "cores": threads, "kind": "port",
+            "sample": f"first {len(starts)} particles of cfg3 x 200 controller steps ({micro} microsteps, {dt:.1f} s), "
+                      f"oracle in reference-RNG mode, OpenMP {threads} threads"}
+
+
+def load_traffic():
+    """HBM bytes per launch of the simulation kernel from the committed rocprofv3 PMC
+    summary (profiles/*_pmc.json written by tools/profile_pmc.py), or None."""
+    path = os.path.join(ROOT, "profiles", "latest_pmc.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return float(d["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--particles", type=int, default=PARTICLES_PER_GPU, help="particles per GPU")
+    ap.add_argument("--cpu-sample", type=int, default=768, help="particles in the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from fast_kinematic_simulator_amd import make_linked_simulator
+    from fast_kinematic_simulator_amd import workloads as W
+
+    n_local = args.particles
+    wl = W.cfg3(scale=(n_local * world) / 65536.0)
+    t0 = time.perf_counter()
+    env = wl.environment()
+    log(f"[rank {rank}] environment 256^3 built in {time.perf_counter() - t0:.1f}s "
+        f"({int(env.normal_offsets[-1])} surface-normal entries)")
+    sim = make_linked_simulator(env, wl.solver, wl.controller_frequency, wl.seed, device=local_rank)
+    sim.set_robot(wl.robot)
+    Wd = wl.robot.config_width
+    lo = rank * n_local
+    dev = torch.device("cuda", local_rank)
+    starts = torch.from_numpy(np.ascontiguousarray(wl.starts[lo:lo + n_local])).to(dev)
+    targets = torch.from_numpy(np.ascontiguousarray(wl.targets)).to(dev)
+    out_q = torch.empty((n_local, Wd), dtype=torch.float64, device=dev)
+    out_coll = torch.empty(n_local, dtype=torch.uint8, device=dev)
+    out_micro = torch.empty(n_local, dtype=torch.int32, device=dev)
+    out_res = torch.empty(n_local, dtype=torch.int32, device=dev)
+    out_err = torch.empty(n_local, dtype=torch.int32, device=dev)
+    packed = torch.empty((n_local, Wd + 4), dtype=torch.float64, device=dev)
+    gathered = [torch.empty_like(packed) for _ in range(world)] if (dist and rank == 0) else None
+    micro_total = torch.zeros((), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(call_index, timed_events=None):
+        # every rank uses the same RNG call index for the same logical batch
+        sim.set_call_index(call_index)
+        if timed_events is not None:
+            timed_events[0].record(stream)
+        sim.forward_simulate_device(wl.robot, starts.data_ptr(), n_local, targets.data_ptr(), 1, lo, True, out_q.data_ptr(),
+                                    out_coll.data_ptr(), out_micro.data_ptr(), out_res.data_ptr(), out_err.data_ptr(),
+                                    stream=stream.cuda_stream, synchronize=False)
+        if timed_events is not None:
+            timed_events[1].record(stream)
+        micro_total.add_(out_micro.sum(dtype=torch.int64))
+        # outcome of every particle -> rank 0 (RCCL gather over xGMI)
+        packed[:, :Wd] = out_q
+        packed[:, Wd] = out_coll.to(torch.float64)
+        packed[:, Wd + 1] = out_micro.to(torch.float64)
+        packed[:, Wd + 2] = out_res.to(torch.float64)
+        packed[:, Wd + 3] = out_err.to(torch.float64)
+        if dist is not None:
+            dist.gather(packed, gathered, dst=0)
+
+    for w in range(args.warmup):
+        step(1000 + w)
+    torch.cuda.synchronize()
+    sim.reset_total_counters()
+    micro_total.zero_()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        step(k, events[k])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    kernel_ms = [a.elapsed_time(b) for a, b in events]
+    tot = sim.total_counters()
+    local_micro = int(micro_total.item())
+    assert local_micro == int(tot["microsteps"]), (local_micro, tot["microsteps"])
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        m = torch.tensor([local_micro], dtype=torch.int64, device=dev)
+        dist.all_reduce(m)
+        all_micro = int(m.item())
+    else:
+        all_micro = local_micro
+
+    if rank == 0:
+        calls = max(1, int(tot["calls"]))
+        avg_kernel_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3
+        bytes_per_launch = tot["sdf_bytes"] / calls
+        achieved = bytes_per_launch / avg_kernel_s / 1e9
+        traffic = load_traffic()
+        cpu = None
+        if not args.no_cpu_baseline:
+            threads = max(1, min(16, os.cpu_count() or 1))
+            t0 = time.perf_counter()
+            cpu = cpu_baseline(W.cfg3(scale=args.cpu_sample / 65536.0), args.cpu_sample, threads)
+            log(f"cpu baseline {cpu['value']:.0f} {UNIT} in {time.perf_counter() - t0:.1f}s")
+        value = all_micro / elapsed
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": UNIT,
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded cfg3 scene: table + 5 pillars, starts = nominal + U(+-0.05 rad))",
+            "config": {
+                "workload": "cfg3: 7-DOF linked arm (8 links x 64 points), 256^3 SDF @ 0.01 m, 65536 particles x 200 "
+                            "controller steps per GPU, allow_contacts, RCCL gather of outcomes to rank 0",
+                "particles_per_gpu": n_local,
+                "particles_total": n_local * world,
+                "controller_steps": wl.steps,
+                "parallelism": f"dp{world} (particle shards)",
+                "microsteps_per_step": all_micro / args.steps,
+                "mean_microsteps_per_controller_step": tot["microsteps"] / max(1, tot["controller_steps"]),
+                "resolver_iterations_per_step": tot["resolver_iterations"] / calls * world,
+                "error_particles": tot["error_particles"],
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "fks_simulate_particles",
+                "avg_kernel_ms": avg_kernel_s * 1e3,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    sim.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

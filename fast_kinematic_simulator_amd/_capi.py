@@ -141,6 +141,7 @@ class CallCounters(ctypes.Structure):
         ("error_particles", c_uint64),
         ("kernel_ms", c_double),
         ("call_ms", c_double),
+        ("calls", c_uint64),
     ]
 
     def as_dict(self):
@@ -187,6 +188,8 @@ PROTOTYPES = [
     ("fks_get_debug_level", c_int32, [c_void_p]),
     ("fks_set_debug_level", c_int32, [c_void_p, c_int32]),
     ("fks_get_last_call_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
+    ("fks_get_total_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
+    ("fks_reset_total_counters", c_int32, [c_void_p]),
     ("fks_env_build", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), POINTER(c_void_p)]),
     ("fks_env_view", c_int32, [c_void_p, POINTER(Environment)]),
     ("fks_env_free", None, [c_void_p]),

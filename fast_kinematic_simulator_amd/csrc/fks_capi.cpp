@@ -129,6 +129,7 @@ struct fks_context {
     size_t cap_particles = 0, cap_targets = 0;
     fks_statistics stats;
     fks_call_counters last;
+    fks_call_counters total;
 };
 
 template <typename T>
@@ -222,6 +223,7 @@ fks_status fks_create(const fks_environment* env, const fks_solver_params* param
     ctx->debug_level = debug_level;
     std::memset(&ctx->stats, 0, sizeof(ctx->stats));
     std::memset(&ctx->last, 0, sizeof(ctx->last));
+    std::memset(&ctx->total, 0, sizeof(ctx->total));
     auto bail = [&](hipError_t e, const char* where) {
         (void)where;
         (void)e;
@@ -504,6 +506,16 @@ static fks_status settle(fks_context* ctx) {
     HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->last.kernel_ms = (double)ms;
     ctx->last.call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ctx->call_start).count();
+    ctx->last.calls = 1;
+    ctx->total.particles += ctx->last.particles;
+    ctx->total.controller_steps += ctx->last.controller_steps;
+    ctx->total.microsteps += ctx->last.microsteps;
+    ctx->total.resolver_iterations += ctx->last.resolver_iterations;
+    ctx->total.sdf_bytes += ctx->last.sdf_bytes;
+    ctx->total.error_particles += ctx->last.error_particles;
+    ctx->total.kernel_ms += ctx->last.kernel_ms;
+    ctx->total.call_ms += ctx->last.call_ms;
+    ctx->total.calls += 1;
     return FKS_OK;
 }
 
@@ -677,6 +689,21 @@ fks_status fks_get_last_call_counters(const fks_context* ctx, fks_call_counters*
     fks_status st = settle(const_cast<fks_context*>(ctx));
     if (st != FKS_OK) return st;
     *out = ctx->last;
+    return FKS_OK;
+}
+
+fks_status fks_get_total_counters(const fks_context* ctx, fks_call_counters* out) {
+    if (!ctx || !out) return FKS_ERR_INVALID_ARGUMENT;
+    fks_status st = settle(const_cast<fks_context*>(ctx));
+    if (st != FKS_OK) return st;
+    *out = ctx->total;
+    return FKS_OK;
+}
+fks_status fks_reset_total_counters(fks_context* ctx) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    fks_status st = settle(ctx);
+    if (st != FKS_OK) return st;
+    std::memset(&ctx->total, 0, sizeof(ctx->total));
     return FKS_OK;
 }
 

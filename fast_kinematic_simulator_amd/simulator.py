@@ -122,6 +122,14 @@ class HipParticleContactSimulator:
         _capi.check(self._lib.fks_get_last_call_counters(self._ctx, ctypes.byref(c)), self._ctx, "counters")
         return c.as_dict()
 
+    def total_counters(self) -> dict:
+        c = _capi.CallCounters()
+        _capi.check(self._lib.fks_get_total_counters(self._ctx, ctypes.byref(c)), self._ctx, "counters")
+        return c.as_dict()
+
+    def reset_total_counters(self):
+        _capi.check(self._lib.fks_reset_total_counters(self._ctx), self._ctx, "counters")
+
     def set_robot(self, robot: RobotDescription):
         key = id(robot)
         if self._robot_key == key and self._robot is robot:

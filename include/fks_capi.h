@@ -197,6 +197,7 @@ typedef struct {
     uint64_t error_particles;
     double kernel_ms;             /* device time of the simulation kernel (HIP events) */
     double call_ms;               /* host wall time of the whole call */
+    uint64_t calls;               /* number of calls these counters cover */
 } fks_call_counters;
 
 typedef struct fks_context fks_context;
@@ -264,6 +265,9 @@ fks_status fks_reset_generators(fks_context* ctx, uint64_t prng_seed);
 int32_t fks_get_debug_level(const fks_context* ctx);
 int32_t fks_set_debug_level(fks_context* ctx, int32_t debug_level);
 fks_status fks_get_last_call_counters(const fks_context* ctx, fks_call_counters* out);
+/* sums over every call since fks_create / fks_reset_total_counters */
+fks_status fks_get_total_counters(const fks_context* ctx, fks_call_counters* out);
+fks_status fks_reset_total_counters(fks_context* ctx);
 
 /* ---- environment preprocessing (CPU; reference SEB.cpp:21-476) ---- */
 /* OBSTACLE_CONFIG (SEB.hpp): pose as 3x4 row-major, half extents, object id > 0 */

@@ -926,6 +926,7 @@ int oracle_forward_simulate(const fks_environment* env, const fks_solver_params*
     fks_call_counters cc;
     std::memset(&cc, 0, sizeof(cc));
     cc.particles = n;
+    cc.calls = 1;
     for (size_t i = 0; i < (size_t)n; ++i) {
         const ParticleCounters& pc = counters[i];
         stats.successful_resolves += pc.stats.successful_resolves;
