@@ -1,0 +1,56 @@
+"""Summarise rocprofv3 PMC passes of bench.py into profiles/<round>_pmc.json.
+
+Usage (after the three passes FETCH_SIZE / WRITE_SIZE / TCC_HIT_sum+TCC_MISS_sum,
+each its own `rocprofv3 --pmc ... --kernel-trace --output-format csv` run of
+`python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline`):
+
+    python tools/profile_pmc.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_tcc r01
+
+HBM traffic per launch = (FETCH_SIZE + WRITE_SIZE) x 1024 bytes, averaged over the
+kernel's dispatches.  FETCH_SIZE counts L2->fabric read requests (Infinity-Cache
+hits included, MI355X_MICROARCH.md §HBM); it is not calibrated for this kernel's
+4-8-byte gathers, so it is reported raw (no x2 streaming correction)."""
+import csv
+import json
+import os
+import sys
+
+KERNEL = "fks_simulate_particles"
+
+
+def counters(path):
+    vals = {}
+    with open(os.path.join(path, "bench_counter_collection.csv")) as f:
+        for row in csv.DictReader(f):
+            if row["Kernel_Name"] != KERNEL:
+                continue
+            vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    fetch_dir, write_dir, tcc_dir, tag = sys.argv[1:5]
+    f = counters(fetch_dir)["FETCH_SIZE"]
+    w = counters(write_dir)["WRITE_SIZE"]
+    t = counters(tcc_dir)
+    hits, misses = t["TCC_HIT_sum"], t["TCC_MISS_sum"]
+    fetch_b = sum(f) / len(f) * 1024.0
+    write_b = sum(w) / len(w) * 1024.0
+    out = {
+        "kernel": KERNEL,
+        "dispatches": len(f),
+        "fetch_bytes_per_launch": fetch_b,
+        "write_bytes_per_launch": write_b,
+        "hbm_bytes_per_launch": fetch_b + write_b,
+        "l2_hit_rate": sum(hits) / (sum(hits) + sum(misses)),
+        "note": "FETCH_SIZE/WRITE_SIZE from separate rocprofv3 --pmc passes of bench.py --steps 2 --warmup 1; raw (uncalibrated for gathers)",
+    }
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for name in (f"{tag}_pmc.json", "latest_pmc.json"):
+        with open(os.path.join(root, "profiles", name), "w") as fo:
+            json.dump(out, fo, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
