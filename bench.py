@@ -156,6 +156,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     kernel_ms = [a.elapsed_time(b) for a, b in events]
     tot = sim.total_counters()
+    phases = sim.phase_cycles(total=True)
     local_micro = int(micro_total.item())
     assert local_micro == int(tot["microsteps"]), (local_micro, tot["microsteps"])
     if dist is not None:
@@ -213,11 +214,13 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "fks_simulate_particles",
+                "kernel": "fks_simulate_linked",
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },
             "cpu_baseline": cpu,
+            # share of wave time per phase of the hot path (s_memtime cycle sums, rank 0)
+            "kernel_phases": {k: round(v / max(1, phases["particle"]), 4) for k, v in phases.items() if k != "particle"},
         }
         print(json.dumps(line), flush=True)
     sim.close()

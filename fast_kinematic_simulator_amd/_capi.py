@@ -11,7 +11,7 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uint8, c_uint32, c_uint64, c_void_p
 
 LIB_NAME = "libfks_hip.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_PATH = os.environ.get("FKS_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 FKS_OK = 0
 STATUS_NAMES = {
@@ -26,6 +26,10 @@ STATUS_NAMES = {
 
 ROBOT_LINKED, ROBOT_SE2, ROBOT_SE3 = 0, 1, 2
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_CONTINUOUS, JOINT_PRISMATIC = 0, 1, 2, 4
+
+NUM_PHASES = 12
+PHASE_NAMES = ["particle", "control", "step_setup", "micro_input", "micro_fk", "env_check", "self_check", "corrections",
+               "solve", "resolve_apply", "output", "reserved"]
 
 PARTICLE_ERR_MICROSTEP_MOTION = 0x1
 PARTICLE_ERR_NORMAL_OOB = 0x2
@@ -190,6 +194,7 @@ PROTOTYPES = [
     ("fks_get_last_call_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
     ("fks_get_total_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
     ("fks_reset_total_counters", c_int32, [c_void_p]),
+    ("fks_get_phase_cycles", c_int32, [c_void_p, c_int32, POINTER(c_uint64)]),
     ("fks_env_build", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), POINTER(c_void_p)]),
     ("fks_env_view", c_int32, [c_void_p, POINTER(Environment)]),
     ("fks_env_free", None, [c_void_p]),

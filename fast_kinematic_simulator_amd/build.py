@@ -21,8 +21,9 @@ def hipcc() -> str:
     return shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 
-def build_command(output: str) -> list:
+def build_command(output: str, defines=()) -> list:
     return [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
+            *[f"-D{d}" for d in defines],
             f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(PKG, 'csrc')}", "-x", "hip",
             *[os.path.join(PKG, s) for s in SOURCES], "-o", output]
 
@@ -47,6 +48,16 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
         print(proc.stdout)
     os.replace(tmp, target)
     return target
+
+
+def build_variant(output: str, defines) -> str:
+    """Build a tuning variant (e.g. FKS_WAVES_PER_EU=3) to a separate path; load it
+    with FKS_LIB_PATH=<output> (tools/variant_bench.py)."""
+    output = os.path.abspath(output)
+    proc = subprocess.run(build_command(output, defines), cwd=PKG, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + proc.stdout[-6000:])
+    return output
 
 
 if __name__ == "__main__":

@@ -23,10 +23,23 @@
 #include "fks_device.h"
 #include "fks_portable_math.h"
 
-extern "C" __global__ void fks_simulate_particles(fksd::SimArgs args);
+extern "C" __global__ void fks_simulate_linked(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_se2(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_se3(const fksd::SimArgs* args);
 extern "C" __global__ void fks_math_probe(const double* a, const double* b, double* out, uint64_t n);
 
 namespace {
+
+typedef void (*sim_kernel_t)(const fksd::SimArgs*);
+
+/* the simulation kernel compiled for one robot family (FKS.cpp:4-71 factories) */
+sim_kernel_t kernel_for(int robot_type) {
+    switch (robot_type) {
+        case FKS_ROBOT_SE2: return fks_simulate_se2;
+        case FKS_ROBOT_SE3: return fks_simulate_se3;
+        default: return fks_simulate_linked;
+    }
+}
 
 using fksd::GridDev;
 using fksd::JointDev;
@@ -112,8 +125,12 @@ struct fks_context {
     uint64_t scratch_per_wave = 0;
     uint32_t grid_waves = 0;
     size_t lds_bytes = 0;
-    unsigned long long* d_counters = nullptr; /* kNumCounters + queue */
+    unsigned long long* d_counters = nullptr; /* kNumCounters + queue + phase cycles */
+    uint64_t phase_last[FKS_NUM_PHASES] = {};
+    uint64_t phase_total[FKS_NUM_PHASES] = {};
     unsigned long long* h_counters = nullptr; /* pinned */
+    fksd::SimArgs* d_args = nullptr;          /* kernel arguments, read through a pointer */
+    fksd::SimArgs* h_args = nullptr;          /* pinned staging for d_args */
     bool pending = false;
     hipStream_t pending_stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -246,10 +263,12 @@ fks_status fks_create(const fks_environment* env, const fks_solver_params* param
             return bail(e, "normal entries upload");
         ctx->has_normals = 1;
     }
-    if ((e = hipMalloc((void**)&ctx->d_counters, (fksd::kNumCounters + 2) * sizeof(unsigned long long))) != hipSuccess)
+    if ((e = hipMalloc((void**)&ctx->d_counters, fksd::kCounterWords * sizeof(unsigned long long))) != hipSuccess)
         return bail(e, "counters");
-    if ((e = hipHostMalloc((void**)&ctx->h_counters, (fksd::kNumCounters + 2) * sizeof(unsigned long long), 0)) != hipSuccess)
+    if ((e = hipHostMalloc((void**)&ctx->h_counters, fksd::kCounterWords * sizeof(unsigned long long), 0)) != hipSuccess)
         return bail(e, "pinned counters");
+    if ((e = hipMalloc((void**)&ctx->d_args, sizeof(fksd::SimArgs))) != hipSuccess) return bail(e, "kernel arguments");
+    if ((e = hipHostMalloc((void**)&ctx->h_args, sizeof(fksd::SimArgs), 0)) != hipSuccess) return bail(e, "kernel arguments");
     if ((e = hipEventCreate(&ctx->ev0)) != hipSuccess) return bail(e, "event");
     if ((e = hipEventCreate(&ctx->ev1)) != hipSuccess) return bail(e, "event");
     (void)same_geometry;
@@ -269,6 +288,8 @@ void fks_destroy(fks_context* ctx) {
     if (ctx->d_nent) (void)hipFree(ctx->d_nent);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
+    if (ctx->d_args) (void)hipFree(ctx->d_args);
+    if (ctx->h_args) (void)hipHostFree(ctx->h_args);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     delete ctx;
@@ -470,7 +491,7 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     ctx->lds_bytes = (size_t)L.total * sizeof(double);
     if (ctx->lds_bytes > 64 * 1024) return fail(ctx, FKS_ERR_UNSUPPORTED, "robot too large for the LDS layout");
     int blocks_per_cu = 0;
-    HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, reinterpret_cast<const void*>(fks_simulate_particles),
+    HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, reinterpret_cast<const void*>(kernel_for(R.type)),
                                                               64, ctx->lds_bytes));
     if (blocks_per_cu < 1) return fail(ctx, FKS_ERR_UNSUPPORTED, "kernel does not fit on a CU");
     int cus = 0;
@@ -502,6 +523,10 @@ static fks_status settle(fks_context* ctx) {
     ctx->last.resolver_iterations = c[fksd::kCntResolver];
     ctx->last.sdf_bytes = c[fksd::kCntSdfBytes];
     ctx->last.error_particles = c[fksd::kCntErrorParticles];
+    for (int k = 0; k < FKS_NUM_PHASES; ++k) {
+        ctx->phase_last[k] = c[fksd::kPhaseBase + k];
+        ctx->phase_total[k] += ctx->phase_last[k];
+    }
     float ms = 0.0f;
     HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->last.kernel_ms = (double)ms;
@@ -576,13 +601,19 @@ fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts,
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, (fksd::kNumCounters + 2) * sizeof(unsigned long long), s));
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G);
+    a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P);
+    /* the previous call has settled, so the pinned staging copy is free */
+    *ctx->h_args = a;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, fksd::kCounterWords * sizeof(unsigned long long), s));
     const uint32_t grid = (uint32_t)((n < (uint64_t)ctx->grid_waves) ? (n > 0 ? n : 1) : ctx->grid_waves);
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
-    hipLaunchKernelGGL(fks_simulate_particles, dim3(grid), dim3(64), ctx->lds_bytes, s, a);
+    hipLaunchKernelGGL(kernel_for(ctx->R.type), dim3(grid), dim3(64), ctx->lds_bytes, s,
+                       static_cast<const fksd::SimArgs*>(ctx->d_args));
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_counters, ctx->d_counters, (fksd::kNumCounters + 2) * sizeof(unsigned long long),
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_counters, ctx->d_counters, fksd::kCounterWords * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, s));
     ctx->pending = true;
     ctx->pending_stream = s;
@@ -704,6 +735,15 @@ fks_status fks_reset_total_counters(fks_context* ctx) {
     fks_status st = settle(ctx);
     if (st != FKS_OK) return st;
     std::memset(&ctx->total, 0, sizeof(ctx->total));
+    std::memset(ctx->phase_total, 0, sizeof(ctx->phase_total));
+    return FKS_OK;
+}
+
+fks_status fks_get_phase_cycles(const fks_context* ctx, int which, uint64_t* out) {
+    if (!ctx || !out || (which != 0 && which != 1)) return FKS_ERR_INVALID_ARGUMENT;
+    fks_status st = settle(const_cast<fks_context*>(ctx));
+    if (st != FKS_OK) return st;
+    std::memcpy(out, which ? ctx->phase_total : ctx->phase_last, sizeof(ctx->phase_last));
     return FKS_OK;
 }
 

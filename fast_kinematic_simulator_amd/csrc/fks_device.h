@@ -10,6 +10,8 @@
  *   per-wave scratch  least-squares matrix (column-major, 3P rows x (D+1) cols),
  *                  self-collision keys / corrections / flags
  * LDS layout (one wavefront per workgroup): see LdsLayout below.
+ * The kernel reads SimArgs through a pointer to a device copy (scalar loads),
+ * never from a private copy of the kernel argument.
  */
 #ifndef FKS_DEVICE_H
 #define FKS_DEVICE_H
@@ -58,60 +60,6 @@ struct RobotDev {
     const double* geom_mass;    /* per geometry: link mass + masses of all later geometries */
     const fks_dof_controller* ctrl;
     const double* weights;
-};
-
-struct SimArgs {
-    GridDev sdf_g, nrm_g, env_g;
-    const float* sdf;
-    const uint32_t* noff;
-    const double* nent;
-    float oob;
-    int32_t has_normals;
-    RobotDev R;
-    fks_solver_params S;
-    double dt;               /* simulation_controller_interval_ = 1/frequency  (SPCS:427)   */
-    double thr_env;          /* 0 - tolerance * sdf resolution (SPCS:923, threshold 0 SPCS:424) */
-    double target_micro;     /* GetResolution() * 0.125 (SPCS:1560) */
-    double allowed_micro;    /* GetResolution() * 1.0   (SPCS:1561) */
-    double time_multiplier;  /* 1.0 / time_interval     (SPCS:1027) */
-    uint32_t T;              /* forward simulation steps (SPCS:856) */
-    uint32_t key0, key1;
-    uint32_t pad0;
-    const double* starts;
-    const double* targets;
-    uint64_t num_targets;
-    uint64_t n;
-    uint64_t first_pid;
-    int32_t allow_contacts;
-    int32_t pad1;
-    double* out_q;
-    uint8_t* out_collided;
-    uint32_t* out_micro;
-    uint32_t* out_resolver;
-    uint32_t* out_err;
-    unsigned long long* counters; /* kCounter* */
-    unsigned long long* queue;
-    double* scratch;
-    uint64_t scratch_per_wave; /* doubles */
-    uint32_t row_cap;          /* 3 * P */
-    uint32_t pad2;
-};
-
-enum {
-    kCntSuccessful = 0,
-    kCntUnsuccessful,
-    kCntFree,
-    kCntCollision,
-    kCntFallback,
-    kCntUnsuccessfulEnv,
-    kCntUnsuccessfulSelf,
-    kCntRecovered,
-    kCntSteps,
-    kCntMicrosteps,
-    kCntResolver,
-    kCntSdfBytes,
-    kCntErrorParticles,
-    kNumCounters = 16
 };
 
 /* LDS carve-out (in doubles), identical on host and device */
@@ -206,6 +154,70 @@ inline
     l.total = (o + 7) & ~7ull;
     return l;
 }
+
+struct SimArgs {
+    GridDev sdf_g, nrm_g, env_g;
+    const float* sdf;
+    const uint32_t* noff;
+    const double* nent;
+    float oob;
+    int32_t has_normals;
+    RobotDev R;
+    fks_solver_params S;
+    double dt;               /* simulation_controller_interval_ = 1/frequency  (SPCS:427)   */
+    double thr_env;          /* 0 - tolerance * sdf resolution (SPCS:923, threshold 0 SPCS:424) */
+    double target_micro;     /* GetResolution() * 0.125 (SPCS:1560) */
+    double allowed_micro;    /* GetResolution() * 1.0   (SPCS:1561) */
+    double time_multiplier;  /* 1.0 / time_interval     (SPCS:1027) */
+    uint32_t T;              /* forward simulation steps (SPCS:856) */
+    uint32_t key0, key1;
+    uint32_t pad0;
+    const double* starts;
+    const double* targets;
+    uint64_t num_targets;
+    uint64_t n;
+    uint64_t first_pid;
+    int32_t allow_contacts;
+    int32_t pad1;
+    double* out_q;
+    uint8_t* out_collided;
+    uint32_t* out_micro;
+    uint32_t* out_resolver;
+    uint32_t* out_err;
+    unsigned long long* counters; /* kCounter* */
+    unsigned long long* queue;
+    double* scratch;
+    uint64_t scratch_per_wave; /* doubles */
+    uint32_t row_cap;          /* 3 * P */
+    uint32_t pad2;
+    LdsLayout L;               /* per-wave LDS carve-out */
+    uint32_t pad3;
+    ScratchLayout SL;          /* per-wave scratch carve-out */
+};
+
+enum {
+    kCntSuccessful = 0,
+    kCntUnsuccessful,
+    kCntFree,
+    kCntCollision,
+    kCntFallback,
+    kCntUnsuccessfulEnv,
+    kCntUnsuccessfulSelf,
+    kCntRecovered,
+    kCntSteps,
+    kCntMicrosteps,
+    kCntResolver,
+    kCntSdfBytes,
+    kCntErrorParticles,
+    kNumCounters = 16
+};
+
+/* per-phase s_memtime cycle sums (lane 0 of every wave), after the counters and the
+ * particle queue in the counter buffer; order = FKS_PHASE_* in fks_capi.h */
+enum {
+    kPhaseBase = kNumCounters + 2,
+    kCounterWords = kPhaseBase + FKS_NUM_PHASES
+};
 
 }  // namespace fksd
 

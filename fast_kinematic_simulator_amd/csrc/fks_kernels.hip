@@ -307,7 +307,6 @@ struct Sim {
     const SimArgs* A;
     double* lds;
     int32_t* ldsi;
-    LdsLayout L;
     double* scratch;
     int lane;
     uint64_t pid;
@@ -315,10 +314,16 @@ struct Sim {
     uint32_t err;          /* per-lane error bits, OR-reduced at decision points */
     uint64_t lane_bytes;   /* per-lane algorithmic SDF bytes */
     uint64_t micro_count, resolver_count, step_count;
-    uint32_t stats[8];
+    uint32_t* stats; /* LDS, lane 0 updates */
+    uint64_t* phase; /* LDS, FKS_NUM_PHASES cycle sums, lane 0 updates */
     double pid_integral, pid_last; /* DOF lanes */
     bool self_nonempty;
 };
+
+__device__ __forceinline__ uint64_t tick() { return __builtin_amdgcn_s_memtime(); }
+__device__ __forceinline__ void tock(Sim& s, int phase, uint64_t t0) {
+    if (s.lane == 0) s.phase[phase] += tick() - t0;
+}
 
 /* sdf_tools EstimateDistance4d (same spec as oracle SDF::EstimateDistance4d) */
 __device__ double estimate_distance(const SimArgs& A, const D4& p, bool* inb, uint64_t* bytes) {
@@ -393,11 +398,12 @@ __device__ __forceinline__ D4 load_point(const RobotDev& R, int i) {
 }
 
 /* ---------------- forward kinematics: cfg (LDS) -> link transforms T (LDS) ---------------- */
+template <int RT>
 __device__ void fk(Sim& s, const double* cfg, double* T) {
     const RobotDev& R = s.A->R;
     const int ln = s.lane;
-    if (R.type == FKS_ROBOT_LINKED) {
-        double* jm = s.lds + s.L.jm;
+    if constexpr (RT == FKS_ROBOT_LINKED) {
+        double* jm = s.lds + s.A->L.jm;
         if (ln < R.J) {
             const JointDev& jd = R.joints[ln];
             if (jd.type == FKS_JOINT_REVOLUTE || jd.type == FKS_JOINT_CONTINUOUS) {
@@ -446,7 +452,7 @@ __device__ void fk(Sim& s, const double* cfg, double* T) {
             }
             wsync();
         }
-    } else if (R.type == FKS_ROBOT_SE2) {
+    } else if constexpr (RT == FKS_ROBOT_SE2) {
         double M[12];
         angle_axis34(cfg[2], 0.0, 0.0, 1.0, M);
         M[3] = cfg[0];
@@ -462,11 +468,12 @@ __device__ void fk(Sim& s, const double* cfg, double* T) {
 
 /* ---------------- robot control-input application (TNUVA ApplyControlInput) ----------------
  * cfg_out = apply(cfg_in, input) with clamp (+ noise if noisy).  Lane d < D owns dof d. */
+template <int RT>
 __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, double* cfg_out, bool noisy, uint32_t micro) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const int ln = s.lane;
-    if (R.type == FKS_ROBOT_LINKED) {
+    if constexpr (RT == FKS_ROBOT_LINKED) {
         if (ln < R.D) {
             const fks_dof_controller& ct = R.ctrl[ln];
             const double vmax = dabs(ct.velocity_limit);
@@ -490,7 +497,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
             cfg_out[ln] = v;
         }
         wsync();
-    } else if (R.type == FKS_ROBOT_SE2) {
+    } else if constexpr (RT == FKS_ROBOT_SE2) {
         if (ln < 3) {
             const fks_dof_controller& ct = R.ctrl[ln];
             const double vmax = dabs(ct.velocity_limit);
@@ -507,7 +514,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
         }
         wsync();
     } else {
-        double* tw = s.lds + s.L.misc; /* 6 doubles */
+        double* tw = s.lds + s.A->L.misc; /* 6 doubles */
         if (ln < 6) {
             const fks_dof_controller& ct = R.ctrl[ln];
             const double vmax = dabs(ct.velocity_limit);
@@ -534,12 +541,13 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
 }
 
 /* GenerateControlAction (TNUVA:179-198, 384-412, 598-614): lane d < D returns u_d */
+template <int RT>
 __device__ double control_action(Sim& s, const double* cfg, const double* target) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const int ln = s.lane;
     double err = 0.0;
-    if (R.type == FKS_ROBOT_LINKED) {
+    if constexpr (RT == FKS_ROBOT_LINKED) {
         if (ln < R.D) {
             const JointDev& jd = R.joints[R.dof_joint[ln]];
             if (jd.type == FKS_JOINT_CONTINUOUS)
@@ -547,7 +555,7 @@ __device__ double control_action(Sim& s, const double* cfg, const double* target
             else
                 err = target[ln] - cfg[ln];
         }
-    } else if (R.type == FKS_ROBOT_SE2) {
+    } else if constexpr (RT == FKS_ROBOT_SE2) {
         if (ln < 2) err = target[ln] - cfg[ln];
         if (ln == 2) err = fks_math::enforce_continuous_revolute_bounds(target[2] - cfg[2]);
     } else {
@@ -583,9 +591,10 @@ __device__ double control_action(Sim& s, const double* cfg, const double* target
 }
 
 /* configuration distance for the simulation shortcut (SPCS:898) */
+template <int RT>
 __device__ double config_distance(Sim& s, const double* cfg, const double* target) {
     const RobotDev& R = s.A->R;
-    if (R.type == FKS_ROBOT_LINKED) {
+    if constexpr (RT == FKS_ROBOT_LINKED) {
         double sum = 0.0;
         for (int k = 0; k < R.D; ++k) {
             const JointDev& jd = R.joints[R.dof_joint[k]];
@@ -595,7 +604,7 @@ __device__ double config_distance(Sim& s, const double* cfg, const double* targe
             sum = sum + d * d;
         }
         return dsqrt(sum);
-    } else if (R.type == FKS_ROBOT_SE2) {
+    } else if constexpr (RT == FKS_ROBOT_SE2) {
         const double dx = target[0] - cfg[0];
         const double dy = target[1] - cfg[1];
         const double dr = fks_math::enforce_continuous_revolute_bounds(target[2] - cfg[2]);
@@ -719,14 +728,16 @@ __device__ void dense_inverse(const double* A, int n, double* aug, double* inv) 
 /* ExtractSelfCollidingPoints for one cell on lane 0.  members: point indices of
  * the cell in ascending order.  Writes corrections + flags into scratch; returns
  * true if the cell is a colliding cell (link_collisions.size() >= 2). */
-__device__ bool extract_cell(Sim& s, const double* Tp, const double* Tc, const int32_t* members, int nm, uint32_t* cells) {
-    const SimArgs& A = *s.A;
+__device__ __noinline__ uint32_t extract_cell(const SimArgs* __restrict__ Ap, double* scratch, const double* Tp, const double* Tc,
+                                              const int32_t* members, int nm, uint32_t* cells) {
+    const SimArgs& A = *Ap;
+    uint32_t err = 0;
     const RobotDev& R = A.R;
-    const ScratchLayout SL = make_scratch_layout(A.row_cap, R.D, R.P);
-    double* corr = s.scratch + SL.corr;
-    double* flag = s.scratch + SL.flag;
-    double* dense = s.scratch + SL.dense;
-    if (nm <= 1) return false;
+    const ScratchLayout& SL = A.SL;
+    double* corr = scratch + SL.corr;
+    double* flag = scratch + SL.flag;
+    double* dense = scratch + SL.dense;
+    if (nm <= 1) return 0;
     /* by_link: geometries present (ascending), ranges into members */
     int geo[kMaxGeoms];
     int gbeg[kMaxGeoms], gend[kMaxGeoms];
@@ -741,7 +752,7 @@ __device__ bool extract_cell(Sim& s, const double* Tp, const double* Tc, const i
         }
         gend[ng - 1] = m + 1;
     }
-    if (ng < 2) return false;
+    if (ng < 2) return 0;
     /* link_collisions: for each present geometry, the present geometries it may not touch */
     uint64_t present = 0;
     for (int a = 0; a < ng; ++a) present |= 1ull << geo[a];
@@ -750,11 +761,10 @@ __device__ bool extract_cell(Sim& s, const double* Tp, const double* Tc, const i
         const uint64_t disallowed = present & ~R.allowed_mask[geo[a]] & ~(1ull << geo[a]);
         if (disallowed) ncollide_links++;
     }
-    if (ncollide_links < 2) return false;
+    if (ncollide_links < 2) return 0;
     (*cells)++;
     if (*cells > FKS_MAX_SELF_CELLS || ng > FKS_MAX_SELF_LINKS) {
-        s.err |= FKS_PARTICLE_ERR_SELF_CAPACITY;
-        return true;
+        return FKS_PARTICLE_ERR_SELF_CAPACITY;
     }
     const double tm = A.time_multiplier;
     D4 mom[FKS_MAX_SELF_LINKS];
@@ -850,7 +860,7 @@ __device__ bool extract_cell(Sim& s, const double* Tp, const double* Tc, const i
         const double np = cnt;
         for (int m = gbeg[a]; m < gend[a]; ++m) {
             const D3 pc{corr3.x / np, corr3.y / np, corr3.z / np};
-            if (pc.x != pc.x || pc.y != pc.y || pc.z != pc.z) s.err |= FKS_PARTICLE_ERR_SELF_SINGULAR;
+            if (pc.x != pc.x || pc.y != pc.y || pc.z != pc.z) err |= FKS_PARTICLE_ERR_SELF_SINGULAR;
             const int pi = members[m];
             corr[3 * pi + 0] = pc.x;
             corr[3 * pi + 1] = pc.y;
@@ -858,8 +868,11 @@ __device__ bool extract_cell(Sim& s, const double* Tp, const double* Tc, const i
             flag[pi] = 1.0;
         }
     }
-    return true;
+    return err;
 }
+
+__device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict__ Ap, double* lds, double* scratch, int ln,
+                                                       uint32_t err, const double* Tp, const double* Tc);
 
 /* CollectSelfCollisions: returns whether the self-collision map is non-empty */
 __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
@@ -867,7 +880,7 @@ __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
     const RobotDev& R = A.R;
     const int ln = s.lane;
     if (!R.self_possible) return false;
-    double* box = s.lds + s.L.box;
+    double* box = s.lds + s.A->L.box;
     bool bad = false;
     if (ln < R.G) {
         const double* gb = R.geom_box + 7 * ln;
@@ -914,13 +927,24 @@ __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
         any = any || ov;
     }
     if (!wave_any(any || bad)) return false;
+    const uint32_t r = self_collisions_exact(s.A, s.lds, s.scratch, ln, s.err, Tp, Tc);
+    s.err = r >> 1;
+    return (r & 1u) != 0u;
+}
 
+/* exact extended-cell comparison for geometry pairs whose boxes overlap, then the
+ * impulse solve of every colliding cell (out of line: rare) */
+__device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict__ Ap, double* lds, double* scratch, int ln,
+                                                       uint32_t err, const double* Tp, const double* Tc) {
+    const SimArgs& A = *Ap;
+    const RobotDev& R = A.R;
+    const double* box = lds + A.L.box;
     /* exact path: extended cell keys of every point (SPCS:1173-1181: division, trunc) */
-    const ScratchLayout SL = make_scratch_layout(A.row_cap, R.D, R.P);
-    int64_t* keys = reinterpret_cast<int64_t*>(s.scratch + SL.keys);
-    double* flag = s.scratch + SL.flag;
-    double* cand = s.scratch + SL.cand;
-    int32_t* list = reinterpret_cast<int32_t*>(s.scratch + SL.list);
+    const ScratchLayout& SL = A.SL;
+    int64_t* keys = reinterpret_cast<int64_t*>(scratch + SL.keys);
+    double* flag = scratch + SL.flag;
+    double* cand = scratch + SL.cand;
+    int32_t* list = reinterpret_cast<int32_t*>(scratch + SL.list);
     for (int i = ln; i < R.P; i += kWave) {
         const D4 p = load_point(R, i);
         const int link = R.geom_link[R.point_geom[i]];
@@ -930,7 +954,7 @@ __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
         for (int a = 0; a < 3; ++a) {
             int64_t k;
             if (q[a] != q[a] || q[a] == __builtin_huge_val() || q[a] == -__builtin_huge_val()) {
-                s.err |= FKS_PARTICLE_ERR_KEY_RANGE;
+                err |= FKS_PARTICLE_ERR_KEY_RANGE;
                 k = 0;
             } else if (q[a] >= 9.0e18) {
                 k = (int64_t)9000000000000000000ll;
@@ -962,7 +986,7 @@ __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
     }
     wsync();
     /* process each candidate cell once */
-    uint32_t* ui = reinterpret_cast<uint32_t*>(s.ldsi + 2 * kMaxDofs); /* spare int words */
+    uint32_t* ui = reinterpret_cast<uint32_t*>(reinterpret_cast<int32_t*>(lds + A.L.ints) + 2 * kMaxDofs); /* spare int words */
     if (ln == 0) {
         ui[0] = 0; /* colliding cells */
         ui[1] = 0; /* any corrected point */
@@ -992,37 +1016,44 @@ __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
             }
             wsync();
             if (ln == 0) {
-                uint32_t cells = ui[0];
-                extract_cell(s, Tp, Tc, list, count, &cells);
-                ui[0] = cells;
+                err |= extract_cell(Ap, scratch, Tp, Tc, list, count, ui);
             }
             wsync();
         }
     }
     bool nonempty = false;
     for (int i = ln; i < R.P; i += kWave) nonempty = nonempty || (flag[i] != 0.0);
-    s.err = wave_or(s.err);
-    return wave_any(nonempty);
+    err = wave_or(err);
+    return (err << 1) | (wave_any(nonempty) ? 1u : 0u);
 }
 
 /* CheckCollision (SPCS:1418-1436) */
+template <int RT>
 __device__ bool check_collision(Sim& s, const double* Tp, const double* Tc) {
+    uint64_t t0 = tick();
     const bool env = env_collision(s, Tc);
-    const bool self = self_collisions(s, Tp, Tc);
+    tock(s, FKS_PHASE_ENV_CHECK, t0);
+    bool self = false;
+    if constexpr (RT == FKS_ROBOT_LINKED) {
+        t0 = tick();
+        self = self_collisions(s, Tp, Tc);
+        tock(s, FKS_PHASE_SELF_CHECK, t0);
+    }
     s.self_nonempty = self;
     return env || self;
 }
 
 /* world joint axes/origins per dof for the Jacobian (linked robots) */
+template <int RT>
 __device__ void joint_frames(Sim& s, const double* Tc) {
     const RobotDev& R = s.A->R;
     const int ln = s.lane;
-    if (R.type == FKS_ROBOT_LINKED && ln < R.D) {
+    if (RT == FKS_ROBOT_LINKED && ln < R.D) {
         const JointDev& jd = R.joints[R.dof_joint[ln]];
         const double* Tch = Tc + 12 * jd.child;
         const D3 aw = rotate(Tch, D3{jd.axis[0], jd.axis[1], jd.axis[2]});
-        double* axw = s.lds + s.L.axis_w;
-        double* orw = s.lds + s.L.orig_w;
+        double* axw = s.lds + s.A->L.axis_w;
+        double* orw = s.lds + s.A->L.orig_w;
         axw[3 * ln + 0] = aw.x;
         axw[3 * ln + 1] = aw.y;
         axw[3 * ln + 2] = aw.z;
@@ -1034,20 +1065,21 @@ __device__ void joint_frames(Sim& s, const double* Tc) {
 }
 
 /* CollectPointCorrectionsAndJacobians (SPCS:1818-1939): rows written to scratch, returns R */
+template <int RT>
 __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* Tc, const double* cfg) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const int ln = s.lane;
     const int D = R.D;
-    const ScratchLayout SL = make_scratch_layout(A.row_cap, R.D, R.P);
+    const ScratchLayout& SL = A.SL;
     double* J = s.scratch + SL.J;
     double* bv = s.scratch + SL.b;
     const double* corr = s.scratch + SL.corr;
     const double* flag = s.scratch + SL.flag;
     const uint32_t rc = A.row_cap;
-    joint_frames(s, Tc);
-    const double* axw = s.lds + s.L.axis_w;
-    const double* orw = s.lds + s.L.orig_w;
+    joint_frames<RT>(s, Tc);
+    const double* axw = s.lds + s.A->L.axis_w;
+    const double* orw = s.lds + s.A->L.orig_w;
     uint32_t rows = 0;
     for (int base = 0; base < R.P; base += kWave) {
         const int i = base + ln;
@@ -1085,7 +1117,7 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
             bv[row + 0] = pcorr.x;
             bv[row + 1] = pcorr.y;
             bv[row + 2] = pcorr.z;
-            if (R.type == FKS_ROBOT_LINKED) {
+            if constexpr (RT == FKS_ROBOT_LINKED) {
                 const uint64_t mask = R.link_dof_mask[link];
                 for (int d = 0; d < D; ++d) {
                     D3 col{0.0, 0.0, 0.0};
@@ -1103,7 +1135,7 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
                     J[(uint64_t)d * rc + row + 1] = col.y;
                     J[(uint64_t)d * rc + row + 2] = col.z;
                 }
-            } else if (R.type == FKS_ROBOT_SE2) {
+            } else if constexpr (RT == FKS_ROBOT_SE2) {
                 J[0 * rc + row + 0] = 0.0 + 1.0;
                 J[0 * rc + row + 1] = 0.0;
                 J[0 * rc + row + 2] = 0.0;
@@ -1135,18 +1167,17 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
 }
 
 /* ColPivHouseholderQR::solve (Eigen 3.2 / 3.3-beta1), rows lane-strided; x -> LDS */
-__device__ void qr_solve(Sim& s, uint32_t Rn, double* x) {
-    const SimArgs& A = *s.A;
+__device__ __noinline__ void qr_solve(const SimArgs* __restrict__ Ap, double* lds, double* scratch, int ln, uint32_t Rn, double* x) {
+    const SimArgs& A = *Ap;
     const int D = A.R.D;
-    const int ln = s.lane;
     const uint32_t rc = A.row_cap;
-    const ScratchLayout SL = make_scratch_layout(A.row_cap, A.R.D, A.R.P);
-    double* Jm = s.scratch + SL.J;
-    double* c = s.scratch + SL.b;
-    double* colsq = s.lds + s.L.colsq;
-    double* hco = s.lds + s.L.hcoef;
-    int32_t* perm = s.ldsi;
-    int32_t* transp = s.ldsi + kMaxDofs;
+    const ScratchLayout& SL = A.SL;
+    double* Jm = scratch + SL.J;
+    double* c = scratch + SL.b;
+    double* colsq = lds + A.L.colsq;
+    double* hco = lds + A.L.hcoef;
+    int32_t* perm = reinterpret_cast<int32_t*>(lds + A.L.ints);
+    int32_t* transp = perm + kMaxDofs;
     auto col = [&](int k) { return Jm + (uint64_t)k * rc; };
     /* canonical tail squared norm of column k over rows [begin, Rn) */
     auto tail_sq = [&](int k, uint32_t begin) {
@@ -1297,29 +1328,31 @@ __device__ void qr_solve(Sim& s, uint32_t Rn, double* x) {
 
 /* one controller step: ResolveForwardSimulation (SPCS:1546-1816).
  * returns 0 ok, 1 error; sets collided/failed; result config in res_cfg */
+template <int RT>
 __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg, bool allow_contacts, bool* out_collided,
                             bool* out_failed, double*& Tcur, double*& Tprev) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const int ln = s.lane;
     const int W = R.W, D = R.D;
-    double* u = s.lds + s.L.u;
-    double* ustep = s.lds + s.L.ustep;
-    double* cfg_tmp = s.lds + s.L.cfg_tmp;
-    double* cfg_prev = s.lds + s.L.cfg_prev;
-    double* cfg_act = s.lds + s.L.cfg_act;
-    double* x = s.lds + s.L.x;
-    double* real = s.lds + s.L.real;
-    double* Ttmp = s.lds + s.L.Ttmp;
-    double* cfg = s.lds + s.L.cfg_work; /* robot(immutable_robot->Clone()) SPCS:1548 */
+    double* u = s.lds + s.A->L.u;
+    double* ustep = s.lds + s.A->L.ustep;
+    double* cfg_tmp = s.lds + s.A->L.cfg_tmp;
+    double* cfg_prev = s.lds + s.A->L.cfg_prev;
+    double* cfg_act = s.lds + s.A->L.cfg_act;
+    double* x = s.lds + s.A->L.x;
+    double* real = s.lds + s.A->L.real;
+    double* Ttmp = s.lds + s.A->L.Ttmp;
+    double* cfg = s.lds + s.A->L.cfg_work; /* robot(immutable_robot->Clone()) SPCS:1548 */
     *out_collided = false;
     *out_failed = false;
+    uint64_t t0 = tick();
     if (ln < W) cfg[ln] = particle_cfg[ln];
     wsync();
     /* real_control_input = u * dt (SPCS:1549), already in u */
-    fk(s, cfg, Tcur);
-    apply_input(s, cfg, u, cfg_tmp, false, 0);
-    fk(s, cfg_tmp, Ttmp);
+    fk<RT>(s, cfg, Tcur);
+    apply_input<RT>(s, cfg, u, cfg_tmp, false, 0);
+    fk<RT>(s, cfg_tmp, Ttmp);
     const double computed_step_motion = max_point_motion(s, Tcur, Ttmp);
     const double raw_steps = __builtin_ceil(computed_step_motion / A.target_micro);
     if (!(raw_steps <= 1048576.0)) {
@@ -1330,13 +1363,14 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
     if (M < 1u) M = 1u;
     if (ln < D) ustep[ln] = u[ln] / (double)M;
     wsync();
-    apply_input(s, cfg, ustep, cfg_tmp, false, 0);
-    fk(s, cfg_tmp, Ttmp);
+    apply_input<RT>(s, cfg, ustep, cfg_tmp, false, 0);
+    fk<RT>(s, cfg_tmp, Ttmp);
     const double micro_motion = max_point_motion(s, Tcur, Ttmp);
     if (micro_motion > A.allowed_micro) {
         s.err |= FKS_PARTICLE_ERR_MICROSTEP_MOTION;
         return 1;
     }
+    tock(s, FKS_PHASE_STEP_SETUP, t0);
     bool collided = false;
     for (uint32_t micro = 0; micro < M; ++micro) {
         s.micro_count++;
@@ -1347,15 +1381,19 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
             Tcur = t;
         }
         wsync();
-        apply_input(s, cfg_prev, ustep, cfg, true, micro);
+        t0 = tick();
+        apply_input<RT>(s, cfg_prev, ustep, cfg, true, micro);
         s.err = wave_or(s.err);
+        tock(s, FKS_PHASE_MICRO_INPUT, t0);
         if (s.err) {
             if (ln < W) res_cfg[ln] = cfg_prev[ln];
             wsync();
             return 1;
         }
-        fk(s, cfg, Tcur);
-        bool in_collision = check_collision(s, Tprev, Tcur);
+        t0 = tick();
+        fk<RT>(s, cfg, Tcur);
+        tock(s, FKS_PHASE_MICRO_FK, t0);
+        bool in_collision = check_collision<RT>(s, Tprev, Tcur);
         if (s.err) return 1;
         if (in_collision) collided = true;
         if (in_collision && allow_contacts) {
@@ -1365,29 +1403,34 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
             double scaling = A.S.resolve_correction_initial_step_size;
             while (in_collision) {
                 s.resolver_count++;
-                const uint32_t Rn = collect_corrections(s, Tprev, Tcur, cfg_act);
+                t0 = tick();
+                const uint32_t Rn = collect_corrections<RT>(s, Tprev, Tcur, cfg_act);
                 s.err = wave_or(s.err);
+                tock(s, FKS_PHASE_CORRECTIONS, t0);
                 if (s.err) return 1;
-                qr_solve(s, Rn, x);
-                apply_input(s, cfg_act, x, cfg_tmp, false, 0);
-                fk(s, cfg_tmp, Ttmp);
+                t0 = tick();
+                qr_solve(s.A, s.lds, s.scratch, ln, Rn, x);
+                tock(s, FKS_PHASE_SOLVE, t0);
+                t0 = tick();
+                apply_input<RT>(s, cfg_act, x, cfg_tmp, false, 0);
+                fk<RT>(s, cfg_tmp, Ttmp);
                 const double est = max_point_motion(s, Tcur, Ttmp);
                 const double step_fraction = dmax(est / A.allowed_micro, 1.0);
                 if (ln < D) real[ln] = (x[ln] / step_fraction) * dabs(scaling);
                 wsync();
-                apply_input(s, cfg_act, real, cfg_tmp, false, 0);
+                apply_input<RT>(s, cfg_act, real, cfg_tmp, false, 0);
                 if (ln < W) cfg_act[ln] = cfg_tmp[ln];
                 wsync();
-                fk(s, cfg_act, Tcur);
-                in_collision = check_collision(s, Tprev, Tcur);
+                fk<RT>(s, cfg_act, Tcur);
+                tock(s, FKS_PHASE_RESOLVE_APPLY, t0);
+                in_collision = check_collision<RT>(s, Tprev, Tcur);
                 if (s.err) return 1;
                 iters++;
                 if (iters > A.S.max_resolver_iterations) {
-                    s.stats[kCntUnsuccessful]++;
-                    if (s.self_nonempty)
-                        s.stats[kCntUnsuccessfulSelf]++;
-                    else
-                        s.stats[kCntUnsuccessfulEnv]++;
+                    if (ln == 0) {
+                        s.stats[kCntUnsuccessful]++;
+                        s.stats[s.self_nonempty ? kCntUnsuccessfulSelf : kCntUnsuccessfulEnv]++;
+                    }
                     if (ln < W) res_cfg[ln] = cfg_prev[ln];
                     wsync();
                     *out_collided = true;
@@ -1406,18 +1449,17 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
             if (ln < W) cfg[ln] = cfg_act[ln];
             wsync();
         } else if (in_collision && !allow_contacts) {
-            s.stats[kCntSuccessful]++;
+            if (s.lane == 0) s.stats[kCntSuccessful]++;
             if (ln < W) res_cfg[ln] = cfg_prev[ln];
             wsync();
             *out_collided = true;
             return 0;
         }
     }
-    s.stats[kCntSuccessful]++;
-    if (collided)
-        s.stats[kCntCollision]++;
-    else
-        s.stats[kCntFree]++;
+    if (ln == 0) {
+        s.stats[kCntSuccessful]++;
+        s.stats[collided ? kCntCollision : kCntFree]++;
+    }
     if (ln < W) res_cfg[ln] = cfg[ln];
     wsync();
     *out_collided = collided;
@@ -1428,23 +1470,24 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
 
 using namespace fksd;
 
-extern "C" __global__ void __launch_bounds__(64) fks_simulate_particles(SimArgs args) {
-    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
-    const SimArgs& A = args;
+template <int RT>
+__device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ args, double* lds_mem) {
+    const SimArgs& A = *args;
     const RobotDev& R = A.R;
     Sim s;
-    s.A = &args;
+    s.A = args;
     s.lds = lds_mem;
-    s.L = make_lds_layout(R.L, R.J, R.D, R.W, R.G);
-    s.ldsi = reinterpret_cast<int32_t*>(lds_mem + s.L.ints);
+    s.ldsi = reinterpret_cast<int32_t*>(lds_mem + s.A->L.ints);
     s.scratch = A.scratch + (uint64_t)blockIdx.x * A.scratch_per_wave;
     s.lane = lane_id();
+    s.stats = reinterpret_cast<uint32_t*>(s.lds + s.A->L.misc + 24); /* 8 x u32 */
+    s.phase = reinterpret_cast<uint64_t*>(s.lds + s.A->L.misc + 8); /* FKS_NUM_PHASES x u64 */
     const int ln = s.lane;
     const int W = R.W, D = R.D;
-    double* cfg = s.lds + s.L.cfg;
-    double* res_cfg = s.lds + s.L.cfg_res;
-    double* u = s.lds + s.L.u;
-    unsigned long long* next_particle = reinterpret_cast<unsigned long long*>(s.lds + s.L.misc + 31);
+    double* cfg = s.lds + s.A->L.cfg;
+    double* res_cfg = s.lds + s.A->L.cfg_res;
+    double* u = s.lds + s.A->L.u;
+    unsigned long long* next_particle = reinterpret_cast<unsigned long long*>(s.lds + s.A->L.misc + 31);
     while (true) {
         if (ln == 0) *next_particle = atomicAdd(A.queue, 1ull);
         wsync();
@@ -1457,39 +1500,43 @@ extern "C" __global__ void __launch_bounds__(64) fks_simulate_particles(SimArgs 
         s.micro_count = 0;
         s.resolver_count = 0;
         s.step_count = 0;
-        for (int k = 0; k < 8; ++k) s.stats[k] = 0;
+        if (ln < 8) s.stats[ln] = 0;
+        if (ln < FKS_NUM_PHASES) s.phase[ln] = 0;
+        const uint64_t t_particle = tick();
         s.pid_integral = 0.0;
         s.pid_last = 0.0;
         s.self_nonempty = false;
         const double* start = A.starts + local * (uint64_t)W;
         const double* target = (A.num_targets == A.n) ? A.targets + local * (uint64_t)W : A.targets;
         /* ResetPosition(start): SetPosition enforces joint limits / angle wrap */
-        if (R.type == FKS_ROBOT_LINKED) {
+        if constexpr (RT == FKS_ROBOT_LINKED) {
             if (ln < D) {
                 const JointDev& jd = R.joints[R.dof_joint[ln]];
                 cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(start[ln])
                                                             : clamp(start[ln], jd.lo, jd.hi);
             }
-        } else if (R.type == FKS_ROBOT_SE2) {
+        } else if constexpr (RT == FKS_ROBOT_SE2) {
             if (ln < 3) cfg[ln] = (ln == 2) ? fks_math::enforce_continuous_revolute_bounds(start[2]) : start[ln];
         } else {
             if (ln < 12) cfg[ln] = start[ln];
         }
         wsync();
-        double* Tcur = s.lds + s.L.Tcur;
-        double* Tprev = s.lds + s.L.Tprev;
+        double* Tcur = s.lds + s.A->L.Tcur;
+        double* Tprev = s.lds + s.A->L.Tprev;
         bool collided = false;
         bool any_failed = false;
         /* ForwardSimulateMutableRobot (SPCS:843-919) */
         for (uint32_t step = 0; step < A.T; ++step) {
             s.step = step;
             s.step_count++;
-            double* tgt_lds = s.lds + s.L.tgt;
-            const double uc = control_action(s, cfg, target);
+            double* tgt_lds = s.lds + s.A->L.tgt;
+            const uint64_t t0 = tick();
+            const double uc = control_action<RT>(s, cfg, target);
             if (ln < D) u[ln] = uc * A.dt;
             wsync();
+            tock(s, FKS_PHASE_CONTROL, t0);
             bool rc = false, rf = false;
-            const int status = resolve_step(s, cfg, res_cfg, A.allow_contacts != 0, &rc, &rf, Tcur, Tprev);
+            const int status = resolve_step<RT>(s, cfg, res_cfg, A.allow_contacts != 0, &rc, &rf, Tcur, Tprev);
             s.err = wave_or(s.err);
             if (status != 0 || s.err) break;
             if (A.allow_contacts || !rc) {
@@ -1500,12 +1547,12 @@ extern "C" __global__ void __launch_bounds__(64) fks_simulate_particles(SimArgs 
                     if (A.S.failed_resolves_end_motion) break;
                     any_failed = true;
                 } else if (any_failed) {
-                    s.stats[kCntRecovered]++;
+                    if (s.lane == 0) s.stats[kCntRecovered]++;
                 }
                 if (A.S.simulation_shortcut_distance > 0.0 || A.S.simulation_shortcut_distance != A.S.simulation_shortcut_distance) {
                     if (ln < W) tgt_lds[ln] = target[ln];
                     wsync();
-                    const double dist = config_distance(s, cfg, tgt_lds);
+                    const double dist = config_distance<RT>(s, cfg, tgt_lds);
                     wsync();
                     if (dist < A.S.simulation_shortcut_distance) break;
                 }
@@ -1514,6 +1561,7 @@ extern "C" __global__ void __launch_bounds__(64) fks_simulate_particles(SimArgs 
             }
         }
         /* outputs */
+        const uint64_t t_out = tick();
         if (ln < W) A.out_q[local * (uint64_t)W + ln] = cfg[ln];
         const uint64_t bytes = wave_sum_u64(s.lane_bytes);
         if (ln == 0) {
@@ -1528,9 +1576,34 @@ extern "C" __global__ void __launch_bounds__(64) fks_simulate_particles(SimArgs 
             atomicAdd(A.counters + kCntResolver, (unsigned long long)s.resolver_count);
             atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes);
             if (s.err) atomicAdd(A.counters + kCntErrorParticles, 1ull);
+            const uint64_t t_end = tick();
+            s.phase[FKS_PHASE_OUTPUT] += t_end - t_out;
+            s.phase[FKS_PHASE_PARTICLE] += t_end - t_particle;
+            for (int k = 0; k < FKS_NUM_PHASES; ++k)
+                if (s.phase[k]) atomicAdd(A.counters + kPhaseBase + k, (unsigned long long)s.phase[k]);
         }
         wsync();
     }
+}
+
+/* one kernel per robot family so each carries only its own FK / Jacobian code.
+ * The occupancy target bounds the VGPR budget of the kernel and of its out-of-line
+ * callees (the rare self-contact path would otherwise set the budget for all). */
+#ifndef FKS_WAVES_PER_EU
+#define FKS_WAVES_PER_EU 4
+#endif
+#define FKS_KERNEL_ATTRS __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FKS_WAVES_PER_EU)))
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_LINKED>(args, lds_mem);
+}
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se2(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_SE2>(args, lds_mem);
+}
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se3(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_SE3>(args, lds_mem);
 }
 
 /* device self-test of the portable libm (fks_selftest_math) */

@@ -130,6 +130,12 @@ class HipParticleContactSimulator:
     def reset_total_counters(self):
         _capi.check(self._lib.fks_reset_total_counters(self._ctx), self._ctx, "counters")
 
+    def phase_cycles(self, total: bool = True) -> dict:
+        """Shader-clock cycles per kernel phase (fks_get_phase_cycles), summed over waves."""
+        arr = (ctypes.c_uint64 * _capi.NUM_PHASES)()
+        _capi.check(self._lib.fks_get_phase_cycles(self._ctx, 1 if total else 0, arr), self._ctx, "phase cycles")
+        return {name: int(arr[i]) for i, name in enumerate(_capi.PHASE_NAMES) if name != "reserved"}
+
     def set_robot(self, robot: RobotDescription):
         key = id(robot)
         if self._robot_key == key and self._robot is robot:

@@ -265,6 +265,27 @@ fks_status fks_reset_generators(fks_context* ctx, uint64_t prng_seed);
 int32_t fks_get_debug_level(const fks_context* ctx);
 int32_t fks_set_debug_level(fks_context* ctx, int32_t debug_level);
 fks_status fks_get_last_call_counters(const fks_context* ctx, fks_call_counters* out);
+/* Kernel phase profile: shader-clock cycles (s_memtime) spent by all waves in each
+ * phase of the hot path, summed over the particles of a call.  Diagnostic only;
+ * the phases follow the reference's call structure (SPCS line ranges). */
+#define FKS_NUM_PHASES 12
+enum fks_phase {
+    FKS_PHASE_PARTICLE = 0,        /* whole particle: ForwardSimulateMutableRobot SPCS:843-919 */
+    FKS_PHASE_CONTROL = 1,         /* controller + sensor noise SPCS:861-876 */
+    FKS_PHASE_STEP_SETUP = 2,      /* microstep count estimate SPCS:1549-1572 */
+    FKS_PHASE_MICRO_INPUT = 3,     /* ApplyControlInput incl. actuator noise SPCS:1582 */
+    FKS_PHASE_MICRO_FK = 4,        /* UpdatePosition of the microstep */
+    FKS_PHASE_ENV_CHECK = 5,       /* CheckEnvironmentCollision SPCS:1438-1459 */
+    FKS_PHASE_SELF_CHECK = 6,      /* CollectSelfCollisions SPCS:1461-1544 */
+    FKS_PHASE_CORRECTIONS = 7,     /* CollectPointCorrectionsAndJacobians SPCS:1818-1939 */
+    FKS_PHASE_SOLVE = 8,           /* ColPivHouseholderQR solve SPCS:1617-1619 */
+    FKS_PHASE_RESOLVE_APPLY = 9,   /* correction step sizing / application SPCS:1620-1656 */
+    FKS_PHASE_OUTPUT = 10,         /* reached configuration + counters */
+    FKS_PHASE_RESERVED = 11
+};
+/* which: 0 = last call, 1 = sums since fks_create / fks_reset_total_counters */
+fks_status fks_get_phase_cycles(const fks_context* ctx, int which, uint64_t* out /* FKS_NUM_PHASES */);
+
 /* sums over every call since fks_create / fks_reset_total_counters */
 fks_status fks_get_total_counters(const fks_context* ctx, fks_call_counters* out);
 fks_status fks_reset_total_counters(fks_context* ctx);

@@ -15,7 +15,7 @@ import json
 import os
 import sys
 
-KERNEL = "fks_simulate_particles"
+KERNEL = "fks_simulate_linked"
 
 
 def counters(path):

@@ -1,0 +1,34 @@
+"""Compare kernel build variants on the GPU: runs bench.py once per library.
+
+    python tools/variant_bench.py build/variants/libfks_w2.so build/variants/libfks_w4.so ...
+
+Each variant runs in its own process (FKS_LIB_PATH selects the library), one after
+another; prints one summary line per variant.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    extra = []
+    libs = []
+    for a in sys.argv[1:]:
+        (extra if a.startswith("--") or (extra and not a.endswith(".so")) else libs).append(a)
+    for lib in libs:
+        env = dict(os.environ, FKS_LIB_PATH=os.path.abspath(lib))
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1", "--no-cpu-baseline", *extra]
+        p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=900)
+        if p.returncode != 0:
+            print(f"{lib}: FAILED rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
+            sys.exit(p.returncode)
+        line = json.loads(p.stdout.strip().splitlines()[-1])
+        print(json.dumps({"lib": os.path.basename(lib), "value": line["value"], "kernel_ms": line["roofline"]["avg_kernel_ms"],
+                          "frac": line["roofline"]["frac"], "phases": line.get("kernel_phases")}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
