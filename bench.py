@@ -220,7 +220,9 @@ def main():
             },
             "cpu_baseline": cpu,
             # share of wave time per phase of the hot path (s_memtime cycle sums, rank 0)
-            "kernel_phases": {k: round(v / max(1, phases["particle"]), 4) for k, v in phases.items() if k != "particle"},
+            # (only in profiling builds of the library: -DFKS_PHASE_TIMERS=1, see tools/variant_bench.py)
+            "kernel_phases": ({k: round(v / max(1, phases["particle"]), 4) for k, v in phases.items() if k != "particle"}
+                              if phases.get("control", 0) > 0 else None),
         }
         print(json.dumps(line), flush=True)
     sim.close()

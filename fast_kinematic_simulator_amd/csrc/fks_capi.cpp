@@ -399,7 +399,7 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     R.npairs = (int32_t)(pairs.size() / 2);
     R.self_possible = !(G == 1 || (G == 2 && ((allowed[0] >> 1) & 1ull)));
     /* per point geometry, per geometry local boxes and link masses (SPCS:1244-1255) */
-    std::vector<uint16_t> point_geom(P);
+    std::vector<uint16_t> point_geom(P), point_link(P);
     std::vector<double> box(7 * (size_t)G), mass(G);
     for (int g = 0; g < G; ++g) {
         const uint32_t b0 = d->geometry_point_offset[g], b1 = d->geometry_point_offset[g + 1];
@@ -407,6 +407,7 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
         bool w_one = true;
         for (uint32_t i = b0; i < b1; ++i) {
             point_geom[i] = (uint16_t)g;
+            point_link[i] = (uint16_t)d->geometry_link[g];
             for (int a = 0; a < 3; ++a) {
                 mn[a] = std::fmin(mn[a], d->points[4 * i + a]);
                 mx[a] = std::fmax(mx[a], d->points[4 * i + a]);
@@ -457,7 +458,7 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     int32_t *dgl = nullptr, *ddj = nullptr, *dpairs = nullptr;
     uint32_t* dgo = nullptr;
     double *dpts = nullptr, *dbox = nullptr, *dmass = nullptr, *dw = nullptr;
-    uint16_t* dpg = nullptr;
+    uint16_t *dpg = nullptr, *dpl = nullptr;
     uint64_t *dlm = nullptr, *dam = nullptr;
     fks_dof_controller* dctrl = nullptr;
     HIP_TRY(ctx, up(&dj, joints.data(), joints.size()));
@@ -465,6 +466,7 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     HIP_TRY(ctx, up(&dgo, d->geometry_point_offset, (size_t)G + 1));
     HIP_TRY(ctx, up(&dpts, d->points, 4 * (size_t)P));
     HIP_TRY(ctx, up(&dpg, point_geom.data(), (size_t)P));
+    HIP_TRY(ctx, up(&dpl, point_link.data(), (size_t)P));
     HIP_TRY(ctx, up(&ddj, dof_joint.data(), dof_joint.size()));
     HIP_TRY(ctx, up(&dlm, link_mask.data(), link_mask.size()));
     HIP_TRY(ctx, up(&dpairs, pairs.data(), pairs.size()));
@@ -478,6 +480,7 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     R.geom_off = dgo;
     R.points = dpts;
     R.point_geom = dpg;
+    R.point_link = dpl;
     R.dof_joint = ddj;
     R.link_dof_mask = dlm;
     R.pairs = dpairs;

@@ -41,6 +41,9 @@ struct JointDev {
     double axis[3];
     double lo, hi;
 };
+constexpr int kJointWords = (int)(sizeof(JointDev) / 8); /* 19 */
+static_assert(sizeof(JointDev) % 8 == 0, "JointDev is copied to LDS as 64-bit words");
+constexpr int kCtrlWords = (int)(sizeof(fks_dof_controller) / 8); /* 9 */
 
 struct RobotDev {
     int32_t type, L, J, G, D, P, W, npairs;
@@ -52,6 +55,7 @@ struct RobotDev {
     const uint32_t* geom_off;
     const double* points;      /* 4 per point */
     const uint16_t* point_geom;
+    const uint16_t* point_link; /* link of each point's geometry (one load instead of two) */
     const int32_t* dof_joint;   /* linked: joint index of dof d */
     const uint64_t* link_dof_mask; /* per link: dofs whose joint child is an ancestor-or-self */
     const int32_t* pairs;       /* disallowed geometry pairs, 2 per pair (a < b) */
@@ -64,7 +68,7 @@ struct RobotDev {
 
 /* LDS carve-out (in doubles), identical on host and device */
 struct LdsLayout {
-    uint32_t Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u, ustep, x, real, axis_w,
+    uint32_t joints, ctrl, base, dofj, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u, ustep, x, real, axis_w,
         orig_w, colsq, hcoef, box, misc, ints, total;
 };
 
@@ -75,6 +79,15 @@ inline
     LdsLayout make_lds_layout(int L, int J, int D, int W, int G) {
     LdsLayout l;
     uint32_t o = 0;
+    /* per-wave copy of the robot tables the hot loops read (filled once per wave) */
+    l.joints = o;
+    o += (uint32_t)kJointWords * (J > 0 ? J : 1);
+    l.ctrl = o;
+    o += (uint32_t)kCtrlWords * (D > 0 ? D : 1);
+    l.base = o;
+    o += 12;
+    l.dofj = o; /* int32 per dof */
+    o += (uint32_t)(D + 1) / 2;
     l.Tcur = o;
     o += 12u * L;
     l.Tprev = o;
@@ -191,7 +204,6 @@ struct SimArgs {
     uint32_t row_cap;          /* 3 * P */
     uint32_t pad2;
     LdsLayout L;               /* per-wave LDS carve-out */
-    uint32_t pad3;
     ScratchLayout SL;          /* per-wave scratch carve-out */
 };
 

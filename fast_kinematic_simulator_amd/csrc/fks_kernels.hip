@@ -240,7 +240,14 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
     return v;
 }
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+/* LDS / scratch hand-off between the lanes of the wave (one wave per workgroup):
+ * a wavefront-scope fence orders the wave's own memory operations without waiting
+ * for outstanding global loads, unlike a workgroup barrier */
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 /* ---------------- RNG (same spec as oracle_rng.h) ---------------- */
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
@@ -316,13 +323,28 @@ struct Sim {
     uint64_t micro_count, resolver_count, step_count;
     uint32_t* stats; /* LDS, lane 0 updates */
     uint64_t* phase; /* LDS, FKS_NUM_PHASES cycle sums, lane 0 updates */
+    const JointDev* joints;          /* LDS copy of R.joints */
+    const fks_dof_controller* ctrl;  /* LDS copy of R.ctrl */
+    const int32_t* dofj;             /* LDS copy of R.dof_joint */
+    const double* base;              /* LDS copy of R.base */
     double pid_integral, pid_last; /* DOF lanes */
     bool self_nonempty;
+    bool tcur_valid; /* Tcur == FK(particle configuration) from the end of the last step */
 };
 
-__device__ __forceinline__ uint64_t tick() { return __builtin_amdgcn_s_memtime(); }
+/* per-phase timers (fks_get_phase_cycles) cost ~10% of wave cycles, so they are
+ * compiled in only for profiling builds (-DFKS_PHASE_TIMERS=1); the per-particle
+ * total is always kept */
+#ifndef FKS_PHASE_TIMERS
+#define FKS_PHASE_TIMERS 0
+#endif
+__device__ __forceinline__ uint64_t tick() {
+    if constexpr (FKS_PHASE_TIMERS) return __builtin_amdgcn_s_memtime();
+    return 0;
+}
 __device__ __forceinline__ void tock(Sim& s, int phase, uint64_t t0) {
-    if (s.lane == 0) s.phase[phase] += tick() - t0;
+    if constexpr (FKS_PHASE_TIMERS)
+        if (s.lane == 0) s.phase[phase] += tick() - t0;
 }
 
 /* sdf_tools EstimateDistance4d (same spec as oracle SDF::EstimateDistance4d) */
@@ -404,8 +426,9 @@ __device__ void fk(Sim& s, const double* cfg, double* T) {
     const int ln = s.lane;
     if constexpr (RT == FKS_ROBOT_LINKED) {
         double* jm = s.lds + s.A->L.jm;
+        const JointDev* JD = s.joints;
         if (ln < R.J) {
-            const JointDev& jd = R.joints[ln];
+            const JointDev& jd = JD[ln];
             if (jd.type == FKS_JOINT_REVOLUTE || jd.type == FKS_JOINT_CONTINUOUS) {
                 double M[12];
                 angle_axis34(cfg[jd.dof], jd.axis[0], jd.axis[1], jd.axis[2], M);
@@ -419,39 +442,41 @@ __device__ void fk(Sim& s, const double* cfg, double* T) {
                 for (int e = 0; e < 12; ++e) jm[12 * ln + e] = M[e];
             }
         }
-        if (ln < 12) T[ln] = R.base[ln];
         wsync();
-        const int r = ln >> 2, c = ln & 3;
-        for (int j = 0; j < R.J; ++j) {
-            const JointDev& jd = R.joints[j];
-            const int parent = jd.parent, child = jd.child, type = jd.type;
-            double Ae = 0.0;
-            if (ln < 12) {
-                const double* Tp = T + 12 * parent;
+        /* row r of a child transform depends only on row r of its parent's, so lane r
+         * walks the whole chain alone: T_child = (T_parent * origin) * motion */
+        if (ln < 3) {
+            const int r = ln;
+            const double* B = s.base + 4 * r;
+            T[4 * r + 0] = B[0];
+            T[4 * r + 1] = B[1];
+            T[4 * r + 2] = B[2];
+            T[4 * r + 3] = B[3];
+            for (int j = 0; j < R.J; ++j) {
+                const JointDev& jd = JD[j];
+                const double* Tp = T + 12 * jd.parent + 4 * r;
+                const double p0 = Tp[0], p1 = Tp[1], p2 = Tp[2], p3 = Tp[3];
                 const double* O = jd.origin;
-                if (c < 3)
-                    Ae = dot3(Tp[4 * r], Tp[4 * r + 1], Tp[4 * r + 2], O[c], O[4 + c], O[8 + c]);
-                else
-                    Ae = dot3(Tp[4 * r], Tp[4 * r + 1], Tp[4 * r + 2], O[3], O[7], O[11]) + Tp[4 * r + 3];
-            }
-            const int rb = ln & ~3;
-            const double a0 = __shfl(Ae, rb + 0, 64), a1 = __shfl(Ae, rb + 1, 64), a2 = __shfl(Ae, rb + 2, 64),
-                         a3 = __shfl(Ae, rb + 3, 64);
-            if (ln < 12) {
-                double out;
-                if (type == FKS_JOINT_FIXED) {
-                    out = Ae;
+                const double a0 = dot3(p0, p1, p2, O[0], O[4], O[8]);
+                const double a1 = dot3(p0, p1, p2, O[1], O[5], O[9]);
+                const double a2 = dot3(p0, p1, p2, O[2], O[6], O[10]);
+                const double a3 = dot3(p0, p1, p2, O[3], O[7], O[11]) + p3;
+                double* Tc = T + 12 * jd.child + 4 * r;
+                if (jd.type == FKS_JOINT_FIXED) {
+                    Tc[0] = a0;
+                    Tc[1] = a1;
+                    Tc[2] = a2;
+                    Tc[3] = a3;
                 } else {
                     const double* M = jm + 12 * j;
-                    if (c < 3)
-                        out = dot3(a0, a1, a2, M[c], M[4 + c], M[8 + c]);
-                    else
-                        out = dot3(a0, a1, a2, M[3], M[7], M[11]) + a3;
+                    Tc[0] = dot3(a0, a1, a2, M[0], M[4], M[8]);
+                    Tc[1] = dot3(a0, a1, a2, M[1], M[5], M[9]);
+                    Tc[2] = dot3(a0, a1, a2, M[2], M[6], M[10]);
+                    Tc[3] = dot3(a0, a1, a2, M[3], M[7], M[11]) + a3;
                 }
-                T[12 * child + ln] = out;
             }
-            wsync();
         }
+        wsync();
     } else if constexpr (RT == FKS_ROBOT_SE2) {
         double M[12];
         angle_axis34(cfg[2], 0.0, 0.0, 1.0, M);
@@ -475,7 +500,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
     const int ln = s.lane;
     if constexpr (RT == FKS_ROBOT_LINKED) {
         if (ln < R.D) {
-            const fks_dof_controller& ct = R.ctrl[ln];
+            const fks_dof_controller& ct = s.ctrl[ln];
             const double vmax = dabs(ct.velocity_limit);
             double real = clamp(input[ln], -vmax, vmax);
             if (noisy) {
@@ -484,7 +509,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
                 const double bound = dmax(prop, floor_noise);
                 real = real + tn_sample(A.key0, A.key1, s.pid, s.step, micro, (uint32_t)ln, &s.err) * bound;
             }
-            const JointDev& jd = R.joints[R.dof_joint[ln]];
+            const JointDev& jd = s.joints[s.dofj[ln]];
             const double raw = cfg_in[ln] + real;
             double v;
             if (jd.type == FKS_JOINT_CONTINUOUS) {
@@ -499,7 +524,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
         wsync();
     } else if constexpr (RT == FKS_ROBOT_SE2) {
         if (ln < 3) {
-            const fks_dof_controller& ct = R.ctrl[ln];
+            const fks_dof_controller& ct = s.ctrl[ln];
             const double vmax = dabs(ct.velocity_limit);
             double real = clamp(input[ln], -vmax, vmax);
             if (noisy) {
@@ -516,7 +541,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
     } else {
         double* tw = s.lds + s.A->L.misc; /* 6 doubles */
         if (ln < 6) {
-            const fks_dof_controller& ct = R.ctrl[ln];
+            const fks_dof_controller& ct = s.ctrl[ln];
             const double vmax = dabs(ct.velocity_limit);
             double real = clamp(input[ln], -vmax, vmax);
             if (noisy) {
@@ -549,7 +574,7 @@ __device__ double control_action(Sim& s, const double* cfg, const double* target
     double err = 0.0;
     if constexpr (RT == FKS_ROBOT_LINKED) {
         if (ln < R.D) {
-            const JointDev& jd = R.joints[R.dof_joint[ln]];
+            const JointDev& jd = s.joints[s.dofj[ln]];
             if (jd.type == FKS_JOINT_CONTINUOUS)
                 err = fks_math::enforce_continuous_revolute_bounds(target[ln] - cfg[ln]);
             else
@@ -574,7 +599,7 @@ __device__ double control_action(Sim& s, const double* cfg, const double* target
     }
     double u = 0.0;
     if (ln < R.D) {
-        const fks_dof_controller& ct = R.ctrl[ln];
+        const fks_dof_controller& ct = s.ctrl[ln];
         /* SimplePIDController::ComputeFeedbackTerm (PID:122-135), gains made positive (PID:104-113) */
         const double kp = dabs(ct.kp), ki = dabs(ct.ki), kd = dabs(ct.kd), iclamp = dabs(ct.integral_clamp);
         const double timestep = A.dt;
@@ -597,7 +622,7 @@ __device__ double config_distance(Sim& s, const double* cfg, const double* targe
     if constexpr (RT == FKS_ROBOT_LINKED) {
         double sum = 0.0;
         for (int k = 0; k < R.D; ++k) {
-            const JointDev& jd = R.joints[R.dof_joint[k]];
+            const JointDev& jd = s.joints[s.dofj[k]];
             const double sd = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(target[k] - cfg[k])
                                                                 : target[k] - cfg[k];
             const double d = R.weights[k] * dabs(sd);
@@ -628,9 +653,10 @@ __device__ double config_distance(Sim& s, const double* cfg, const double* targe
 __device__ double max_point_motion(Sim& s, const double* TA, const double* TB) {
     const RobotDev& R = s.A->R;
     double m = 0.0;
+#pragma unroll 2
     for (int i = s.lane; i < R.P; i += kWave) {
         const D4 p = load_point(R, i);
-        const int link = R.geom_link[R.point_geom[i]];
+        const int link = R.point_link[i];
         const D4 a = xform4(TA + 12 * link, p), b = xform4(TB + 12 * link, p);
         const double sq = sqnorm4(D4{b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w});
         if (sq > m) m = sq;
@@ -638,45 +664,55 @@ __device__ double max_point_motion(Sim& s, const double* TA, const double* TB) {
     return dsqrt(wave_max_nonneg(m));
 }
 
-/* CheckEnvironmentCollision (SPCS:921-981) with threshold 0: evaluated one
- * 64-point round at a time, stopping after the round holding the first colliding
- * point; algorithmic bytes are counted up to that point, as the reference reads */
+/* one point of CheckEnvironmentCollision: nearest-cell read, then EstimateDistance4d
+ * only where the nearest value cannot decide (SPCS:921-981, threshold 0) */
+__device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int i, uint64_t* b) {
+    const RobotDev& R = A.R;
+    if (i >= R.P) return false;
+    const D4 p = load_point(R, i);
+    const int link = R.point_link[i];
+    const D4 x = xform4(T + 12 * link, p);
+    int32_t idx[3];
+    float d = A.oob;
+    if (grid_index(A.sdf_g, x, idx)) {
+        d = A.sdf[grid_linear(A.sdf_g, idx[0], idx[1], idx[2])];
+        *b += 4;
+    }
+    const double thr = A.thr_env;
+    if ((double)d < thr) {
+        if ((double)d < thr - A.sdf_g.res) return true;
+        bool inb;
+        const double est = estimate_distance(A, x, &inb, b);
+        if (est < thr) return true;
+    }
+    return false;
+}
+
+/* CheckEnvironmentCollision (SPCS:921-981) with threshold 0: two 64-point rounds are
+ * evaluated together (their loads overlap), stopping after the pair holding the first
+ * colliding point; algorithmic bytes are counted up to that point, as the reference
+ * reads them (its loop returns at the first colliding point) */
 __device__ bool env_collision(Sim& s, const double* T) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
-    const double thr = A.thr_env;
-    const double thr2 = thr - A.sdf_g.res;
-    for (int base = 0; base < R.P; base += kWave) {
-        const int i = base + s.lane;
-        bool col = false;
-        uint64_t b = 0;
-        if (i < R.P) {
-            const D4 p = load_point(R, i);
-            const int link = R.geom_link[R.point_geom[i]];
-            const D4 x = xform4(T + 12 * link, p);
-            int32_t idx[3];
-            float d = A.oob;
-            if (grid_index(A.sdf_g, x, idx)) {
-                d = A.sdf[grid_linear(A.sdf_g, idx[0], idx[1], idx[2])];
-                b += 4;
-            }
-            if ((double)d < thr) {
-                if ((double)d < thr2) {
-                    col = true;
-                } else {
-                    bool inb;
-                    const double est = estimate_distance(A, x, &inb, &b);
-                    if (est < thr) col = true;
-                }
-            }
-        }
-        const uint64_t m = __ballot(col);
-        if (m) {
-            const int first = __ffsll((unsigned long long)m) - 1;
-            if (s.lane <= first) s.lane_bytes += b;
+    for (int base = 0; base < R.P; base += 2 * kWave) {
+        uint64_t b0 = 0, b1 = 0;
+        const bool c0 = env_point(A, T, base + s.lane, &b0);
+        const bool c1 = env_point(A, T, base + kWave + s.lane, &b1);
+        const uint64_t m0 = __ballot(c0);
+        const uint64_t m1 = __ballot(c1);
+        if (m0) {
+            const int first = __ffsll((unsigned long long)m0) - 1;
+            if (s.lane <= first) s.lane_bytes += b0;
             return true;
         }
-        s.lane_bytes += b;
+        s.lane_bytes += b0;
+        if (m1) {
+            const int first = __ffsll((unsigned long long)m1) - 1;
+            if (s.lane <= first) s.lane_bytes += b1;
+            return true;
+        }
+        s.lane_bytes += b1;
     }
     return false;
 }
@@ -947,7 +983,7 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
     int32_t* list = reinterpret_cast<int32_t*>(scratch + SL.list);
     for (int i = ln; i < R.P; i += kWave) {
         const D4 p = load_point(R, i);
-        const int link = R.geom_link[R.point_geom[i]];
+        const int link = R.point_link[i];
         const D4 x = xform4(Tc + 12 * link, p);
         const D4 g = xform4(A.env_g.inv, x);
         const double q[3] = {g.x / A.env_g.res, g.y / A.env_g.res, g.z / A.env_g.res};
@@ -1049,7 +1085,7 @@ __device__ void joint_frames(Sim& s, const double* Tc) {
     const RobotDev& R = s.A->R;
     const int ln = s.lane;
     if (RT == FKS_ROBOT_LINKED && ln < R.D) {
-        const JointDev& jd = R.joints[R.dof_joint[ln]];
+        const JointDev& jd = s.joints[s.dofj[ln]];
         const double* Tch = Tc + 12 * jd.child;
         const D3 aw = rotate(Tch, D3{jd.axis[0], jd.axis[1], jd.axis[2]});
         double* axw = s.lds + s.A->L.axis_w;
@@ -1089,7 +1125,7 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
         int link = 0;
         if (i < R.P) {
             const D4 p = load_point(R, i);
-            link = R.geom_link[R.point_geom[i]];
+            link = R.point_link[i];
             xc = xform4(Tc + 12 * link, p);
             const bool has_self = s.self_nonempty && flag[i] != 0.0;
             bool inb;
@@ -1123,7 +1159,7 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
                     D3 col{0.0, 0.0, 0.0};
                     if ((mask >> d) & 1ull) {
                         const D3 aw{axw[3 * d], axw[3 * d + 1], axw[3 * d + 2]};
-                        const int jt = R.joints[R.dof_joint[d]].type;
+                        const int jt = s.joints[s.dofj[d]].type;
                         if (jt == FKS_JOINT_PRISMATIC) {
                             col = aw;
                         } else {
@@ -1261,17 +1297,38 @@ __device__ __noinline__ void qr_solve(const SimArgs* __restrict__ Ap, double* ld
             if (ln == 0)
                 for (int j = k + 1; j < D; ++j) col(j)[k] = col(j)[k] * (1.0 - tau);
         } else if (tau != 0.0) {
-            for (int j = k + 1; j < D; ++j) {
-                double* cj = col(j);
-                double acc = 0.0;
-                for (uint32_t r = (uint32_t)ln; r < Rn; r += kWave)
-                    if (r > (uint32_t)k) acc = acc + ck[r] * cj[r];
-                double tmp = bfly_sum(acc);
-                tmp = tmp + cj[k];
+            /* columns are independent: four Householder applications at a time so their
+             * reductions overlap (same per-column arithmetic) */
+            for (int j0 = k + 1; j0 < D; j0 += 4) {
+                double acc[4] = {0.0, 0.0, 0.0, 0.0};
+                for (uint32_t r = (uint32_t)ln; r < Rn; r += kWave) {
+                    if (r > (uint32_t)k) {
+                        const double v = ck[r];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (j0 + q < D) acc[q] = acc[q] + v * col(j0 + q)[r];
+                    }
+                }
+                double tmp[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) tmp[q] = bfly_sum(acc[q]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (j0 + q < D) tmp[q] = tmp[q] + col(j0 + q)[k];
                 wsync();
-                if (ln == 0) cj[k] = cj[k] - tau * tmp;
-                for (uint32_t r = (uint32_t)ln; r < Rn; r += kWave)
-                    if (r > (uint32_t)k) cj[r] = cj[r] - (tau * ck[r]) * tmp;
+                if (ln == 0) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (j0 + q < D) col(j0 + q)[k] = col(j0 + q)[k] - tau * tmp[q];
+                }
+                for (uint32_t r = (uint32_t)ln; r < Rn; r += kWave) {
+                    if (r > (uint32_t)k) {
+                        const double tk = tau * ck[r];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (j0 + q < D) col(j0 + q)[r] = col(j0 + q)[r] - tk * tmp[q];
+                    }
+                }
                 wsync();
             }
         }
@@ -1349,8 +1406,10 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
     uint64_t t0 = tick();
     if (ln < W) cfg[ln] = particle_cfg[ln];
     wsync();
-    /* real_control_input = u * dt (SPCS:1549), already in u */
-    fk<RT>(s, cfg, Tcur);
+    /* real_control_input = u * dt (SPCS:1549), already in u.  FK of the start
+     * configuration is still in Tcur when the previous step ended normally */
+    if (!s.tcur_valid) fk<RT>(s, cfg, Tcur);
+    s.tcur_valid = false;
     apply_input<RT>(s, cfg, u, cfg_tmp, false, 0);
     fk<RT>(s, cfg_tmp, Ttmp);
     const double computed_step_motion = max_point_motion(s, Tcur, Ttmp);
@@ -1463,6 +1522,7 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
     if (ln < W) res_cfg[ln] = cfg[ln];
     wsync();
     *out_collided = collided;
+    s.tcur_valid = true;
     return 0;
 }
 
@@ -1482,6 +1542,23 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     s.lane = lane_id();
     s.stats = reinterpret_cast<uint32_t*>(s.lds + s.A->L.misc + 24); /* 8 x u32 */
     s.phase = reinterpret_cast<uint64_t*>(s.lds + s.A->L.misc + 8); /* FKS_NUM_PHASES x u64 */
+    {
+        /* per-wave copy of the robot tables read in the inner loops */
+        uint64_t* dj = reinterpret_cast<uint64_t*>(s.lds + A.L.joints);
+        const uint64_t* sj = reinterpret_cast<const uint64_t*>(R.joints);
+        for (int k = s.lane; k < R.J * kJointWords; k += kWave) dj[k] = sj[k];
+        uint64_t* dc = reinterpret_cast<uint64_t*>(s.lds + A.L.ctrl);
+        const uint64_t* sc = reinterpret_cast<const uint64_t*>(R.ctrl);
+        for (int k = s.lane; k < R.D * kCtrlWords; k += kWave) dc[k] = sc[k];
+        int32_t* dd = reinterpret_cast<int32_t*>(s.lds + A.L.dofj);
+        if (RT == FKS_ROBOT_LINKED && s.lane < R.D) dd[s.lane] = R.dof_joint[s.lane];
+        if (s.lane < 12) s.lds[A.L.base + s.lane] = R.base[s.lane];
+        s.joints = reinterpret_cast<const JointDev*>(dj);
+        s.ctrl = reinterpret_cast<const fks_dof_controller*>(dc);
+        s.dofj = dd;
+        s.base = s.lds + A.L.base;
+        wsync();
+    }
     const int ln = s.lane;
     const int W = R.W, D = R.D;
     double* cfg = s.lds + s.A->L.cfg;
@@ -1502,16 +1579,17 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         s.step_count = 0;
         if (ln < 8) s.stats[ln] = 0;
         if (ln < FKS_NUM_PHASES) s.phase[ln] = 0;
-        const uint64_t t_particle = tick();
+        const uint64_t t_particle = __builtin_amdgcn_s_memtime();
         s.pid_integral = 0.0;
         s.pid_last = 0.0;
         s.self_nonempty = false;
+        s.tcur_valid = false;
         const double* start = A.starts + local * (uint64_t)W;
         const double* target = (A.num_targets == A.n) ? A.targets + local * (uint64_t)W : A.targets;
         /* ResetPosition(start): SetPosition enforces joint limits / angle wrap */
         if constexpr (RT == FKS_ROBOT_LINKED) {
             if (ln < D) {
-                const JointDev& jd = R.joints[R.dof_joint[ln]];
+                const JointDev& jd = s.joints[s.dofj[ln]];
                 cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(start[ln])
                                                             : clamp(start[ln], jd.lo, jd.hi);
             }
@@ -1561,7 +1639,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             }
         }
         /* outputs */
-        const uint64_t t_out = tick();
+        const uint64_t t_out = __builtin_amdgcn_s_memtime();
         if (ln < W) A.out_q[local * (uint64_t)W + ln] = cfg[ln];
         const uint64_t bytes = wave_sum_u64(s.lane_bytes);
         if (ln == 0) {
@@ -1576,7 +1654,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             atomicAdd(A.counters + kCntResolver, (unsigned long long)s.resolver_count);
             atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes);
             if (s.err) atomicAdd(A.counters + kCntErrorParticles, 1ull);
-            const uint64_t t_end = tick();
+            const uint64_t t_end = __builtin_amdgcn_s_memtime();
             s.phase[FKS_PHASE_OUTPUT] += t_end - t_out;
             s.phase[FKS_PHASE_PARTICLE] += t_end - t_particle;
             for (int k = 0; k < FKS_NUM_PHASES; ++k)
