@@ -74,7 +74,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--particles", type=int, default=PARTICLES_PER_GPU, help="particles per GPU")
-    ap.add_argument("--cpu-sample", type=int, default=768, help="particles in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=2048, help="particles in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -94,8 +94,12 @@ def main():
     from fast_kinematic_simulator_amd import make_linked_simulator
     from fast_kinematic_simulator_amd import workloads as W
 
-    n_local = args.particles
-    wl = W.cfg3(scale=(n_local * world) / 65536.0)
+    from fast_kinematic_simulator_amd.sharding import gather_outcomes, pack_outcomes, shard_bounds
+
+    n_total = args.particles * world
+    lo, hi = shard_bounds(n_total, world, rank)
+    n_local = hi - lo
+    wl = W.cfg3(scale=n_total / 65536.0)
     t0 = time.perf_counter()
     env = wl.environment()
     log(f"[rank {rank}] environment 256^3 built in {time.perf_counter() - t0:.1f}s "
@@ -103,7 +107,6 @@ def main():
     sim = make_linked_simulator(env, wl.solver, wl.controller_frequency, wl.seed, device=local_rank)
     sim.set_robot(wl.robot)
     Wd = wl.robot.config_width
-    lo = rank * n_local
     dev = torch.device("cuda", local_rank)
     starts = torch.from_numpy(np.ascontiguousarray(wl.starts[lo:lo + n_local])).to(dev)
     targets = torch.from_numpy(np.ascontiguousarray(wl.targets)).to(dev)
@@ -129,13 +132,9 @@ def main():
             timed_events[1].record(stream)
         micro_total.add_(out_micro.sum(dtype=torch.int64))
         # outcome of every particle -> rank 0 (RCCL gather over xGMI)
-        packed[:, :Wd] = out_q
-        packed[:, Wd] = out_coll.to(torch.float64)
-        packed[:, Wd + 1] = out_micro.to(torch.float64)
-        packed[:, Wd + 2] = out_res.to(torch.float64)
-        packed[:, Wd + 3] = out_err.to(torch.float64)
+        pack_outcomes(out_q, out_coll, out_micro, out_res, out_err, out=packed)
         if dist is not None:
-            dist.gather(packed, gathered, dst=0)
+            gather_outcomes(packed, dist, n_total, world, rank, gathered)
 
     for w in range(args.warmup):
         step(1000 + w)
@@ -205,6 +204,7 @@ def main():
                 "microsteps_per_step": all_micro / args.steps,
                 "mean_microsteps_per_controller_step": tot["microsteps"] / max(1, tot["controller_steps"]),
                 "resolver_iterations_per_step": tot["resolver_iterations"] / calls * world,
+                "mean_least_squares_rows": tot["least_squares_rows"] / max(1, tot["resolver_iterations"]),
                 "error_particles": tot["error_particles"],
             },
             "roofline": {

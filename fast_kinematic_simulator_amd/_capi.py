@@ -146,6 +146,7 @@ class CallCounters(ctypes.Structure):
         ("kernel_ms", c_double),
         ("call_ms", c_double),
         ("calls", c_uint64),
+        ("least_squares_rows", c_uint64),
     ]
 
     def as_dict(self):

@@ -60,5 +60,24 @@ def build_variant(output: str, defines) -> str:
     return output
 
 
+def build_example(force: bool = False) -> str:
+    """Compile examples/cpp_forward_simulate.cpp (C++ host code over the C-ABI and
+    include/fast_kinematic_simulator_amd/hip_particle_contact_simulator.hpp)."""
+    lib = build_library()
+    src = os.path.join(ROOT, "examples", "cpp_forward_simulate.cpp")
+    out_dir = os.path.join(ROOT, "build")
+    os.makedirs(out_dir, exist_ok=True)
+    target = os.path.join(out_dir, "cpp_forward_simulate")
+    hdr = os.path.join(ROOT, "include", "fast_kinematic_simulator_amd", "hip_particle_contact_simulator.hpp")
+    if not force and os.path.exists(target) and all(os.path.getmtime(target) >= os.path.getmtime(p) for p in (src, hdr, lib)):
+        return target
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", f"-I{os.path.join(ROOT, 'include')}", src, "-o", target, f"-L{PKG}",
+           "-lfks_hip", "-Wl,-rpath,$ORIGIN/../fast_kinematic_simulator_amd", "-Wl,-rpath-link,/opt/rocm/lib"]
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError("g++ failed:\n" + proc.stdout[-6000:])
+    return target
+
+
 if __name__ == "__main__":
     print(build_library(force=True, verbose=True))

@@ -12,11 +12,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fks_capi.h"
@@ -101,6 +103,55 @@ bool same_geometry(const fks_grid_geometry& a, const fks_grid_geometry& b) {
 
 }  // namespace
 
+/* Lipschitz-type constants of the SDF that make a round of points provably free of
+ * contact: over axis-neighbour cell pairs, lplus = max |a - b| / res
+ * where both values are positive, cmax = max a / res over positive cells with a
+ * non-positive neighbour.  For an exact signed EDT both are 1.  Any non-finite value
+ * disables skipping. */
+static bool analyze_sdf(const float* v, int64_t nx, int64_t ny, int64_t nz, double res, double* lplus, double* cmax) {
+    const int T = (int)std::max<unsigned>(1u, std::min<unsigned>(16u, std::thread::hardware_concurrency()));
+    std::vector<double> lp(T, 0.0), cm(T, 0.0);
+    std::vector<int> bad(T, 0);
+    std::vector<std::thread> th;
+    const double inv = 1.0 / res;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t]() {
+            for (int64_t x = t; x < nx; x += T)
+                for (int64_t y = 0; y < ny; ++y)
+                    for (int64_t z = 0; z < nz; ++z) {
+                        const size_t i = ((size_t)x * ny + y) * nz + z;
+                        const double a = v[i];
+                        if (!std::isfinite(a)) {
+                            bad[t] = 1;
+                            continue;
+                        }
+                        const size_t nb[3] = {x + 1 < nx ? i + (size_t)ny * nz : i, y + 1 < ny ? i + (size_t)nz : i,
+                                              z + 1 < nz ? i + 1 : i};
+                        for (int k = 0; k < 3; ++k) {
+                            if (nb[k] == i) continue;
+                            const double b = v[nb[k]];
+                            if (!std::isfinite(b)) continue; /* flagged when visited */
+                            if (a > 0.0 && b > 0.0) {
+                                lp[t] = std::max(lp[t], std::fabs(a - b) * inv);
+                            } else if (a > 0.0) {
+                                cm[t] = std::max(cm[t], a * inv);
+                            } else if (b > 0.0) {
+                                cm[t] = std::max(cm[t], b * inv);
+                            }
+                        }
+                    }
+        });
+    for (auto& h : th) h.join();
+    *lplus = 0.0;
+    *cmax = 0.0;
+    for (int t = 0; t < T; ++t) {
+        if (bad[t]) return false;
+        *lplus = std::max(*lplus, lp[t]);
+        *cmax = std::max(*cmax, cm[t]);
+    }
+    return *lplus > 0.0;
+}
+
 struct fks_context {
     int device = 0;
     std::string last_error;
@@ -116,6 +167,8 @@ struct fks_context {
     GridDev sdf_g, nrm_g, env_g;
     float oob = 0.0f;
     int32_t has_normals = 0;
+    int32_t skip_enabled = 0;
+    double skip_lplus = 0.0, skip_cmax = 0.0;
     /* robot */
     bool has_robot = false;
     RobotDev R;
@@ -255,6 +308,15 @@ fks_status fks_create(const fks_environment* env, const fks_solver_params* param
     ctx->oob = env->sdf_oob_value;
     const size_t cells = (size_t)env->sdf.num_cells[0] * (size_t)env->sdf.num_cells[1] * (size_t)env->sdf.num_cells[2];
     if ((e = dev_upload(&ctx->d_sdf, env->sdf_values, cells)) != hipSuccess) return bail(e, "sdf upload");
+    {
+        double lp = 0.0, cm = 0.0;
+        if (analyze_sdf(env->sdf_values, env->sdf.num_cells[0], env->sdf.num_cells[1], env->sdf.num_cells[2],
+                        env->sdf.resolution, &lp, &cm)) {
+            ctx->skip_enabled = 1;
+            ctx->skip_lplus = lp * (1.0 + 1e-6) + 1e-6;
+            ctx->skip_cmax = cm * (1.0 + 1e-6) + 1e-6;
+        }
+    }
     if (env->normal_offsets && env->normal_entries) {
         const size_t ncells = (size_t)env->normals.num_cells[0] * (size_t)env->normals.num_cells[1] * (size_t)env->normals.num_cells[2];
         const size_t entries = env->normal_offsets[ncells];
@@ -423,6 +485,25 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
         }
         box[7 * g + 6] = w_one ? 1.0 : 0.0;
     }
+    /* 64-point rounds of the kernel's lane-strided loops */
+    const int NR = ((int)P + 63) / 64;
+    std::vector<fksd::RoundDev> rounds(NR > 0 ? NR : 1);
+    for (int r = 0; r < NR; ++r) {
+        fksd::RoundDev rd;
+        rd.link = -1;
+        rd.npts = std::min(64, (int)P - 64 * r);
+        rd.radius = 0.0;
+        bool uniform = true;
+        for (int i = 64 * r; i < 64 * r + rd.npts; ++i) {
+            const double* p = d->points + 4 * (size_t)i;
+            uniform = uniform && point_link[i] == point_link[64 * r] && p[3] == 1.0;
+            rd.radius = std::max(rd.radius, std::sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]));
+        }
+        if (uniform && std::isfinite(rd.radius)) rd.link = point_link[64 * r];
+        rd.radius = rd.radius * (1.0 + 1e-9) + 1e-12;
+        rounds[r] = rd;
+    }
+    R.nrounds = NR;
     double previous_link_masses = 0.0;
     for (int g = G - 1; g >= 0; --g) {
         const double link_mass = (double)(d->geometry_point_offset[g + 1] - d->geometry_point_offset[g]);
@@ -475,6 +556,8 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     HIP_TRY(ctx, up(&dmass, mass.data(), mass.size()));
     HIP_TRY(ctx, up(&dctrl, d->controllers, (size_t)R.D));
     HIP_TRY(ctx, up(&dw, weights.data(), weights.size()));
+    fksd::RoundDev* drounds = nullptr;
+    HIP_TRY(ctx, up(&drounds, rounds.data(), rounds.size()));
     R.joints = dj;
     R.geom_link = dgl;
     R.geom_off = dgo;
@@ -489,8 +572,9 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     R.geom_mass = dmass;
     R.ctrl = dctrl;
     R.weights = dw;
+    R.rounds = drounds;
     /* launch geometry: one wave per workgroup, as many resident waves as fit */
-    const fksd::LdsLayout L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G);
+    const fksd::LdsLayout L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds);
     ctx->lds_bytes = (size_t)L.total * sizeof(double);
     if (ctx->lds_bytes > 64 * 1024) return fail(ctx, FKS_ERR_UNSUPPORTED, "robot too large for the LDS layout");
     int blocks_per_cu = 0;
@@ -526,6 +610,7 @@ static fks_status settle(fks_context* ctx) {
     ctx->last.resolver_iterations = c[fksd::kCntResolver];
     ctx->last.sdf_bytes = c[fksd::kCntSdfBytes];
     ctx->last.error_particles = c[fksd::kCntErrorParticles];
+    ctx->last.least_squares_rows = c[fksd::kCntLsqRows];
     for (int k = 0; k < FKS_NUM_PHASES; ++k) {
         ctx->phase_last[k] = c[fksd::kPhaseBase + k];
         ctx->phase_total[k] += ctx->phase_last[k];
@@ -541,6 +626,7 @@ static fks_status settle(fks_context* ctx) {
     ctx->total.resolver_iterations += ctx->last.resolver_iterations;
     ctx->total.sdf_bytes += ctx->last.sdf_bytes;
     ctx->total.error_particles += ctx->last.error_particles;
+    ctx->total.least_squares_rows += ctx->last.least_squares_rows;
     ctx->total.kernel_ms += ctx->last.kernel_ms;
     ctx->total.call_ms += ctx->last.call_ms;
     ctx->total.calls += 1;
@@ -578,6 +664,9 @@ fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts,
     a.nent = ctx->d_nent;
     a.oob = ctx->oob;
     a.has_normals = ctx->has_normals;
+    a.skip_enabled = ctx->skip_enabled;
+    a.skip_lplus = ctx->skip_lplus;
+    a.skip_cmax = ctx->skip_cmax;
     a.R = ctx->R;
     a.S = ctx->params;
     a.dt = 1.0 / ctx->frequency;
@@ -604,7 +693,7 @@ fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts,
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P);
     /* the previous call has settled, so the pinned staging copy is free */
     *ctx->h_args = a;

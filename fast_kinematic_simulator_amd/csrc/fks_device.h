@@ -45,10 +45,20 @@ constexpr int kJointWords = (int)(sizeof(JointDev) / 8); /* 19 */
 static_assert(sizeof(JointDev) % 8 == 0, "JointDev is copied to LDS as 64-bit words");
 constexpr int kCtrlWords = (int)(sizeof(fks_dof_controller) / 8); /* 9 */
 
+/* a 64-point round of the lane-strided point loops: the link of all its points
+ * (-1 if mixed or any w != 1: such rounds are never skipped), point count and the
+ * largest |p_xyz| (link frame) for motion bounds */
+struct RoundDev {
+    int32_t link;
+    int32_t npts;
+    double radius;
+};
+constexpr int kRoundState = 14; /* per round in LDS: reference transform (12), min SDF value, min grid margin (cells) */
+
 struct RobotDev {
     int32_t type, L, J, G, D, P, W, npairs;
     int32_t self_possible;
-    int32_t pad;
+    int32_t nrounds;
     double base[12];
     const JointDev* joints;
     const int32_t* geom_link;
@@ -64,11 +74,12 @@ struct RobotDev {
     const double* geom_mass;    /* per geometry: link mass + masses of all later geometries */
     const fks_dof_controller* ctrl;
     const double* weights;
+    const RoundDev* rounds;
 };
 
 /* LDS carve-out (in doubles), identical on host and device */
 struct LdsLayout {
-    uint32_t joints, ctrl, base, dofj, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u, ustep, x, real, axis_w,
+    uint32_t joints, ctrl, base, dofj, rstate, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u, ustep, x, real, axis_w,
         orig_w, colsq, hcoef, box, misc, ints, total;
 };
 
@@ -76,7 +87,7 @@ inline
 #if defined(__HIPCC__)
     __host__ __device__
 #endif
-    LdsLayout make_lds_layout(int L, int J, int D, int W, int G) {
+    LdsLayout make_lds_layout(int L, int J, int D, int W, int G, int NR) {
     LdsLayout l;
     uint32_t o = 0;
     /* per-wave copy of the robot tables the hot loops read (filled once per wave) */
@@ -88,6 +99,8 @@ inline
     o += 12;
     l.dofj = o; /* int32 per dof */
     o += (uint32_t)(D + 1) / 2;
+    l.rstate = o; /* kRoundState per round, persists across the wave's particles */
+    o += (uint32_t)kRoundState * (NR > 0 ? NR : 1);
     l.Tcur = o;
     o += 12u * L;
     l.Tprev = o;
@@ -175,6 +188,12 @@ struct SimArgs {
     const double* nent;
     float oob;
     int32_t has_normals;
+    /* provably-free rounds may skip their SDF reads when the SDF
+     * satisfies: axis neighbours with positive values differ by <= lplus*res, and
+     * positive cells next to a non-positive one are <= cmax*res */
+    int32_t skip_enabled;
+    int32_t pad_skip;
+    double skip_lplus, skip_cmax;
     RobotDev R;
     fks_solver_params S;
     double dt;               /* simulation_controller_interval_ = 1/frequency  (SPCS:427)   */
@@ -221,6 +240,7 @@ enum {
     kCntResolver,
     kCntSdfBytes,
     kCntErrorParticles,
+    kCntLsqRows,
     kNumCounters = 16
 };
 

@@ -215,19 +215,48 @@ __device__ __forceinline__ void inverse34(const double* T, double* I) {
 
 /* ---------------- wave primitives ---------------- */
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63u); }
-/* canonical 64-lane sum: xor butterfly over 32,16,8,4,2,1 (oracle canon_sum) */
-__device__ __forceinline__ double bfly_sum(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
-    return v;
+/* 64-bit lane moves: DPP within rows of 16, readlane across rows */
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+constexpr int kDppXor1 = 0xB1;       /* quad_perm [1,0,3,2] */
+constexpr int kDppXor2 = 0x4E;       /* quad_perm [2,3,0,1] */
+constexpr int kDppHalfMirror = 0x141; /* lane 7-i within 8: xor 4 once quads are uniform */
+constexpr int kDppMirror = 0x140;     /* lane 15-i within 16: xor 8 once 8-groups are uniform */
+
+/* canonical 64-lane sum (oracle canon_sum): xor butterfly with offsets 1, 2, 4,
+ * 8, 16, 32; every lane gets the same value.  Call with all 64 lanes active. */
+__device__ __forceinline__ double bfly_sum(double v) {
+    v = v + dpp_f64<kDppXor1>(v);
+    v = v + dpp_f64<kDppXor2>(v);
+    v = v + dpp_f64<kDppHalfMirror>(v);
+    v = v + dpp_f64<kDppMirror>(v);
+    const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16), r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
+    return (r0 + r1) + (r2 + r3);
+}
+/* max over lanes of non-negative values (order-insensitive) */
 __device__ __forceinline__ double wave_max_nonneg(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const double o = __shfl_xor(v, off, 64);
-        v = (o > v) ? o : v;
-    }
-    return v;
+    double o = dpp_f64<kDppXor1>(v);
+    v = (o > v) ? o : v;
+    o = dpp_f64<kDppXor2>(v);
+    v = (o > v) ? o : v;
+    o = dpp_f64<kDppHalfMirror>(v);
+    v = (o > v) ? o : v;
+    o = dpp_f64<kDppMirror>(v);
+    v = (o > v) ? o : v;
+    const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16), r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
+    const double a = (r1 > r0) ? r1 : r0, b = (r3 > r2) ? r3 : r2;
+    return (b > a) ? b : a;
 }
 __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
 #pragma unroll
@@ -320,7 +349,7 @@ struct Sim {
     uint32_t step;
     uint32_t err;          /* per-lane error bits, OR-reduced at decision points */
     uint64_t lane_bytes;   /* per-lane algorithmic SDF bytes */
-    uint64_t micro_count, resolver_count, step_count;
+    uint64_t micro_count, resolver_count, step_count, lsq_rows;
     uint32_t* stats; /* LDS, lane 0 updates */
     uint64_t* phase; /* LDS, FKS_NUM_PHASES cycle sums, lane 0 updates */
     const JointDev* joints;          /* LDS copy of R.joints */
@@ -649,34 +678,163 @@ __device__ double config_distance(Sim& s, const double* cfg, const double* targe
     }
 }
 
-/* EstimateMaxControlInputWorkspaceMotion over two transform sets (SPCS:1492-1527) */
+/* ---------------- provably-free rounds ----------------
+ * Every 64-point round whose points share one link (and have w = 1) keeps, in LDS,
+ * the link transform at which it was last evaluated in full, the smallest nearest-
+ * cell SDF value of its points there and their smallest margin to the grid
+ * boundary (in cells).  A rigid motion moves each point by at most
+ * b = |dt| + ||dR||_F * radius, i.e. by at most K = sqrt(3)*b/res + 3 axis steps
+ * of cells; with the SDF constants of fks_create (positive neighbours differ by
+ * <= lplus cells, positive cells next to a non-positive one are <= cmax) a round
+ * whose cached minimum keeps every cell within K steps positive cannot collide, and
+ * one that keeps them above 0.5 + 1.5*lplus cannot produce a correction.  Skipped
+ * points are still counted in the algorithmic bytes the reference reads (their
+ * grid margin guarantees they are in bounds). */
+__device__ __forceinline__ double rigid_motion_bound(const double* T, const double* Tref, double radius) {
+    const double dt0 = T[3] - Tref[3], dt1 = T[7] - Tref[7], dt2 = T[11] - Tref[11];
+    double f = 0.0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double d = T[4 * r + c] - Tref[4 * r + c];
+            f = f + d * d;
+        }
+    const double b = dsqrt((dt0 * dt0 + dt1 * dt1) + dt2 * dt2) + dsqrt(f) * radius;
+    return b * (1.0 + 1e-9) + 1e-12;
+}
+__device__ __forceinline__ double wave_min(double v) {
+    double o = dpp_f64<kDppXor1>(v);
+    v = (o < v) ? o : v;
+    o = dpp_f64<kDppXor2>(v);
+    v = (o < v) ? o : v;
+    o = dpp_f64<kDppHalfMirror>(v);
+    v = (o < v) ? o : v;
+    o = dpp_f64<kDppMirror>(v);
+    v = (o < v) ? o : v;
+    const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16), r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
+    const double a = (r1 < r0) ? r1 : r0, b = (r3 < r2) ? r3 : r2;
+    return (b < a) ? b : a;
+}
+constexpr double kInvalidRound = -1.0e308;
+enum { kSkipCheck = 1, kSkipCorrections = 2 };
+
+/* which rounds (bit r, r < 64) may skip the env check / the correction estimate at
+ * transforms T; lane r evaluates round r */
+__device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, int what) {
+    const SimArgs& A = *s.A;
+    const RobotDev& R = A.R;
+    if (!A.skip_enabled) return 0ull;
+    bool sk = false;
+    const int ln = s.lane;
+    if (ln < R.nrounds) {
+        const RoundDev& rd = R.rounds[ln];
+        const double* st = s.lds + A.L.rstate + kRoundState * ln;
+        if (rd.link >= 0 && st[12] > kInvalidRound) {
+            const double b = rigid_motion_bound(T + 12 * rd.link, st, rd.radius) * A.sdf_g.inv_res; /* cells */
+            const double K = 1.7320508075688773 * b + 3.0;
+            const double Sr = st[12] * A.sdf_g.inv_res;
+            const double lp = A.skip_lplus;
+            const bool inb = st[13] - b > 1e-6;
+            if (what == kSkipCheck)
+                sk = inb && (Sr - A.skip_cmax) > (K - 1.0) * lp + 1e-9;
+            else
+                sk = inb && (Sr - A.skip_cmax) > K * lp + 1e-9 && (Sr - K * lp) > 0.5 + 1.5 * lp + 1e-6;
+        }
+    }
+    return __ballot(sk);
+}
+
+/* cache the state of round r after a full evaluation at T (uniform call) */
+__device__ __forceinline__ void round_update(Sim& s, int r, const double* T, double S, double G) {
+    const SimArgs& A = *s.A;
+    if (!A.skip_enabled || r >= kWave || r >= A.R.nrounds) return;
+    const RoundDev& rd = A.R.rounds[r];
+    if (rd.link < 0) return;
+    const double smin = wave_min(S), gmin = wave_min(G);
+    double* st = s.lds + A.L.rstate + kRoundState * r;
+    if (s.lane < 12) st[s.lane] = T[12 * rd.link + s.lane];
+    if (s.lane == 0) {
+        st[12] = smin;
+        st[13] = gmin;
+    }
+}
+
+/* EstimateMaxControlInputWorkspaceMotion over two transform sets (SPCS:1492-1527).
+ * The result is the exact max over all points; rounds whose rigid-motion bound
+ * cannot reach the max of the round with the largest bound are not evaluated. */
+__device__ __forceinline__ double round_max_motion(const RobotDev& R, const double* TA, const double* TB, int r, int ln) {
+    const int i = kWave * r + ln;
+    if (i >= R.P) return 0.0;
+    const D4 p = load_point(R, i);
+    const int link = R.point_link[i];
+    const D4 a = xform4(TA + 12 * link, p), b = xform4(TB + 12 * link, p);
+    return sqnorm4(D4{b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w});
+}
 __device__ double max_point_motion(Sim& s, const double* TA, const double* TB) {
     const RobotDev& R = s.A->R;
+    const int ln = s.lane;
+    const int nr = R.nrounds;
     double m = 0.0;
+    if (nr <= 2 || nr > kWave) {
 #pragma unroll 2
-    for (int i = s.lane; i < R.P; i += kWave) {
-        const D4 p = load_point(R, i);
-        const int link = R.point_link[i];
-        const D4 a = xform4(TA + 12 * link, p), b = xform4(TB + 12 * link, p);
-        const double sq = sqnorm4(D4{b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w});
+        for (int r = 0; r < nr; ++r) {
+            const double sq = round_max_motion(R, TA, TB, r, ln);
+            if (sq > m) m = sq;
+        }
+        return dsqrt(wave_max_nonneg(m));
+    }
+    double ub = 0.0;
+    if (ln < nr) {
+        const RoundDev& rd = R.rounds[ln];
+        ub = (rd.link >= 0) ? rigid_motion_bound(TB + 12 * rd.link, TA + 12 * rd.link, rd.radius) : __builtin_huge_val();
+    }
+    const double top = wave_max_nonneg(ub);
+    int rtop = __ffsll((unsigned long long)__ballot(ln < nr && ub == top)) - 1;
+    if (rtop < 0) rtop = 0; /* non-finite transforms: evaluate every round */
+    m = round_max_motion(R, TA, TB, rtop, ln);
+    const double lower = wave_max_nonneg(m);
+    uint64_t rest = __ballot(ln < nr && ln != rtop && !(ub * ub * (1.0 + 1e-9) < lower));
+    while (rest) {
+        const int r = __ffsll((unsigned long long)rest) - 1;
+        rest &= rest - 1ull;
+        const double sq = round_max_motion(R, TA, TB, r, ln);
         if (sq > m) m = sq;
     }
     return dsqrt(wave_max_nonneg(m));
 }
 
 /* one point of CheckEnvironmentCollision: nearest-cell read, then EstimateDistance4d
- * only where the nearest value cannot decide (SPCS:921-981, threshold 0) */
-__device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int i, uint64_t* b) {
+ * only where the nearest value cannot decide (SPCS:921-981, threshold 0).  Also
+ * returns the nearest value S (-inf out of bounds) and the grid margin G in cells. */
+__device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int i, uint64_t* b, double* S, double* G) {
     const RobotDev& R = A.R;
     if (i >= R.P) return false;
     const D4 p = load_point(R, i);
     const int link = R.point_link[i];
     const D4 x = xform4(T + 12 * link, p);
+    const GridDev& g = A.sdf_g;
+    const D4 q = xform4(g.inv, x);
+    const double v[3] = {q.x * g.inv_res, q.y * g.inv_res, q.z * g.inv_res};
     int32_t idx[3];
+    bool ok = true;
+    double margin = __builtin_huge_val();
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const bool fin = (v[a] > -2147483648.0) && (v[a] < 2147483647.0);
+        idx[a] = fin ? (int32_t)v[a] : -1;
+        ok = ok && fin && idx[a] >= 0 && (int64_t)idx[a] < g.n[a];
+        margin = dmin(margin, dmin(v[a] + 1.0, (double)g.n[a] - v[a]));
+    }
     float d = A.oob;
-    if (grid_index(A.sdf_g, x, idx)) {
-        d = A.sdf[grid_linear(A.sdf_g, idx[0], idx[1], idx[2])];
+    if (ok) {
+        d = A.sdf[grid_linear(g, idx[0], idx[1], idx[2])];
         *b += 4;
+        *S = (double)d;
+        *G = margin;
+    } else {
+        *S = kInvalidRound;
+        *G = kInvalidRound;
     }
     const double thr = A.thr_env;
     if ((double)d < thr) {
@@ -691,14 +849,29 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
 /* CheckEnvironmentCollision (SPCS:921-981) with threshold 0: two 64-point rounds are
  * evaluated together (their loads overlap), stopping after the pair holding the first
  * colliding point; algorithmic bytes are counted up to that point, as the reference
- * reads them (its loop returns at the first colliding point) */
+ * reads them (its loop returns at the first colliding point).  Provably-free rounds
+ * are not read but still counted (4 B per point, all in bounds). */
 __device__ bool env_collision(Sim& s, const double* T) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
-    for (int base = 0; base < R.P; base += 2 * kWave) {
+    const uint64_t skip = skippable_rounds(s, T, kSkipCheck);
+    for (int base = 0, r = 0; base < R.P; base += 2 * kWave, r += 2) {
+        const bool sk0 = r < kWave && ((skip >> r) & 1ull);
+        const bool sk1 = r + 1 < kWave && ((skip >> (r + 1)) & 1ull);
         uint64_t b0 = 0, b1 = 0;
-        const bool c0 = env_point(A, T, base + s.lane, &b0);
-        const bool c1 = env_point(A, T, base + kWave + s.lane, &b1);
+        double S0 = __builtin_huge_val(), S1 = __builtin_huge_val(), G0 = __builtin_huge_val(), G1 = __builtin_huge_val();
+        bool c0 = false, c1 = false;
+        const int i0 = base + s.lane, i1 = base + kWave + s.lane;
+        if (sk0)
+            b0 = (i0 < R.P) ? 4 : 0;
+        else
+            c0 = env_point(A, T, i0, &b0, &S0, &G0);
+        if (sk1)
+            b1 = (i1 < R.P) ? 4 : 0;
+        else
+            c1 = env_point(A, T, i1, &b1, &S1, &G1);
+        if (!sk0) round_update(s, r, T, S0, G0);
+        if (!sk1 && base + kWave < R.P) round_update(s, r + 1, T, S1, G1);
         const uint64_t m0 = __ballot(c0);
         const uint64_t m1 = __ballot(c1);
         if (m0) {
@@ -1117,8 +1290,17 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
     const double* axw = s.lds + s.A->L.axis_w;
     const double* orw = s.lds + s.A->L.orig_w;
     uint32_t rows = 0;
+    /* rounds that provably hold no corrected point: their EstimateDistance reads are
+     * counted (28 B per point, in bounds) but not made */
+    const uint64_t skip = skippable_rounds(s, Tc, kSkipCorrections);
     for (int base = 0; base < R.P; base += kWave) {
         const int i = base + ln;
+        const int r = base / kWave;
+        const bool skr = r < kWave && ((skip >> r) & 1ull);
+        if (skr && !s.self_nonempty) {
+            if (i < R.P) s.lane_bytes += 28;
+            continue;
+        }
         bool has = false;
         D3 pcorr{0.0, 0.0, 0.0};
         D4 xc{0.0, 0.0, 0.0, 0.0};
@@ -1128,8 +1310,12 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
             link = R.point_link[i];
             xc = xform4(Tc + 12 * link, p);
             const bool has_self = s.self_nonempty && flag[i] != 0.0;
-            bool inb;
-            const double est = estimate_distance(A, xc, &inb, &s.lane_bytes);
+            bool inb = false;
+            double est = 0.0;
+            if (skr)
+                s.lane_bytes += 28;
+            else
+                est = estimate_distance(A, xc, &inb, &s.lane_bytes);
             const bool has_env = (est < 0.0) && inb;
             D3 ecorr{0.0, 0.0, 0.0};
             if (has_env) {
@@ -1200,6 +1386,179 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
     }
     wsync();
     return rows * 3u;
+}
+
+/* value of column `k` (wave-uniform, runtime) of this lane's register row */
+template <int DM>
+__device__ __forceinline__ double col_sel(const double (&a)[DM], int k) {
+    double v = a[0];
+#pragma unroll
+    for (int c = 1; c < DM; ++c)
+        if (c == k) v = a[c];
+    return v;
+}
+
+/* ColPivHouseholderQR::solve for Rn <= 64 rows and D <= DM columns with the matrix
+ * in registers: lane r holds row r (the lane-strided layout of the general solver
+ * with one row per lane), so every long sum is the same canonical reduction and the
+ * results equal qr_solve's bit for bit, without touching scratch memory. */
+template <int DM>
+__device__ __noinline__ void qr_solve_regs(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
+                                           uint32_t Rn, double* x) {
+    const SimArgs& A = *Ap;
+    const int D = A.R.D;
+    const uint32_t rc = A.row_cap;
+    const double* Jm = scratch + A.SL.J;
+    const double* bv = scratch + A.SL.b;
+    double* colsq = lds + A.L.colsq;
+    double* hco = lds + A.L.hcoef;
+    int32_t* perm = reinterpret_cast<int32_t*>(lds + A.L.ints);
+    int32_t* transp = perm + kMaxDofs;
+    const bool has = (uint32_t)ln < Rn;
+    double a[DM];
+#pragma unroll
+    for (int c = 0; c < DM; ++c) a[c] = (has && c < D) ? Jm[(uint64_t)c * rc + ln] : 0.0;
+    double bb = has ? bv[ln] : 0.0;
+    if (ln < D) x[ln] = 0.0;
+    if (D == 0) {
+        wsync();
+        return;
+    }
+    {
+        double cs[DM];
+#pragma unroll
+        for (int c = 0; c < DM; ++c) cs[c] = bfly_sum(has ? 0.0 + a[c] * a[c] : 0.0);
+        if (ln == 0) {
+#pragma unroll
+            for (int c = 0; c < DM; ++c)
+                if (c < D) colsq[c] = cs[c];
+        }
+    }
+    wsync();
+    double maxsq = colsq[0];
+    for (int k = 1; k < D; ++k)
+        if (colsq[k] > maxsq) maxsq = colsq[k];
+    const double eps = 2.220446049250313e-16;
+    const double threshold_helper = maxsq * (eps * eps) / (double)Rn;
+    const int size = ((int)Rn < D) ? (int)Rn : D;
+    int nz = size;
+    for (int k = 0; k < size; ++k) {
+        int biggest = k;
+        double bsq = colsq[k];
+        for (int c2 = k + 1; c2 < D; ++c2)
+            if (colsq[c2] > bsq) {
+                bsq = colsq[c2];
+                biggest = c2;
+            }
+        {
+            const double vb = col_sel(a, biggest);
+            bsq = bfly_sum((has && ln >= k) ? 0.0 + vb * vb : 0.0);
+        }
+        if (nz == size && bsq < threshold_helper * (double)(Rn - (uint32_t)k)) nz = k;
+        wsync();
+        if (ln == 0) {
+            colsq[biggest] = bsq;
+            transp[k] = biggest;
+        }
+        if (k != biggest) {
+            const double vk = col_sel(a, k), vb = col_sel(a, biggest);
+#pragma unroll
+            for (int c = 0; c < DM; ++c) a[c] = (c == k) ? vb : ((c == biggest) ? vk : a[c]);
+            if (ln == 0) {
+                const double t = colsq[k];
+                colsq[k] = colsq[biggest];
+                colsq[biggest] = t;
+            }
+        }
+        wsync();
+        const double colk = col_sel(a, k);
+        const double c0 = readlane_f64(colk, k);
+        const bool below = has && ln > k;
+        const double tail = (Rn - (uint32_t)k == 1u) ? 0.0 : bfly_sum(below ? 0.0 + colk * colk : 0.0);
+        double tau, beta, v;
+        if (tail <= 2.2250738585072014e-308) {
+            tau = 0.0;
+            beta = c0;
+            v = below ? 0.0 : colk;
+        } else {
+            beta = dsqrt(c0 * c0 + tail);
+            if (c0 >= 0.0) beta = -beta;
+            const double denom = c0 - beta;
+            v = below ? colk / denom : colk;
+            tau = (beta - c0) / beta;
+        }
+        if (ln == k) v = beta;
+#pragma unroll
+        for (int c = 0; c < DM; ++c)
+            if (c == k) a[c] = v;
+        if (ln == 0) hco[k] = tau;
+        if (Rn - (uint32_t)k == 1u) {
+            if (ln == k) {
+#pragma unroll
+                for (int c = 0; c < DM; ++c)
+                    if (c > k && c < D) a[c] = a[c] * (1.0 - tau);
+            }
+        } else if (tau != 0.0) {
+            double tmp[DM];
+#pragma unroll
+            for (int c = 0; c < DM; ++c) tmp[c] = (c > k && c < D) ? bfly_sum(below ? 0.0 + v * a[c] : 0.0) : 0.0;
+#pragma unroll
+            for (int c = 0; c < DM; ++c) {
+                if (c > k && c < D) {
+                    const double t = tmp[c] + readlane_f64(a[c], k);
+                    if (ln == k) a[c] = a[c] - tau * t;
+                    if (below) a[c] = a[c] - (tau * v) * t;
+                }
+            }
+        }
+        {
+            /* colsq downdate with the updated row k (held by lane k) */
+            double rk[DM];
+#pragma unroll
+            for (int c = 0; c < DM; ++c) rk[c] = (c > k && c < D) ? readlane_f64(a[c], k) : 0.0;
+            if (ln == 0) {
+#pragma unroll
+                for (int c = 0; c < DM; ++c)
+                    if (c > k && c < D) colsq[c] = colsq[c] - rk[c] * rk[c];
+            }
+        }
+        wsync();
+    }
+    if (ln == 0) {
+        for (int i = 0; i < D; ++i) perm[i] = i;
+        for (int k = 0; k < size; ++k) {
+            const int t = perm[k];
+            perm[k] = perm[transp[k]];
+            perm[transp[k]] = t;
+        }
+    }
+    wsync();
+    if (nz == 0) return;
+    /* Q^T b */
+    for (int k = 0; k < nz; ++k) {
+        const double tau = hco[k];
+        if (Rn - (uint32_t)k == 1u) {
+            if (ln == k) bb = bb * (1.0 - tau);
+        } else if (tau != 0.0) {
+            const double vk = col_sel(a, k);
+            const bool below = has && ln > k;
+            const double t = bfly_sum(below ? 0.0 + vk * bb : 0.0) + readlane_f64(bb, k);
+            if (ln == k) bb = bb - tau * t;
+            if (below) bb = bb - (tau * vk) * t;
+        }
+    }
+    /* column-oriented back substitution on the nz x nz upper triangle */
+    for (int ii = nz - 1; ii >= 0; --ii) {
+        const double ci = readlane_f64(bb, ii);
+        if (ci != 0.0) {
+            const double cii = col_sel(a, ii);
+            const double v = ci / readlane_f64(cii, ii);
+            if (ln == ii) bb = v;
+            if (ln < ii) bb = bb - v * cii;
+        }
+    }
+    if (ln < nz) x[perm[ln]] = bb;
+    wsync();
 }
 
 /* ColPivHouseholderQR::solve (Eigen 3.2 / 3.3-beta1), rows lane-strided; x -> LDS */
@@ -1464,11 +1823,17 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
                 s.resolver_count++;
                 t0 = tick();
                 const uint32_t Rn = collect_corrections<RT>(s, Tprev, Tcur, cfg_act);
+                s.lsq_rows += Rn;
                 s.err = wave_or(s.err);
                 tock(s, FKS_PHASE_CORRECTIONS, t0);
                 if (s.err) return 1;
                 t0 = tick();
-                qr_solve(s.A, s.lds, s.scratch, ln, Rn, x);
+                if (Rn <= (uint32_t)kWave && R.D <= 8)
+                    qr_solve_regs<8>(s.A, s.lds, s.scratch, ln, Rn, x);
+                else if (RT == FKS_ROBOT_LINKED && Rn <= (uint32_t)kWave && R.D <= 16)
+                    qr_solve_regs<RT == FKS_ROBOT_LINKED ? 16 : 8>(s.A, s.lds, s.scratch, ln, Rn, x);
+                else
+                    qr_solve(s.A, s.lds, s.scratch, ln, Rn, x);
                 tock(s, FKS_PHASE_SOLVE, t0);
                 t0 = tick();
                 apply_input<RT>(s, cfg_act, x, cfg_tmp, false, 0);
@@ -1557,6 +1922,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         s.ctrl = reinterpret_cast<const fks_dof_controller*>(dc);
         s.dofj = dd;
         s.base = s.lds + A.L.base;
+        for (int r = s.lane; r < R.nrounds; r += kWave) s.lds[A.L.rstate + kRoundState * r + 12] = kInvalidRound;
         wsync();
     }
     const int ln = s.lane;
@@ -1576,6 +1942,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         s.lane_bytes = 0;
         s.micro_count = 0;
         s.resolver_count = 0;
+        s.lsq_rows = 0;
         s.step_count = 0;
         if (ln < 8) s.stats[ln] = 0;
         if (ln < FKS_NUM_PHASES) s.phase[ln] = 0;
@@ -1652,6 +2019,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             atomicAdd(A.counters + kCntSteps, (unsigned long long)s.step_count);
             atomicAdd(A.counters + kCntMicrosteps, (unsigned long long)s.micro_count);
             atomicAdd(A.counters + kCntResolver, (unsigned long long)s.resolver_count);
+            atomicAdd(A.counters + kCntLsqRows, (unsigned long long)s.lsq_rows);
             atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes);
             if (s.err) atomicAdd(A.counters + kCntErrorParticles, 1ull);
             const uint64_t t_end = __builtin_amdgcn_s_memtime();

@@ -201,6 +201,8 @@ def _cfg4_env():
             continue
         h = [rng.uniform(0.04, 0.15) for _ in range(3)]
         obstacles.append(box(i + 1, c, h, rotation_from_axis_angle(rng.normal(size=3), rng.uniform(0, np.pi))))
+    # a block across the straight-line path to the target, so particles slide along it
+    obstacles.append(box(100, [0.2, 0.14, -0.09], [0.04, 0.04, 0.04], rotation_from_axis_angle([0.0, 0.0, 1.0], 0.3)))
     return build_complete_environment(obstacles, 0.01, origin=grid_origin([-1.28, -1.28, -1.28]), num_cells=(256, 256, 256))
 
 

@@ -1,0 +1,269 @@
+/*
+ * hip_particle_contact_simulator.hpp — C++ host mirror of the reference
+ * simulator interface over the C-ABI in fks_capi.h (header-only, C++17).
+ *
+ * Mirrors simple_particle_contact_simulator::SimpleParticleContactSimulator as the
+ * planner sees it through uncertainty_planning_core's SimulatorInterface
+ * (reference: include/fast_kinematic_simulator/simple_particle_contact_simulator.hpp,
+ * "SPCS") and the factories of fast_kinematic_simulator.hpp/.cpp ("FKS").  Method
+ * names, argument meaning and result layout follow the reference; configurations
+ * are flat double vectors (linked robot: joint values; SE(2): x, y, theta;
+ * SE(3): 3x4 row-major pose) because the reference's Eigen / arc_utilities types
+ * are not part of this repository.  INTEGRATION.md shows the conversion a
+ * maintainer adds on the reference side.
+ *
+ * Every simulation runs on the GPU through libfks_hip.so; there is no CPU
+ * fallback.  Errors from the C-ABI are raised as fks::SimulatorError.
+ */
+#ifndef FAST_KINEMATIC_SIMULATOR_AMD_HIP_PARTICLE_CONTACT_SIMULATOR_HPP
+#define FAST_KINEMATIC_SIMULATOR_AMD_HIP_PARTICLE_CONTACT_SIMULATOR_HPP
+
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "fks_capi.h"
+
+namespace fks {
+
+class SimulatorError : public std::runtime_error {
+  public:
+    SimulatorError(fks_status status, const std::string& what) : std::runtime_error(what), status_(status) {}
+    fks_status status() const { return status_; }
+
+  private:
+    fks_status status_;
+};
+
+inline void check(fks_status st, const fks_context* ctx, const char* what) {
+    if (st == FKS_OK) return;
+    std::string msg = std::string(what) + ": " + fks_status_string(st);
+    if (ctx) {
+        const char* detail = fks_get_last_error(ctx);
+        if (detail && detail[0]) msg += std::string(" (") + detail + ")";
+    }
+    throw SimulatorError(st, msg);
+}
+
+using Configuration = std::vector<double>;
+
+/* simple_simulator_interface::SimulationResult as built at SPCS:918 */
+struct SimulationResult {
+    Configuration result_config;
+    Configuration target_config;
+    bool did_contact = false;
+    bool outcome_is_valid = true;
+    uint32_t microsteps = 0;
+    uint32_t resolver_iterations = 0;
+    uint32_t error_flags = 0; /* FKS_PARTICLE_ERR_* */
+};
+
+/* fast_kinematic_simulator::GetDefaultSolverParameters (FKS.hpp:13-16) */
+inline fks_solver_params GetDefaultSolverParameters() {
+    fks_solver_params p;
+    check(fks_default_solver_params(&p), nullptr, "GetDefaultSolverParameters");
+    return p;
+}
+
+/* A flattened robot (fks_robot_desc) that owns its arrays: the immutable_robot
+ * argument of ForwardSimulateRobots (SPCS:788).  Build it once per robot. */
+class RobotDescription {
+  public:
+    fks_robot_type type = FKS_ROBOT_LINKED;
+    int32_t num_links = 1;
+    int32_t num_dofs = 0;
+    double base_transform[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    std::vector<fks_joint_desc> joints;
+    std::vector<int32_t> geometry_link;
+    std::vector<uint32_t> geometry_point_offset{0};
+    std::vector<double> points; /* x, y, z, w per point */
+    std::vector<int32_t> allowed_pairs; /* geometry index pairs */
+    std::vector<fks_dof_controller> controllers;
+    std::vector<double> distance_weights;
+
+    /* geometry `g` of link `link`: points as (x, y, z, w) quadruples */
+    int32_t AddGeometry(int32_t link, const std::vector<double>& xyzw) {
+        if (xyzw.size() % 4 != 0) throw std::invalid_argument("points are x, y, z, w quadruples");
+        geometry_link.push_back(link);
+        points.insert(points.end(), xyzw.begin(), xyzw.end());
+        geometry_point_offset.push_back((uint32_t)(points.size() / 4));
+        return (int32_t)geometry_link.size() - 1;
+    }
+    void AllowSelfCollision(int32_t geometry_a, int32_t geometry_b) {
+        allowed_pairs.push_back(geometry_a);
+        allowed_pairs.push_back(geometry_b);
+    }
+    int32_t ConfigurationWidth() const {
+        return type == FKS_ROBOT_SE2 ? 3 : (type == FKS_ROBOT_SE3 ? 12 : num_dofs);
+    }
+    fks_robot_desc View() const {
+        fks_robot_desc d;
+        d.robot_type = type;
+        d.num_links = num_links;
+        d.num_joints = (int32_t)joints.size();
+        d.num_geometries = (int32_t)geometry_link.size();
+        d.num_dofs = num_dofs;
+        d.num_allowed_pairs = (int32_t)(allowed_pairs.size() / 2);
+        for (int i = 0; i < 12; ++i) d.base_transform[i] = base_transform[i];
+        d.joints = joints.empty() ? nullptr : joints.data();
+        d.geometry_link = geometry_link.data();
+        d.geometry_point_offset = geometry_point_offset.data();
+        d.points = points.data();
+        d.allowed_pairs = allowed_pairs.empty() ? nullptr : allowed_pairs.data();
+        d.controllers = controllers.data();
+        d.distance_weights = distance_weights.empty() ? nullptr : distance_weights.data();
+        return d;
+    }
+};
+
+/* SimpleParticleContactSimulator on one MI355X.  The stacked-Jacobian resolver is
+ * always used, as the reference factories hard-wire (FKS.cpp:22,45,68). */
+class HipParticleContactSimulator {
+  public:
+    using DisplayFn = std::function<void(const void*)>;
+
+    HipParticleContactSimulator(const fks_environment& environment, const fks_solver_params& solver_config,
+                                double simulation_controller_frequency, uint64_t prng_seed, int32_t debug_level,
+                                int32_t device = 0) {
+        fks_context* ctx = nullptr;
+        check(fks_create(&environment, &solver_config, simulation_controller_frequency, prng_seed, debug_level, device, &ctx),
+              nullptr, "fks_create");
+        ctx_.reset(ctx);
+    }
+
+    /* SPCS:446-455 */
+    int32_t GetDebugLevel() const { return fks_get_debug_level(ctx_.get()); }
+    int32_t SetDebugLevel(int32_t debug_level) { return fks_set_debug_level(ctx_.get(), debug_level); }
+
+    /* SPCS:488-512: the eight resolve counters, by the reference's names */
+    std::vector<std::pair<std::string, double>> GetStatistics() const {
+        fks_statistics s;
+        check(fks_get_statistics(ctx_.get(), &s), ctx_.get(), "GetStatistics");
+        return {{"successful_resolves", (double)s.successful_resolves},
+                {"unsuccessful_resolves", (double)s.unsuccessful_resolves},
+                {"free_resolves", (double)s.free_resolves},
+                {"collision_resolves", (double)s.collision_resolves},
+                {"fallback_resolves", (double)s.fallback_resolves},
+                {"unsuccessful_env_collision_resolves", (double)s.unsuccessful_env_collision_resolves},
+                {"unsuccessful_self_collision_resolves", (double)s.unsuccessful_self_collision_resolves},
+                {"recovered_unsuccessful_resolves", (double)s.recovered_unsuccessful_resolves}};
+    }
+    void ResetStatistics() { check(fks_reset_statistics(ctx_.get()), ctx_.get(), "ResetStatistics"); }
+    /* SPCS:457-471 */
+    void ResetGenerators(uint64_t prng_seed) { check(fks_reset_generators(ctx_.get(), prng_seed), ctx_.get(), "ResetGenerators"); }
+
+    /* ForwardSimulateRobots (SPCS:788-804).  display_fn is accepted for interface
+     * parity; the batch path never draws (SPCS:801 passes enable_tracing=false). */
+    std::vector<SimulationResult> ForwardSimulateRobots(const RobotDescription& immutable_robot,
+                                                        const std::vector<Configuration>& start_positions,
+                                                        const std::vector<Configuration>& target_positions,
+                                                        bool allow_contacts, const DisplayFn& display_fn = {}) {
+        (void)display_fn;
+        return Simulate(immutable_robot, start_positions, target_positions, allow_contacts, false);
+    }
+    /* ReverseSimulateRobots (SPCS:806-822) == forward simulation (SPCS:838-841) */
+    std::vector<SimulationResult> ReverseSimulateRobots(const RobotDescription& immutable_robot,
+                                                        const std::vector<Configuration>& start_positions,
+                                                        const std::vector<Configuration>& target_positions,
+                                                        bool allow_contacts, const DisplayFn& display_fn = {}) {
+        (void)display_fn;
+        return Simulate(immutable_robot, start_positions, target_positions, allow_contacts, true);
+    }
+    /* ForwardSimulateRobot (SPCS:824-829) as a batch of one */
+    SimulationResult ForwardSimulateRobot(const RobotDescription& immutable_robot, const Configuration& start_position,
+                                          const Configuration& target_position, bool allow_contacts) {
+        return Simulate(immutable_robot, {start_position}, {target_position}, allow_contacts, false).front();
+    }
+    /* ReverseSimulateRobot (SPCS:831-836) */
+    SimulationResult ReverseSimulateRobot(const RobotDescription& immutable_robot, const Configuration& start_position,
+                                          const Configuration& target_position, bool allow_contacts) {
+        return Simulate(immutable_robot, {start_position}, {target_position}, allow_contacts, true).front();
+    }
+
+    fks_context* context() { return ctx_.get(); }
+
+  private:
+    struct Destroy {
+        void operator()(fks_context* c) const { fks_destroy(c); }
+    };
+    std::unique_ptr<fks_context, Destroy> ctx_;
+    const RobotDescription* robot_ = nullptr;
+
+    void SetRobot(const RobotDescription& robot) {
+        if (robot_ == &robot) return;
+        const fks_robot_desc d = robot.View();
+        check(fks_set_robot(ctx_.get(), &d), ctx_.get(), "fks_set_robot");
+        robot_ = &robot;
+    }
+
+    std::vector<SimulationResult> Simulate(const RobotDescription& robot, const std::vector<Configuration>& starts,
+                                           const std::vector<Configuration>& targets, bool allow_contacts, bool reverse) {
+        /* SPCS:792: one target per particle or one shared target */
+        if (!starts.empty() && targets.size() != 1 && targets.size() != starts.size())
+            throw std::invalid_argument("target_positions must hold 1 or start_positions.size() configurations");
+        SetRobot(robot);
+        const size_t W = (size_t)robot.ConfigurationWidth();
+        const size_t n = starts.size();
+        std::vector<double> s(n * W), t(targets.size() * W), out(n * W);
+        for (size_t i = 0; i < n; ++i) {
+            if (starts[i].size() != W) throw std::invalid_argument("start configuration has the wrong width");
+            std::copy(starts[i].begin(), starts[i].end(), s.begin() + i * W);
+        }
+        for (size_t i = 0; i < targets.size(); ++i) {
+            if (targets[i].size() != W) throw std::invalid_argument("target configuration has the wrong width");
+            std::copy(targets[i].begin(), targets[i].end(), t.begin() + i * W);
+        }
+        std::vector<uint8_t> collided(n);
+        std::vector<uint32_t> micro(n), resolver(n), errors(n);
+        auto fn = reverse ? fks_reverse_simulate : fks_forward_simulate;
+        check(fn(ctx_.get(), s.data(), n, t.data(), targets.size(), allow_contacts ? 1 : 0, out.data(), collided.data(),
+                 micro.data(), resolver.data(), errors.data()),
+              ctx_.get(), reverse ? "ReverseSimulateRobots" : "ForwardSimulateRobots");
+        std::vector<SimulationResult> results(n);
+        for (size_t i = 0; i < n; ++i) {
+            SimulationResult& r = results[i];
+            r.result_config.assign(out.begin() + i * W, out.begin() + (i + 1) * W);
+            r.target_config = targets.size() == n ? targets[i] : targets[0];
+            r.did_contact = collided[i] != 0;
+            r.outcome_is_valid = true;
+            r.microsteps = micro[i];
+            r.resolver_iterations = resolver[i];
+            r.error_flags = errors[i];
+        }
+        return results;
+    }
+};
+
+/* fast_kinematic_simulator::Make{SE2,SE3,Linked}Simulator (FKS.cpp:4-71) */
+inline std::shared_ptr<HipParticleContactSimulator> MakeSE2Simulator(const fks_environment& environment,
+                                                                     const fks_solver_params& solver_config,
+                                                                     double simulation_controller_frequency,
+                                                                     uint64_t prng_seed, int32_t debug_level,
+                                                                     int32_t device = 0) {
+    return std::make_shared<HipParticleContactSimulator>(environment, solver_config, simulation_controller_frequency,
+                                                         prng_seed, debug_level, device);
+}
+inline std::shared_ptr<HipParticleContactSimulator> MakeSE3Simulator(const fks_environment& environment,
+                                                                     const fks_solver_params& solver_config,
+                                                                     double simulation_controller_frequency,
+                                                                     uint64_t prng_seed, int32_t debug_level,
+                                                                     int32_t device = 0) {
+    return std::make_shared<HipParticleContactSimulator>(environment, solver_config, simulation_controller_frequency,
+                                                         prng_seed, debug_level, device);
+}
+inline std::shared_ptr<HipParticleContactSimulator> MakeLinkedSimulator(const fks_environment& environment,
+                                                                        const fks_solver_params& solver_config,
+                                                                        double simulation_controller_frequency,
+                                                                        uint64_t prng_seed, int32_t debug_level,
+                                                                        int32_t device = 0) {
+    return std::make_shared<HipParticleContactSimulator>(environment, solver_config, simulation_controller_frequency,
+                                                         prng_seed, debug_level, device);
+}
+
+}  // namespace fks
+
+#endif

@@ -198,6 +198,7 @@ typedef struct {
     double kernel_ms;             /* device time of the simulation kernel (HIP events) */
     double call_ms;               /* host wall time of the whole call */
     uint64_t calls;               /* number of calls these counters cover */
+    uint64_t least_squares_rows;  /* sum over resolver iterations of the stacked-Jacobian rows (3 x corrected points) */
 } fks_call_counters;
 
 typedef struct fks_context fks_context;

@@ -45,6 +45,7 @@ struct ParticleCounters {
     uint64_t resolver_iterations = 0;
     uint64_t controller_steps = 0;
     uint64_t sdf_bytes = 0;
+    uint64_t lsq_rows = 0;
     uint32_t error_flags = 0;
     fks_statistics stats;
     ParticleCounters() { std::memset(&stats, 0, sizeof(stats)); }
@@ -61,14 +62,14 @@ static inline bool trunc_index(double v, int64_t* out) {
 /* ---------------- canonical wave reduction ----------------
  * sum_{r in [begin,end)} terms[r], evaluated as 64 lane-strided partial sums
  * (lane l accumulates rows r = l mod 64 in ascending r, starting from +0.0),
- * then an xor-butterfly over offsets 32,16,8,4,2,1.  This is the order the HIP
- * kernel's 64-lane wavefront reduction produces; it is the oracle's definition
+ * then an xor-butterfly over offsets 1,2,4,8,16,32.  This is the order the HIP
+ * kernel's 64-lane wavefront reduction (DPP within rows, readlane across rows) produces; it is the oracle's definition
  * of every long sum in the least-squares solve (DESIGN.md §Canonical sums). */
 static double canon_sum(const std::vector<double>& terms, size_t begin, size_t end) {
     double partial[64];
     for (int l = 0; l < 64; ++l) partial[l] = 0.0;
     for (size_t r = begin; r < end; ++r) partial[r % 64] = partial[r % 64] + terms[r];
-    for (int off = 32; off >= 1; off >>= 1) {
+    for (int off = 1; off <= 32; off <<= 1) {
         double next[64];
         for (int l = 0; l < 64; ++l) next[l] = partial[l] + partial[l ^ off];
         for (int l = 0; l < 64; ++l) partial[l] = next[l];
@@ -745,6 +746,7 @@ class Simulator {
                     size_t rows = 0;
                     CollectPointCorrectionsAndJacobians(robot, previous_configuration, active_configuration, geoms,
                                                         self_collision_map, J, b, rows, pc);
+                    pc.lsq_rows += rows;
                     if (pc.error_flags) return ResolveResult{previous_configuration, collided, false, true};
                     const std::vector<double> raw_correction_step = colpiv_qr_solve(J, rows, D, b);
                     if (std::getenv("FKS_ORACLE_TRACE")) {
@@ -941,6 +943,7 @@ int oracle_forward_simulate(const fks_environment* env, const fks_solver_params*
         cc.microsteps += pc.microsteps;
         cc.resolver_iterations += pc.resolver_iterations;
         cc.sdf_bytes += pc.sdf_bytes;
+        cc.least_squares_rows += pc.lsq_rows;
         cc.error_particles += pc.error_flags ? 1 : 0;
     }
     if (out_stats) *out_stats = stats;

@@ -31,7 +31,7 @@ def test_forward_parity(fks_lib, oracle_lib, name, scale):
     print(name, mismatch_report(g, o))
     assert_identical(g, o)
     assert g["statistics"] == o["statistics"]
-    for k in ("microsteps", "resolver_iterations", "controller_steps", "sdf_bytes", "error_particles"):
+    for k in ("microsteps", "resolver_iterations", "controller_steps", "sdf_bytes", "error_particles", "least_squares_rows"):
         assert g["counters"][k] == o["counters"][k], k
 
 
