@@ -94,6 +94,7 @@ def main():
     from fast_kinematic_simulator_amd import make_linked_simulator
     from fast_kinematic_simulator_amd import workloads as W
 
+    from fast_kinematic_simulator_amd._capi import PHASE_COUNTS
     from fast_kinematic_simulator_amd.sharding import gather_outcomes, pack_outcomes, shard_bounds
 
     n_total = args.particles * world
@@ -221,7 +222,8 @@ def main():
             "cpu_baseline": cpu,
             # share of wave time per phase of the hot path (s_memtime cycle sums, rank 0)
             # (only in profiling builds of the library: -DFKS_PHASE_TIMERS=1, see tools/variant_bench.py)
-            "kernel_phases": ({k: round(v / max(1, phases["particle"]), 4) for k, v in phases.items() if k != "particle"}
+            "kernel_phases": ({k: (v if k in PHASE_COUNTS else round(v / max(1, phases["particle"]), 4))
+                               for k, v in phases.items() if k not in ("particle", "reserved")}
                               if phases.get("control", 0) > 0 else None),
         }
         print(json.dumps(line), flush=True)

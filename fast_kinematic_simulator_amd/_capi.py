@@ -27,9 +27,11 @@ STATUS_NAMES = {
 ROBOT_LINKED, ROBOT_SE2, ROBOT_SE3 = 0, 1, 2
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_CONTINUOUS, JOINT_PRISMATIC = 0, 1, 2, 4
 
-NUM_PHASES = 12
+NUM_PHASES = 16
 PHASE_NAMES = ["particle", "control", "step_setup", "micro_input", "micro_fk", "env_check", "self_check", "corrections",
-               "solve", "resolve_apply", "output", "reserved"]
+               "solve", "resolve_apply", "output", "env_rounds_skipped", "env_rounds_evaluated", "corr_rounds_skipped",
+               "corr_rounds_evaluated", "reserved"]
+PHASE_COUNTS = {"env_rounds_skipped", "env_rounds_evaluated", "corr_rounds_skipped", "corr_rounds_evaluated"}
 
 PARTICLE_ERR_MICROSTEP_MOTION = 0x1
 PARTICLE_ERR_NORMAL_OOB = 0x2

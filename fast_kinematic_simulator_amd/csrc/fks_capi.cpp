@@ -522,6 +522,44 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
             }
         }
     }
+    /* lever arm bound per dof: max over downstream points of (path reach from the
+     * joint frame origin) + |p|; prismatic joints on the path add their largest stroke */
+    std::vector<double> lever(std::max(1, R.D), HUGE_VAL);
+    if (d->robot_type == FKS_ROBOT_LINKED) {
+        bool w_one = true;
+        for (uint32_t i = 0; i < P; ++i) w_one = w_one && d->points[4 * (size_t)i + 3] == 1.0;
+        for (int k = 0; k < R.D && w_one; ++k) {
+            const int jd = dof_joint[k];
+            if (joints[jd].type == FKS_JOINT_PRISMATIC) {
+                const double* ax = joints[jd].axis;
+                lever[k] = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+                continue;
+            }
+            double worst = 0.0;
+            for (int g = 0; g < G; ++g) {
+                const int l = d->geometry_link[g];
+                if (!((link_mask[l] >> k) & 1ull)) continue;
+                /* reach from joint jd's frame origin (= its child link origin) down to link l */
+                double reach = 0.0;
+                for (int cur = l; cur != joints[jd].child;) {
+                    const JointDev& jp = joints[link_parent_joint[cur]];
+                    reach += std::sqrt(jp.origin[3] * jp.origin[3] + jp.origin[7] * jp.origin[7] + jp.origin[11] * jp.origin[11]);
+                    if (jp.type == FKS_JOINT_PRISMATIC)
+                        reach += std::max(std::fabs(jp.lo), std::fabs(jp.hi)) *
+                                 std::sqrt(jp.axis[0] * jp.axis[0] + jp.axis[1] * jp.axis[1] + jp.axis[2] * jp.axis[2]);
+                    cur = jp.parent;
+                }
+                for (uint32_t i = d->geometry_point_offset[g]; i < d->geometry_point_offset[g + 1]; ++i) {
+                    const double* p = d->points + 4 * (size_t)i;
+                    worst = std::max(worst, reach + std::sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]));
+                }
+            }
+            const double* ax = joints[jd].axis;
+            const double an = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+            /* AngleAxis with a non-unit axis is not a rotation: no bound */
+            lever[k] = (std::fabs(an - 1.0) < 1e-12 && std::isfinite(worst)) ? worst * (1.0 + 1e-9) + 1e-12 : HUGE_VAL;
+        }
+    }
     std::vector<double> weights;
     if (d->robot_type == FKS_ROBOT_LINKED) {
         for (int k = 0; k < R.D; ++k) weights.push_back(d->distance_weights ? d->distance_weights[k] : 1.0);
@@ -558,6 +596,8 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     HIP_TRY(ctx, up(&dw, weights.data(), weights.size()));
     fksd::RoundDev* drounds = nullptr;
     HIP_TRY(ctx, up(&drounds, rounds.data(), rounds.size()));
+    double* dlever = nullptr;
+    HIP_TRY(ctx, up(&dlever, lever.data(), lever.size()));
     R.joints = dj;
     R.geom_link = dgl;
     R.geom_off = dgo;
@@ -573,6 +613,7 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     R.ctrl = dctrl;
     R.weights = dw;
     R.rounds = drounds;
+    R.dof_lever = dlever;
     /* launch geometry: one wave per workgroup, as many resident waves as fit */
     const fksd::LdsLayout L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds);
     ctx->lds_bytes = (size_t)L.total * sizeof(double);

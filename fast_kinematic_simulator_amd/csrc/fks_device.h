@@ -53,7 +53,10 @@ struct RoundDev {
     int32_t npts;
     double radius;
 };
-constexpr int kRoundState = 14; /* per round in LDS: reference transform (12), min SDF value, min grid margin (cells) */
+/* per round in LDS: reference transform (12), min SDF value, min grid-bounds margin
+ * (cells), min distance to a cell face (cells), spare */
+constexpr int kRoundState = 16;
+constexpr int kLdsPairs = 128; /* disallowed geometry pairs cached in LDS (the rest are read from HBM) */
 
 struct RobotDev {
     int32_t type, L, J, G, D, P, W, npairs;
@@ -75,11 +78,16 @@ struct RobotDev {
     const fks_dof_controller* ctrl;
     const double* weights;
     const RoundDev* rounds;
+    /* per dof: a configuration-independent bound on how far any point moves per
+     * unit of joint motion (distance to the joint axis; 1 for prismatic), +inf if
+     * unknown.  Lets the microstep-motion check of SPCS:1570-1575 be proven instead
+     * of recomputed. */
+    const double* dof_lever;
 };
 
 /* LDS carve-out (in doubles), identical on host and device */
 struct LdsLayout {
-    uint32_t joints, ctrl, base, dofj, rstate, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u, ustep, x, real, axis_w,
+    uint32_t joints, ctrl, base, dofj, rstate, gbox, gpairs, noise, noise_err, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u, ustep, x, real, axis_w,
         orig_w, colsq, hcoef, box, misc, ints, total;
 };
 
@@ -101,6 +109,14 @@ inline
     o += (uint32_t)(D + 1) / 2;
     l.rstate = o; /* kRoundState per round, persists across the wave's particles */
     o += (uint32_t)kRoundState * (NR > 0 ? NR : 1);
+    l.gbox = o; /* per geometry: local box (7) + link */
+    o += 8u * (G > 0 ? G : 1);
+    l.gpairs = o; /* first kLdsPairs disallowed pairs, a | b << 16 */
+    o += (uint32_t)kLdsPairs / 2;
+    l.noise = o; /* actuator noise samples of the next floor(64/D) microsteps, [micro][dof] */
+    o += 64;
+    l.noise_err = o; /* their error bits, 64 x u32 */
+    o += 32;
     l.Tcur = o;
     o += 12u * L;
     l.Tprev = o;

@@ -94,8 +94,8 @@ __device__ __forceinline__ D3 safe_normal3(const D3& v) {
 }
 /* Eigen::AngleAxisd::toRotationMatrix into a 3x4 (translation untouched) */
 __device__ __forceinline__ void angle_axis34(double angle, double a0, double a1, double a2, double* M) {
-    const double s = fks_math::sin(angle);
-    const double c = fks_math::cos(angle);
+    double s, c;
+    fks_math::sincos(angle, &s, &c);
     const double sa0 = s * a0, sa1 = s * a1, sa2 = s * a2;
     const double omc = 1.0 - c;
     const double c1a0 = omc * a0, c1a1 = omc * a1, c1a2 = omc * a2;
@@ -233,6 +233,10 @@ constexpr int kDppXor1 = 0xB1;       /* quad_perm [1,0,3,2] */
 constexpr int kDppXor2 = 0x4E;       /* quad_perm [2,3,0,1] */
 constexpr int kDppHalfMirror = 0x141; /* lane 7-i within 8: xor 4 once quads are uniform */
 constexpr int kDppMirror = 0x140;     /* lane 15-i within 16: xor 8 once 8-groups are uniform */
+constexpr int kDppQuadBcast0 = 0x00;  /* quad_perm [0,0,0,0] */
+constexpr int kDppQuadBcast1 = 0x55;  /* quad_perm [1,1,1,1] */
+constexpr int kDppQuadBcast2 = 0xAA;  /* quad_perm [2,2,2,2] */
+constexpr int kDppQuadBcast3 = 0xFF;  /* quad_perm [3,3,3,3] */
 
 /* canonical 64-lane sum (oracle canon_sum): xor butterfly with offsets 1, 2, 4,
  * 8, 16, 32; every lane gets the same value.  Call with all 64 lanes active. */
@@ -320,6 +324,13 @@ __device__ double tn_sample(uint32_t k0, uint32_t k1, uint64_t particle, uint32_
     return 0.0;
 }
 
+/* Actuator noise does not depend on the particle state, so the samples of the next
+ * floor(64 / D) microsteps are drawn at once, one lane per (microstep, dof), into LDS;
+ * noise_sample() consumes them (and their error bits) in the DOF lanes. */
+struct Sim;
+__device__ void refill_noise(Sim& s, uint32_t micro0, uint32_t M);
+__device__ __forceinline__ double noise_sample(Sim& s, uint32_t micro);
+
 /* ---------------- grids ---------------- */
 /* VoxelGrid LocationToGridIndex4d + IndexInBounds: trunc toward zero of
  * (inverse_origin * p) * (1/res); indices beyond int32 are out of bounds anyway */
@@ -374,6 +385,38 @@ __device__ __forceinline__ uint64_t tick() {
 __device__ __forceinline__ void tock(Sim& s, int phase, uint64_t t0) {
     if constexpr (FKS_PHASE_TIMERS)
         if (s.lane == 0) s.phase[phase] += tick() - t0;
+}
+__device__ __forceinline__ void count_event(Sim& s, int slot, uint64_t n) {
+    if constexpr (FKS_PHASE_TIMERS)
+        if (s.lane == 0) s.phase[slot] += n;
+}
+
+__device__ __noinline__ void refill_noise_lanes(const SimArgs* __restrict__ Ap, double* lds, int ln, uint64_t pid, uint32_t step,
+                                                uint32_t micro0, uint32_t M) {
+    const SimArgs& A = *Ap;
+    const int D = A.R.D;
+    const int per = kWave / D;
+    double* nz = lds + A.L.noise;
+    uint32_t* ne = reinterpret_cast<uint32_t*>(lds + A.L.noise_err);
+    if (ln < per * D) {
+        const uint32_t m = micro0 + (uint32_t)(ln / D);
+        if (m < M) {
+            uint32_t e = 0;
+            nz[ln] = tn_sample(A.key0, A.key1, pid, step, m, (uint32_t)(ln % D), &e);
+            ne[ln] = e;
+        }
+    }
+    wsync();
+}
+__device__ void refill_noise(Sim& s, uint32_t micro0, uint32_t M) {
+    refill_noise_lanes(s.A, s.lds, s.lane, s.pid, s.step, micro0, M);
+}
+__device__ __forceinline__ double noise_sample(Sim& s, uint32_t micro) {
+    const SimArgs& A = *s.A;
+    const int D = A.R.D;
+    const int slot = (int)(micro % (uint32_t)(kWave / D)) * D + s.lane;
+    s.err |= reinterpret_cast<const uint32_t*>(s.lds + A.L.noise_err)[slot];
+    return s.lds[A.L.noise + slot];
 }
 
 /* sdf_tools EstimateDistance4d (same spec as oracle SDF::EstimateDistance4d) */
@@ -472,38 +515,63 @@ __device__ void fk(Sim& s, const double* cfg, double* T) {
             }
         }
         wsync();
-        /* row r of a child transform depends only on row r of its parent's, so lane r
-         * walks the whole chain alone: T_child = (T_parent * origin) * motion */
-        if (ln < 3) {
-            const int r = ln;
-            const double* B = s.base + 4 * r;
-            T[4 * r + 0] = B[0];
-            T[4 * r + 1] = B[1];
-            T[4 * r + 2] = B[2];
-            T[4 * r + 3] = B[3];
-            for (int j = 0; j < R.J; ++j) {
-                const JointDev& jd = JD[j];
-                const double* Tp = T + 12 * jd.parent + 4 * r;
-                const double p0 = Tp[0], p1 = Tp[1], p2 = Tp[2], p3 = Tp[3];
-                const double* O = jd.origin;
-                const double a0 = dot3(p0, p1, p2, O[0], O[4], O[8]);
-                const double a1 = dot3(p0, p1, p2, O[1], O[5], O[9]);
-                const double a2 = dot3(p0, p1, p2, O[2], O[6], O[10]);
-                const double a3 = dot3(p0, p1, p2, O[3], O[7], O[11]) + p3;
-                double* Tc = T + 12 * jd.child + 4 * r;
-                if (jd.type == FKS_JOINT_FIXED) {
-                    Tc[0] = a0;
-                    Tc[1] = a1;
-                    Tc[2] = a2;
-                    Tc[3] = a3;
-                } else {
-                    const double* M = jm + 12 * j;
-                    Tc[0] = dot3(a0, a1, a2, M[0], M[4], M[8]);
-                    Tc[1] = dot3(a0, a1, a2, M[1], M[5], M[9]);
-                    Tc[2] = dot3(a0, a1, a2, M[2], M[6], M[10]);
-                    Tc[3] = dot3(a0, a1, a2, M[3], M[7], M[11]) + a3;
-                }
+        /* 12-lane chain: lane 4r+c owns element (r, c) of the running transform; the
+         * row a lane needs is broadcast inside its quad (DPP), so the chain never
+         * goes through memory.  T_child = (T_parent * origin) * motion, each element
+         * the same dot3 as the oracle.  The next joint's origin / motion columns are
+         * loaded one joint ahead. */
+        const int r = ln >> 2, c = ln & 3;
+        const bool act = ln < 12;
+        double own = act ? s.base[4 * r + c] : 0.0;
+        if (act) T[4 * r + c] = own;
+        double p0 = dpp_f64<kDppQuadBcast0>(own), p1 = dpp_f64<kDppQuadBcast1>(own), p2 = dpp_f64<kDppQuadBcast2>(own),
+               p3 = dpp_f64<kDppQuadBcast3>(own);
+        int last = 0;
+        const int J = R.J;
+        double o0 = 0.0, o1 = 0.0, o2 = 0.0, m0 = 0.0, m1 = 0.0, m2 = 0.0;
+        if (J > 0) {
+            o0 = JD[0].origin[c];
+            o1 = JD[0].origin[4 + c];
+            o2 = JD[0].origin[8 + c];
+            m0 = jm[c];
+            m1 = jm[4 + c];
+            m2 = jm[8 + c];
+        }
+        for (int j = 0; j < J; ++j) {
+            const int parent = __builtin_amdgcn_readfirstlane(JD[j].parent);
+            const int child = __builtin_amdgcn_readfirstlane(JD[j].child);
+            const int type = __builtin_amdgcn_readfirstlane(JD[j].type);
+            const double co0 = o0, co1 = o1, co2 = o2, cm0 = m0, cm1 = m1, cm2 = m2;
+            if (j + 1 < J) {
+                o0 = JD[j + 1].origin[c];
+                o1 = JD[j + 1].origin[4 + c];
+                o2 = JD[j + 1].origin[8 + c];
+                m0 = jm[12 * (j + 1) + c];
+                m1 = jm[12 * (j + 1) + 4 + c];
+                m2 = jm[12 * (j + 1) + 8 + c];
             }
+            if (parent != last) {
+                const double* Tp = T + 12 * parent + 4 * (act ? r : 0);
+                p0 = Tp[0];
+                p1 = Tp[1];
+                p2 = Tp[2];
+                p3 = Tp[3];
+            }
+            double a = dot3(p0, p1, p2, co0, co1, co2);
+            if (c == 3) a = a + p3;
+            double out = a;
+            if (type != FKS_JOINT_FIXED) {
+                const double a0 = dpp_f64<kDppQuadBcast0>(a), a1 = dpp_f64<kDppQuadBcast1>(a),
+                             a2 = dpp_f64<kDppQuadBcast2>(a), a3 = dpp_f64<kDppQuadBcast3>(a);
+                out = dot3(a0, a1, a2, cm0, cm1, cm2);
+                if (c == 3) out = out + a3;
+            }
+            if (act) T[12 * child + 4 * r + c] = out;
+            p0 = dpp_f64<kDppQuadBcast0>(out);
+            p1 = dpp_f64<kDppQuadBcast1>(out);
+            p2 = dpp_f64<kDppQuadBcast2>(out);
+            p3 = dpp_f64<kDppQuadBcast3>(out);
+            last = child;
         }
         wsync();
     } else if constexpr (RT == FKS_ROBOT_SE2) {
@@ -536,7 +604,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
                 const double prop = dabs(ct.max_actuator_proportional_noise) * dabs(real);
                 const double floor_noise = dabs(ct.max_actuator_minimum_noise) * vmax;
                 const double bound = dmax(prop, floor_noise);
-                real = real + tn_sample(A.key0, A.key1, s.pid, s.step, micro, (uint32_t)ln, &s.err) * bound;
+                real = real + noise_sample(s, micro) * bound;
             }
             const JointDev& jd = s.joints[s.dofj[ln]];
             const double raw = cfg_in[ln] + real;
@@ -560,7 +628,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
                 const double prop = dabs(ct.max_actuator_proportional_noise) * dabs(real);
                 const double floor_noise = dabs(ct.max_actuator_minimum_noise) * vmax;
                 const double bound = dmax(prop, floor_noise);
-                real = real + tn_sample(A.key0, A.key1, s.pid, s.step, micro, (uint32_t)ln, &s.err) * bound;
+                real = real + noise_sample(s, micro) * bound;
             }
             double v = cfg_in[ln] + real;
             if (ln == 2) v = fks_math::enforce_continuous_revolute_bounds(v);
@@ -577,7 +645,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
                 const double prop = dabs(ct.max_actuator_proportional_noise) * dabs(real);
                 const double floor_noise = dabs(ct.max_actuator_minimum_noise) * vmax;
                 const double bound = dmax(prop, floor_noise);
-                real = real + tn_sample(A.key0, A.key1, s.pid, s.step, micro, (uint32_t)ln, &s.err) * bound;
+                real = real + noise_sample(s, micro) * bound;
             }
             tw[ln] = real;
         }
@@ -736,27 +804,36 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
             const double Sr = st[12] * A.sdf_g.inv_res;
             const double lp = A.skip_lplus;
             const bool inb = st[13] - b > 1e-6;
+            /* every point still in the cell it was evaluated in: nearest values unchanged
+             * (always true for a link that has not moved at all, e.g. a fixed base) */
+            const double* Tl = T + 12 * rd.link;
+            bool still = true;
+#pragma unroll
+            for (int e = 0; e < 12; ++e) still = still && (Tl[e] == st[e]);
+            const bool same_cell = still || b < st[14] - 1e-9;
             if (what == kSkipCheck)
-                sk = inb && (Sr - A.skip_cmax) > (K - 1.0) * lp + 1e-9;
+                sk = (inb && (Sr - A.skip_cmax) > (K - 1.0) * lp + 1e-9) || (same_cell && st[12] >= A.thr_env);
             else
-                sk = inb && (Sr - A.skip_cmax) > K * lp + 1e-9 && (Sr - K * lp) > 0.5 + 1.5 * lp + 1e-6;
+                sk = (inb && (Sr - A.skip_cmax) > K * lp + 1e-9 && (Sr - K * lp) > 0.5 + 1.5 * lp + 1e-6) ||
+                     (same_cell && Sr > A.skip_cmax + 1e-9 && Sr > 0.5 + 1.5 * lp + 1e-6);
         }
     }
     return __ballot(sk);
 }
 
 /* cache the state of round r after a full evaluation at T (uniform call) */
-__device__ __forceinline__ void round_update(Sim& s, int r, const double* T, double S, double G) {
+__device__ __forceinline__ void round_update(Sim& s, int r, const double* T, double S, double G, double C) {
     const SimArgs& A = *s.A;
     if (!A.skip_enabled || r >= kWave || r >= A.R.nrounds) return;
     const RoundDev& rd = A.R.rounds[r];
     if (rd.link < 0) return;
-    const double smin = wave_min(S), gmin = wave_min(G);
+    const double smin = wave_min(S), gmin = wave_min(G), cmin = wave_min(C);
     double* st = s.lds + A.L.rstate + kRoundState * r;
     if (s.lane < 12) st[s.lane] = T[12 * rd.link + s.lane];
     if (s.lane == 0) {
         st[12] = smin;
         st[13] = gmin;
+        st[14] = cmin;
     }
 }
 
@@ -807,7 +884,8 @@ __device__ double max_point_motion(Sim& s, const double* TA, const double* TB) {
 /* one point of CheckEnvironmentCollision: nearest-cell read, then EstimateDistance4d
  * only where the nearest value cannot decide (SPCS:921-981, threshold 0).  Also
  * returns the nearest value S (-inf out of bounds) and the grid margin G in cells. */
-__device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int i, uint64_t* b, double* S, double* G) {
+__device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int i, uint64_t* b, double* S, double* G,
+                                          double* C) {
     const RobotDev& R = A.R;
     if (i >= R.P) return false;
     const D4 p = load_point(R, i);
@@ -818,13 +896,15 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
     const double v[3] = {q.x * g.inv_res, q.y * g.inv_res, q.z * g.inv_res};
     int32_t idx[3];
     bool ok = true;
-    double margin = __builtin_huge_val();
+    double margin = __builtin_huge_val(), face = __builtin_huge_val();
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const bool fin = (v[a] > -2147483648.0) && (v[a] < 2147483647.0);
         idx[a] = fin ? (int32_t)v[a] : -1;
         ok = ok && fin && idx[a] >= 0 && (int64_t)idx[a] < g.n[a];
         margin = dmin(margin, dmin(v[a] + 1.0, (double)g.n[a] - v[a]));
+        const double fr = v[a] - (double)idx[a];
+        face = dmin(face, (v[a] >= 0.0) ? dmin(fr, 1.0 - fr) : 0.0);
     }
     float d = A.oob;
     if (ok) {
@@ -832,9 +912,11 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
         *b += 4;
         *S = (double)d;
         *G = margin;
+        *C = face;
     } else {
         *S = kInvalidRound;
         *G = kInvalidRound;
+        *C = kInvalidRound;
     }
     const double thr = A.thr_env;
     if ((double)d < thr) {
@@ -860,18 +942,21 @@ __device__ bool env_collision(Sim& s, const double* T) {
         const bool sk1 = r + 1 < kWave && ((skip >> (r + 1)) & 1ull);
         uint64_t b0 = 0, b1 = 0;
         double S0 = __builtin_huge_val(), S1 = __builtin_huge_val(), G0 = __builtin_huge_val(), G1 = __builtin_huge_val();
+        double C0 = __builtin_huge_val(), C1 = __builtin_huge_val();
         bool c0 = false, c1 = false;
         const int i0 = base + s.lane, i1 = base + kWave + s.lane;
         if (sk0)
             b0 = (i0 < R.P) ? 4 : 0;
         else
-            c0 = env_point(A, T, i0, &b0, &S0, &G0);
+            c0 = env_point(A, T, i0, &b0, &S0, &G0, &C0);
         if (sk1)
             b1 = (i1 < R.P) ? 4 : 0;
         else
-            c1 = env_point(A, T, i1, &b1, &S1, &G1);
-        if (!sk0) round_update(s, r, T, S0, G0);
-        if (!sk1 && base + kWave < R.P) round_update(s, r + 1, T, S1, G1);
+            c1 = env_point(A, T, i1, &b1, &S1, &G1, &C1);
+        if (!sk0) round_update(s, r, T, S0, G0, C0);
+        if (!sk1 && base + kWave < R.P) round_update(s, r + 1, T, S1, G1, C1);
+        count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (sk0 ? 1 : 0) + ((sk1 && base + kWave < R.P) ? 1 : 0));
+        count_event(s, FKS_PHASE_ENV_ROUNDS_EVALUATED, (sk0 ? 0 : 1) + ((!sk1 && base + kWave < R.P) ? 1 : 0));
         const uint64_t m0 = __ballot(c0);
         const uint64_t m1 = __ballot(c1);
         if (m0) {
@@ -1092,8 +1177,8 @@ __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
     double* box = s.lds + s.A->L.box;
     bool bad = false;
     if (ln < R.G) {
-        const double* gb = R.geom_box + 7 * ln;
-        const int link = R.geom_link[ln];
+        const double* gb = s.lds + A.L.gbox + 8 * ln;
+        const int link = (int)gb[7];
         const double* T = Tc + 12 * link;
         double lo[3], hi[3];
         if (gb[6] != 0.0) {
@@ -1129,8 +1214,17 @@ __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
     }
     wsync();
     bool any = false;
+    const uint32_t* lpairs = reinterpret_cast<const uint32_t*>(s.lds + A.L.gpairs);
     for (int k = ln; k < R.npairs; k += kWave) {
-        const int a = R.pairs[2 * k], b = R.pairs[2 * k + 1];
+        int a, b;
+        if (k < kLdsPairs) {
+            const uint32_t ab = lpairs[k];
+            a = (int)(ab & 0xffffu);
+            b = (int)(ab >> 16);
+        } else {
+            a = R.pairs[2 * k];
+            b = R.pairs[2 * k + 1];
+        }
         bool ov = true;
         for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
         any = any || ov;
@@ -1297,6 +1391,7 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
         const int i = base + ln;
         const int r = base / kWave;
         const bool skr = r < kWave && ((skip >> r) & 1ull);
+        count_event(s, skr ? FKS_PHASE_CORR_ROUNDS_SKIPPED : FKS_PHASE_CORR_ROUNDS_EVALUATED, 1);
         if (skr && !s.self_nonempty) {
             if (i < R.P) s.lane_bytes += 28;
             continue;
@@ -1781,12 +1876,24 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
     if (M < 1u) M = 1u;
     if (ln < D) ustep[ln] = u[ln] / (double)M;
     wsync();
-    apply_input<RT>(s, cfg, ustep, cfg_tmp, false, 0);
-    fk<RT>(s, cfg_tmp, Ttmp);
-    const double micro_motion = max_point_motion(s, Tcur, Ttmp);
-    if (micro_motion > A.allowed_micro) {
-        s.err |= FKS_PARTICLE_ERR_MICROSTEP_MOTION;
-        return 1;
+    /* SPCS:1563-1575: the motion of one clean microstep must not exceed the allowed
+     * distance.  Linked robots: sum_d |u_d / M| * lever_d bounds it (clamping only
+     * shortens joint motion), so the check is evaluated only when the bound does not
+     * already prove it. */
+    bool proven = false;
+    if constexpr (RT == FKS_ROBOT_LINKED) {
+        const double term = (ln < D) ? dabs(ustep[ln]) * R.dof_lever[ln] : 0.0;
+        const double bound = bfly_sum(0.0 + term);
+        proven = bound * (1.0 + 1e-6) + 1e-12 < A.allowed_micro;
+    }
+    if (!proven) {
+        apply_input<RT>(s, cfg, ustep, cfg_tmp, false, 0);
+        fk<RT>(s, cfg_tmp, Ttmp);
+        const double micro_motion = max_point_motion(s, Tcur, Ttmp);
+        if (micro_motion > A.allowed_micro) {
+            s.err |= FKS_PARTICLE_ERR_MICROSTEP_MOTION;
+            return 1;
+        }
     }
     tock(s, FKS_PHASE_STEP_SETUP, t0);
     bool collided = false;
@@ -1800,6 +1907,7 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
         }
         wsync();
         t0 = tick();
+        if (micro % (uint32_t)(kWave / R.D) == 0u) refill_noise(s, micro, M);
         apply_input<RT>(s, cfg_prev, ustep, cfg, true, micro);
         s.err = wave_or(s.err);
         tock(s, FKS_PHASE_MICRO_INPUT, t0);
@@ -1923,6 +2031,13 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         s.dofj = dd;
         s.base = s.lds + A.L.base;
         for (int r = s.lane; r < R.nrounds; r += kWave) s.lds[A.L.rstate + kRoundState * r + 12] = kInvalidRound;
+        if (RT == FKS_ROBOT_LINKED) {
+            for (int k = s.lane; k < 8 * R.G; k += kWave)
+                s.lds[A.L.gbox + k] = (k % 8 == 7) ? (double)R.geom_link[k / 8] : R.geom_box[7 * (k / 8) + k % 8];
+            uint32_t* lp = reinterpret_cast<uint32_t*>(s.lds + A.L.gpairs);
+            for (int k = s.lane; k < R.npairs && k < kLdsPairs; k += kWave)
+                lp[k] = (uint32_t)R.pairs[2 * k] | ((uint32_t)R.pairs[2 * k + 1] << 16);
+        }
         wsync();
     }
     const int ln = s.lane;

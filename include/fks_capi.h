@@ -269,7 +269,7 @@ fks_status fks_get_last_call_counters(const fks_context* ctx, fks_call_counters*
 /* Kernel phase profile: shader-clock cycles (s_memtime) spent by all waves in each
  * phase of the hot path, summed over the particles of a call.  Diagnostic only;
  * the phases follow the reference's call structure (SPCS line ranges). */
-#define FKS_NUM_PHASES 12
+#define FKS_NUM_PHASES 16
 enum fks_phase {
     FKS_PHASE_PARTICLE = 0,        /* whole particle: ForwardSimulateMutableRobot SPCS:843-919 */
     FKS_PHASE_CONTROL = 1,         /* controller + sensor noise SPCS:861-876 */
@@ -282,7 +282,12 @@ enum fks_phase {
     FKS_PHASE_SOLVE = 8,           /* ColPivHouseholderQR solve SPCS:1617-1619 */
     FKS_PHASE_RESOLVE_APPLY = 9,   /* correction step sizing / application SPCS:1620-1656 */
     FKS_PHASE_OUTPUT = 10,         /* reached configuration + counters */
-    FKS_PHASE_RESERVED = 11
+    /* event counts (not cycles) of the profiling build */
+    FKS_PHASE_ENV_ROUNDS_SKIPPED = 11,   /* 64-point rounds proven free (no SDF reads) */
+    FKS_PHASE_ENV_ROUNDS_EVALUATED = 12, /* 64-point rounds read from the SDF */
+    FKS_PHASE_CORR_ROUNDS_SKIPPED = 13,  /* correction rounds proven free */
+    FKS_PHASE_CORR_ROUNDS_EVALUATED = 14,
+    FKS_PHASE_RESERVED = 15
 };
 /* which: 0 = last call, 1 = sums since fks_create / fks_reset_total_counters */
 fks_status fks_get_phase_cycles(const fks_context* ctx, int which, uint64_t* out /* FKS_NUM_PHASES */);

@@ -161,6 +161,48 @@ FKS_HD inline double cos(double x) {
     }
 }
 
+/* sin and cos of one argument sharing the argument reduction; bit-identical to
+ * sin(x) and cos(x) */
+FKS_HD inline void sincos(double x, double* s, double* c) {
+    const uint32_t ix = hi_word(x) & 0x7fffffffu;
+    if (ix <= 0x3fe921fbu) {
+        *s = (ix < 0x3e500000u) ? x : kernel_sin(x, 0.0, 0);
+        *c = (ix < 0x3e46a09eu) ? 1.0 : kernel_cos(x, 0.0);
+        return;
+    }
+    if (ix >= 0x7ff00000u) {
+        *s = x - x;
+        *c = x - x;
+        return;
+    }
+    double y0, y1;
+    const int32_t n = rem_pio2(x, &y0, &y1);
+    if (n == INT32_MIN) {
+        *s = from_bits(0x7ff8000000000000ull);
+        *c = *s;
+        return;
+    }
+    const double ks = kernel_sin(y0, y1, 1), kc = kernel_cos(y0, y1);
+    switch (n & 3) {
+        case 0:
+            *s = ks;
+            *c = kc;
+            break;
+        case 1:
+            *s = kc;
+            *c = -ks;
+            break;
+        case 2:
+            *s = -ks;
+            *c = -kc;
+            break;
+        default:
+            *s = -kc;
+            *c = ks;
+            break;
+    }
+}
+
 /* ---------------- log ---------------- */
 FKS_HD inline double log(double x) {
     const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
