@@ -177,6 +177,7 @@ struct fks_context {
     double* d_scratch = nullptr;
     uint64_t scratch_per_wave = 0;
     uint32_t grid_waves = 0;
+    uint32_t grid_groups = 0;
     size_t lds_bytes = 0;
     unsigned long long* d_counters = nullptr; /* kNumCounters + queue + phase cycles */
     uint64_t phase_last[FKS_NUM_PHASES] = {};
@@ -616,15 +617,16 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     R.dof_lever = dlever;
     /* launch geometry: one wave per workgroup, as many resident waves as fit */
     const fksd::LdsLayout L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds);
-    ctx->lds_bytes = (size_t)L.total * sizeof(double);
-    if (ctx->lds_bytes > 64 * 1024) return fail(ctx, FKS_ERR_UNSUPPORTED, "robot too large for the LDS layout");
+    ctx->lds_bytes = ((size_t)L.shared_total + (size_t)fksd::kWavesPerGroup * L.total) * sizeof(double);
+    if (ctx->lds_bytes > 160 * 1024) return fail(ctx, FKS_ERR_UNSUPPORTED, "robot too large for the LDS layout");
     int blocks_per_cu = 0;
     HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, reinterpret_cast<const void*>(kernel_for(R.type)),
-                                                              64, ctx->lds_bytes));
+                                                              64 * fksd::kWavesPerGroup, ctx->lds_bytes));
     if (blocks_per_cu < 1) return fail(ctx, FKS_ERR_UNSUPPORTED, "kernel does not fit on a CU");
     int cus = 0;
     HIP_TRY(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    ctx->grid_waves = (uint32_t)(cus * blocks_per_cu);
+    ctx->grid_groups = (uint32_t)(cus * blocks_per_cu);
+    ctx->grid_waves = ctx->grid_groups * (uint32_t)fksd::kWavesPerGroup;
     ctx->scratch_per_wave = fksd::make_scratch_layout(3u * P, R.D, (int)P).total;
     HIP_TRY(ctx, hipMalloc((void**)&ctx->d_scratch, (size_t)ctx->grid_waves * ctx->scratch_per_wave * sizeof(double)));
     ctx->R = R;
@@ -740,9 +742,11 @@ fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts,
     *ctx->h_args = a;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice, s));
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, fksd::kCounterWords * sizeof(unsigned long long), s));
-    const uint32_t grid = (uint32_t)((n < (uint64_t)ctx->grid_waves) ? (n > 0 ? n : 1) : ctx->grid_waves);
+    const uint64_t groups_needed = (n + fksd::kWavesPerGroup - 1) / fksd::kWavesPerGroup;
+    const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? (groups_needed > 0 ? groups_needed : 1)
+                                                                                  : ctx->grid_groups);
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
-    hipLaunchKernelGGL(kernel_for(ctx->R.type), dim3(grid), dim3(64), ctx->lds_bytes, s,
+    hipLaunchKernelGGL(kernel_for(ctx->R.type), dim3(grid), dim3(64 * fksd::kWavesPerGroup), ctx->lds_bytes, s,
                        static_cast<const fksd::SimArgs*>(ctx->d_args));
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));

@@ -85,10 +85,16 @@ struct RobotDev {
     const double* dof_lever;
 };
 
-/* LDS carve-out (in doubles), identical on host and device */
+/* LDS carve-out (in doubles), identical on host and device.  A workgroup holds
+ * kWavesPerGroup waves, one particle each.  The robot tables (joints ... gpairs) are
+ * one shared copy at the start of the workgroup's LDS (offsets relative to it,
+ * `shared_total` doubles); every other offset is relative to the wave's own block of
+ * `total` doubles that follows. */
+constexpr int kWavesPerGroup = 4;
 struct LdsLayout {
-    uint32_t joints, ctrl, base, dofj, rstate, gbox, gpairs, noise, noise_err, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u, ustep, x, real, axis_w,
-        orig_w, colsq, hcoef, box, misc, ints, total;
+    uint32_t joints, ctrl, base, dofj, gbox, gpairs, shared_total;
+    uint32_t rstate, noise, noise_err, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u,
+        ustep, x, real, axis_w, orig_w, colsq, hcoef, box, misc, ints, total;
 };
 
 inline
@@ -98,7 +104,7 @@ inline
     LdsLayout make_lds_layout(int L, int J, int D, int W, int G, int NR) {
     LdsLayout l;
     uint32_t o = 0;
-    /* per-wave copy of the robot tables the hot loops read (filled once per wave) */
+    /* shared: the robot tables the hot loops read (filled once per workgroup) */
     l.joints = o;
     o += (uint32_t)kJointWords * (J > 0 ? J : 1);
     l.ctrl = o;
@@ -107,12 +113,16 @@ inline
     o += 12;
     l.dofj = o; /* int32 per dof */
     o += (uint32_t)(D + 1) / 2;
-    l.rstate = o; /* kRoundState per round, persists across the wave's particles */
-    o += (uint32_t)kRoundState * (NR > 0 ? NR : 1);
     l.gbox = o; /* per geometry: local box (7) + link */
     o += 8u * (G > 0 ? G : 1);
     l.gpairs = o; /* first kLdsPairs disallowed pairs, a | b << 16 */
     o += (uint32_t)kLdsPairs / 2;
+    o = (o + 1u) & ~1u;
+    l.shared_total = o;
+    /* per wave */
+    o = 0;
+    l.rstate = o; /* kRoundState per round, persists across the wave's particles */
+    o += (uint32_t)kRoundState * (NR > 0 ? NR : 1);
     l.noise = o; /* actuator noise samples of the next floor(64/D) microsteps, [micro][dof] */
     o += 64;
     l.noise_err = o; /* their error bits, 64 x u32 */

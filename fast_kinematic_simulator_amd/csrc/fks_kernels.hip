@@ -352,7 +352,8 @@ __device__ __forceinline__ uint32_t grid_linear(const GridDev& g, int32_t i, int
 
 struct Sim {
     const SimArgs* A;
-    double* lds;
+    double* lds;    /* this wave's LDS block */
+    double* shared; /* the workgroup's robot tables */
     int32_t* ldsi;
     double* scratch;
     int lane;
@@ -1177,7 +1178,7 @@ __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
     double* box = s.lds + s.A->L.box;
     bool bad = false;
     if (ln < R.G) {
-        const double* gb = s.lds + A.L.gbox + 8 * ln;
+        const double* gb = s.shared + A.L.gbox + 8 * ln;
         const int link = (int)gb[7];
         const double* T = Tc + 12 * link;
         double lo[3], hi[3];
@@ -1214,7 +1215,7 @@ __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
     }
     wsync();
     bool any = false;
-    const uint32_t* lpairs = reinterpret_cast<const uint32_t*>(s.lds + A.L.gpairs);
+    const uint32_t* lpairs = reinterpret_cast<const uint32_t*>(s.shared + A.L.gpairs);
     for (int k = ln; k < R.npairs; k += kWave) {
         int a, b;
         if (k < kLdsPairs) {
@@ -2007,39 +2008,44 @@ template <int RT>
 __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ args, double* lds_mem) {
     const SimArgs& A = *args;
     const RobotDev& R = A.R;
+    const int wave = (int)(threadIdx.x >> 6);
+    double* shared = lds_mem;
+    {
+        /* one copy per workgroup of the robot tables read in the inner loops */
+        const int t = (int)threadIdx.x, nt = (int)blockDim.x;
+        uint64_t* dj = reinterpret_cast<uint64_t*>(shared + A.L.joints);
+        const uint64_t* sj = reinterpret_cast<const uint64_t*>(R.joints);
+        for (int k = t; k < R.J * kJointWords; k += nt) dj[k] = sj[k];
+        uint64_t* dc = reinterpret_cast<uint64_t*>(shared + A.L.ctrl);
+        const uint64_t* sc = reinterpret_cast<const uint64_t*>(R.ctrl);
+        for (int k = t; k < R.D * kCtrlWords; k += nt) dc[k] = sc[k];
+        int32_t* dd = reinterpret_cast<int32_t*>(shared + A.L.dofj);
+        if (RT == FKS_ROBOT_LINKED && t < R.D) dd[t] = R.dof_joint[t];
+        if (t < 12) shared[A.L.base + t] = R.base[t];
+        if (RT == FKS_ROBOT_LINKED) {
+            for (int k = t; k < 8 * R.G; k += nt)
+                shared[A.L.gbox + k] = (k % 8 == 7) ? (double)R.geom_link[k / 8] : R.geom_box[7 * (k / 8) + k % 8];
+            uint32_t* lp = reinterpret_cast<uint32_t*>(shared + A.L.gpairs);
+            for (int k = t; k < R.npairs && k < kLdsPairs; k += nt)
+                lp[k] = (uint32_t)R.pairs[2 * k] | ((uint32_t)R.pairs[2 * k + 1] << 16);
+        }
+        __syncthreads(); /* the only workgroup barrier: waves run independently afterwards */
+    }
     Sim s;
     s.A = args;
-    s.lds = lds_mem;
-    s.ldsi = reinterpret_cast<int32_t*>(lds_mem + s.A->L.ints);
-    s.scratch = A.scratch + (uint64_t)blockIdx.x * A.scratch_per_wave;
+    s.shared = shared;
+    s.lds = lds_mem + A.L.shared_total + (uint64_t)wave * A.L.total;
+    s.ldsi = reinterpret_cast<int32_t*>(s.lds + A.L.ints);
+    s.scratch = A.scratch + ((uint64_t)blockIdx.x * kWavesPerGroup + (uint64_t)wave) * A.scratch_per_wave;
     s.lane = lane_id();
     s.stats = reinterpret_cast<uint32_t*>(s.lds + s.A->L.misc + 24); /* 8 x u32 */
     s.phase = reinterpret_cast<uint64_t*>(s.lds + s.A->L.misc + 8); /* FKS_NUM_PHASES x u64 */
-    {
-        /* per-wave copy of the robot tables read in the inner loops */
-        uint64_t* dj = reinterpret_cast<uint64_t*>(s.lds + A.L.joints);
-        const uint64_t* sj = reinterpret_cast<const uint64_t*>(R.joints);
-        for (int k = s.lane; k < R.J * kJointWords; k += kWave) dj[k] = sj[k];
-        uint64_t* dc = reinterpret_cast<uint64_t*>(s.lds + A.L.ctrl);
-        const uint64_t* sc = reinterpret_cast<const uint64_t*>(R.ctrl);
-        for (int k = s.lane; k < R.D * kCtrlWords; k += kWave) dc[k] = sc[k];
-        int32_t* dd = reinterpret_cast<int32_t*>(s.lds + A.L.dofj);
-        if (RT == FKS_ROBOT_LINKED && s.lane < R.D) dd[s.lane] = R.dof_joint[s.lane];
-        if (s.lane < 12) s.lds[A.L.base + s.lane] = R.base[s.lane];
-        s.joints = reinterpret_cast<const JointDev*>(dj);
-        s.ctrl = reinterpret_cast<const fks_dof_controller*>(dc);
-        s.dofj = dd;
-        s.base = s.lds + A.L.base;
-        for (int r = s.lane; r < R.nrounds; r += kWave) s.lds[A.L.rstate + kRoundState * r + 12] = kInvalidRound;
-        if (RT == FKS_ROBOT_LINKED) {
-            for (int k = s.lane; k < 8 * R.G; k += kWave)
-                s.lds[A.L.gbox + k] = (k % 8 == 7) ? (double)R.geom_link[k / 8] : R.geom_box[7 * (k / 8) + k % 8];
-            uint32_t* lp = reinterpret_cast<uint32_t*>(s.lds + A.L.gpairs);
-            for (int k = s.lane; k < R.npairs && k < kLdsPairs; k += kWave)
-                lp[k] = (uint32_t)R.pairs[2 * k] | ((uint32_t)R.pairs[2 * k + 1] << 16);
-        }
-        wsync();
-    }
+    s.joints = reinterpret_cast<const JointDev*>(shared + A.L.joints);
+    s.ctrl = reinterpret_cast<const fks_dof_controller*>(shared + A.L.ctrl);
+    s.dofj = reinterpret_cast<const int32_t*>(shared + A.L.dofj);
+    s.base = shared + A.L.base;
+    for (int r = s.lane; r < R.nrounds; r += kWave) s.lds[A.L.rstate + kRoundState * r + 12] = kInvalidRound;
+    wsync();
     const int ln = s.lane;
     const int W = R.W, D = R.D;
     double* cfg = s.lds + s.A->L.cfg;
@@ -2151,9 +2157,9 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
  * The occupancy target bounds the VGPR budget of the kernel and of its out-of-line
  * callees (the rare self-contact path would otherwise set the budget for all). */
 #ifndef FKS_WAVES_PER_EU
-#define FKS_WAVES_PER_EU 4
+#define FKS_WAVES_PER_EU 5
 #endif
-#define FKS_KERNEL_ATTRS __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FKS_WAVES_PER_EU)))
+#define FKS_KERNEL_ATTRS __launch_bounds__(64 * kWavesPerGroup) __attribute__((amdgpu_waves_per_eu(FKS_WAVES_PER_EU)))
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
     simulate_particles<FKS_ROBOT_LINKED>(args, lds_mem);
