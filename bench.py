@@ -54,6 +54,45 @@ def cpu_baseline(wl, sample_particles: int, threads: int):
                       f"oracle in reference-RNG mode, OpenMP {threads} threads"}
 
 
+def config_check_bench(sim, wl, dev, n=1 << 20, reps=3, cpu_sample=16384, threads=16, with_cpu=True):
+    """Batched CheckConfigCollision (SPCS:1398-1416) on the cfg3 arm:
+    n configurations uniform in the joint limits, inflation ratio 0.5, inputs in HBM.
+    Reported beside the headline metric (not part of it)."""
+    import numpy as np
+    import torch
+
+    lo, hi = wl.robot.dof_limits()
+    rng = np.random.default_rng(21)
+    cfgs = rng.uniform(lo, hi, size=(n, wl.robot.config_width))
+    d_cfg = torch.from_numpy(cfgs).to(dev)
+    d_out = torch.empty(n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sim.check_config_collisions_device(wl.robot, d_cfg.data_ptr(), n, 0.5, d_out.data_ptr(), stream=stream.cuda_stream,
+                                       synchronize=True)
+    ms = []
+    for _ in range(reps):
+        sim.check_config_collisions_device(wl.robot, d_cfg.data_ptr(), n, 0.5, d_out.data_ptr(), stream=stream.cuda_stream,
+                                           synchronize=True)
+        ms.append(sim.last_check_counters()["kernel_ms"])
+    c = sim.last_check_counters()
+    kernel_s = sum(ms) / len(ms) / 1e3
+    out = {"metric": "configurations checked/s (batched CheckConfigCollision, cfg3 arm, 256^3 SDF, inflation 0.5)",
+           "value": n / kernel_s, "unit": "configs/s", "configs": n, "kernel_ms": kernel_s * 1e3,
+           "collided_fraction": float(d_out.float().mean().item()),
+           "roofline": {"bound": "hbm", "achieved": c["sdf_bytes"] / kernel_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": c["sdf_bytes"] / kernel_s / 1e9 / HBM_PEAK_GBS,
+                        "algorithmic_bytes_per_launch": c["sdf_bytes"]}}
+    if with_cpu:
+        import oracle
+
+        t0 = time.perf_counter()
+        oracle.check_config_collision(wl.environment(), wl.robot, wl.solver, cfgs[:cpu_sample], 0.5, threads=threads)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": cpu_sample / dt, "unit": "configs/s", "cores": threads, "kind": "port",
+                               "sample": f"first {cpu_sample} configurations, oracle CheckConfigCollision, OpenMP {threads} threads"}
+    return out
+
+
 def load_traffic():
     """HBM bytes per launch of the simulation kernel from the committed rocprofv3 PMC
     summary (profiles/*_pmc.json written by tools/profile_pmc.py), or None."""
@@ -76,6 +115,7 @@ def main():
     ap.add_argument("--particles", type=int, default=PARTICLES_PER_GPU, help="particles per GPU")
     ap.add_argument("--cpu-sample", type=int, default=2048, help="particles in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-config-check", action="store_true", help="skip the batched CheckConfigCollision line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -182,6 +222,10 @@ def main():
             cpu = cpu_baseline(W.cfg3(scale=args.cpu_sample / 65536.0), args.cpu_sample, threads)
             log(f"cpu baseline {cpu['value']:.0f} {UNIT} in {time.perf_counter() - t0:.1f}s")
         value = all_micro / elapsed
+        cc = None
+        if not args.no_config_check:
+            cc = config_check_bench(sim, wl, dev, with_cpu=not args.no_cpu_baseline)
+            log(f"config check {cc['value']:.3e} configs/s")
         line = {
             "metric": METRIC,
             "value": value,
@@ -220,6 +264,7 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },
             "cpu_baseline": cpu,
+            "config_check": cc,
             # share of wave time per phase of the hot path (s_memtime cycle sums, rank 0)
             # (only in profiling builds of the library: -DFKS_PHASE_TIMERS=1, see tools/variant_bench.py)
             "kernel_phases": ({k: (v if k in PHASE_COUNTS else round(v / max(1, phases["particle"]), 4))

@@ -187,6 +187,11 @@ PROTOTYPES = [
         [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p, c_int32],
     ),
+    ("fks_check_config_collision", c_int32,
+     [c_void_p, POINTER(c_double), c_uint64, c_double, POINTER(c_uint8), POINTER(c_uint32)]),
+    ("fks_check_config_collision_device", c_int32,
+     [c_void_p, c_void_p, c_uint64, c_double, c_void_p, c_void_p, c_void_p, c_int32]),
+    ("fks_get_last_check_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
     ("fks_set_call_index", c_int32, [c_void_p, c_uint64]),
     ("fks_get_call_index", c_uint64, [c_void_p]),
     ("fks_get_statistics", c_int32, [c_void_p, POINTER(Statistics)]),

@@ -28,11 +28,23 @@
 extern "C" __global__ void fks_simulate_linked(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se2(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se3(const fksd::SimArgs* args);
+extern "C" __global__ void fks_check_configs_linked(const fksd::SimArgs* args);
+extern "C" __global__ void fks_check_configs_se2(const fksd::SimArgs* args);
+extern "C" __global__ void fks_check_configs_se3(const fksd::SimArgs* args);
 extern "C" __global__ void fks_math_probe(const double* a, const double* b, double* out, uint64_t n);
 
 namespace {
 
 typedef void (*sim_kernel_t)(const fksd::SimArgs*);
+
+/* the batched CheckConfigCollision kernel for one robot family */
+sim_kernel_t check_kernel_for(int robot_type) {
+    switch (robot_type) {
+        case FKS_ROBOT_SE2: return fks_check_configs_se2;
+        case FKS_ROBOT_SE3: return fks_check_configs_se3;
+        default: return fks_check_configs_linked;
+    }
+}
 
 /* the simulation kernel compiled for one robot family (FKS.cpp:4-71 factories) */
 sim_kernel_t kernel_for(int robot_type) {
@@ -186,7 +198,9 @@ struct fks_context {
     fksd::SimArgs* d_args = nullptr;          /* kernel arguments, read through a pointer */
     fksd::SimArgs* h_args = nullptr;          /* pinned staging for d_args */
     bool pending = false;
+    int pending_kind = 0; /* 0 = forward simulation, 1 = batched config check */
     hipStream_t pending_stream = nullptr;
+    fks_call_counters check_last;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::chrono::steady_clock::time_point call_start;
     /* host-API staging */
@@ -640,6 +654,17 @@ static fks_status settle(fks_context* ctx) {
     HIP_TRY(ctx, hipStreamSynchronize(ctx->pending_stream));
     ctx->pending = false;
     const unsigned long long* c = ctx->h_counters;
+    if (ctx->pending_kind == 1) {
+        /* a config check: no simulator statistics, only its own counters */
+        float ms = 0.0f;
+        HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+        ctx->check_last.sdf_bytes = c[fksd::kCntSdfBytes];
+        ctx->check_last.kernel_ms = (double)ms;
+        ctx->check_last.call_ms =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ctx->call_start).count();
+        ctx->check_last.calls = 1;
+        return FKS_OK;
+    }
     ctx->stats.successful_resolves += c[fksd::kCntSuccessful];
     ctx->stats.unsuccessful_resolves += c[fksd::kCntUnsuccessful];
     ctx->stats.free_resolves += c[fksd::kCntFree];
@@ -753,8 +778,106 @@ fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts,
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_counters, ctx->d_counters, fksd::kCounterWords * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, s));
     ctx->pending = true;
+    ctx->pending_kind = 0;
     ctx->pending_stream = s;
     if (synchronize) return settle(ctx);
+    return FKS_OK;
+}
+
+fks_status fks_check_config_collision_device(fks_context* ctx, const double* d_configs, uint64_t n, double inflation_ratio,
+                                             uint8_t* d_out_collided, uint32_t* d_out_error_flags, void* stream,
+                                             int32_t synchronize) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    if (!ctx->has_robot) return fail(ctx, FKS_ERR_NO_ROBOT, "fks_set_robot has not been called");
+    if (n > 0 && (!d_configs || !d_out_collided)) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "null device buffer");
+    if (!(inflation_ratio == inflation_ratio)) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "inflation_ratio is NaN");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    fks_status st = settle(ctx);
+    if (st != FKS_OK) return st;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    ctx->call_start = std::chrono::steady_clock::now();
+    std::memset(&ctx->check_last, 0, sizeof(ctx->check_last));
+    ctx->check_last.particles = n;
+    if (n == 0) return FKS_OK;
+    fksd::SimArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.sdf_g = ctx->sdf_g;
+    a.nrm_g = ctx->nrm_g;
+    a.env_g = ctx->env_g;
+    a.sdf = ctx->d_sdf;
+    a.noff = ctx->d_noff;
+    a.nent = ctx->d_nent;
+    a.oob = ctx->oob;
+    a.has_normals = ctx->has_normals;
+    a.R = ctx->R;
+    a.S = ctx->params;
+    /* SPCS:1403-1404 thresholds, SPCS:923 tolerance */
+    a.thr_env = (inflation_ratio * ctx->env_g.res) - (ctx->params.environment_collision_check_tolerance * ctx->sdf_g.res);
+    a.self_res = (inflation_ratio + 1.0) * ctx->env_g.res;
+    a.starts = d_configs;
+    a.n = n;
+    a.out_collided = d_out_collided;
+    a.out_err = d_out_error_flags;
+    a.counters = ctx->d_counters;
+    a.queue = ctx->d_counters + fksd::kNumCounters;
+    a.scratch = ctx->d_scratch;
+    a.scratch_per_wave = ctx->scratch_per_wave;
+    a.row_cap = 3u * (uint32_t)ctx->R.P;
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds);
+    a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P);
+    *ctx->h_args = a;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, fksd::kCounterWords * sizeof(unsigned long long), s));
+    const uint64_t groups_needed = (n + fksd::kWavesPerGroup - 1) / fksd::kWavesPerGroup;
+    const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? groups_needed : ctx->grid_groups);
+    HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
+    hipLaunchKernelGGL(check_kernel_for(ctx->R.type), dim3(grid), dim3(64 * fksd::kWavesPerGroup), ctx->lds_bytes, s,
+                       static_cast<const fksd::SimArgs*>(ctx->d_args));
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_counters, ctx->d_counters, fksd::kCounterWords * sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost, s));
+    ctx->pending = true;
+    ctx->pending_kind = 1;
+    ctx->pending_stream = s;
+    if (synchronize) return settle(ctx);
+    return FKS_OK;
+}
+
+fks_status fks_check_config_collision(fks_context* ctx, const double* configs, uint64_t n, double inflation_ratio,
+                                      uint8_t* out_collided, uint32_t* out_error_flags) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    if (!ctx->has_robot) return fail(ctx, FKS_ERR_NO_ROBOT, "fks_set_robot has not been called");
+    if (n > 0 && (!configs || !out_collided)) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "null host buffer");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    fks_status st = settle(ctx);
+    if (st != FKS_OK) return st;
+    const size_t W = (size_t)ctx->R.W;
+    if (n > ctx->cap_particles) {
+        HIP_TRY(ctx, ensure(&ctx->d_starts, n * W));
+        HIP_TRY(ctx, ensure(&ctx->d_out, n * W));
+        HIP_TRY(ctx, ensure(&ctx->d_coll, n));
+        HIP_TRY(ctx, ensure(&ctx->d_micro, n));
+        HIP_TRY(ctx, ensure(&ctx->d_res, n));
+        HIP_TRY(ctx, ensure(&ctx->d_err, n));
+        ctx->cap_particles = n;
+    }
+    if (n == 0) return fks_check_config_collision_device(ctx, nullptr, 0, inflation_ratio, nullptr, nullptr, nullptr, 1);
+    HIP_TRY(ctx, hipMemcpy(ctx->d_starts, configs, n * W * sizeof(double), hipMemcpyHostToDevice));
+    st = fks_check_config_collision_device(ctx, ctx->d_starts, n, inflation_ratio, ctx->d_coll, ctx->d_err, nullptr, 1);
+    if (st != FKS_OK) return st;
+    HIP_TRY(ctx, hipMemcpy(out_collided, ctx->d_coll, n, hipMemcpyDeviceToHost));
+    if (out_error_flags) HIP_TRY(ctx, hipMemcpy(out_error_flags, ctx->d_err, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    ctx->check_last.call_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ctx->call_start).count();
+    return FKS_OK;
+}
+
+fks_status fks_get_last_check_counters(const fks_context* ctx, fks_call_counters* out) {
+    if (!ctx || !out) return FKS_ERR_INVALID_ARGUMENT;
+    fks_status st = settle(const_cast<fks_context*>(ctx));
+    if (st != FKS_OK) return st;
+    *out = ctx->check_last;
     return FKS_OK;
 }
 

@@ -250,6 +250,7 @@ struct SimArgs {
     uint32_t pad2;
     LdsLayout L;               /* per-wave LDS carve-out */
     ScratchLayout SL;          /* per-wave scratch carve-out */
+    double self_res;           /* batched CheckConfigCollision: extended-cell size (SPCS:1404) */
 };
 
 enum {

@@ -327,6 +327,14 @@ __device__ double tn_sample(uint32_t k0, uint32_t k1, uint64_t particle, uint32_
 /* Actuator noise does not depend on the particle state, so the samples of the next
  * floor(64 / D) microsteps are drawn at once, one lane per (microstep, dof), into LDS;
  * noise_sample() consumes them (and their error bits) in the DOF lanes. */
+/* call boundaries of the hot loop (build variants: tools/variant_bench.py) */
+#ifndef FKS_QR_ATTR
+#define FKS_QR_ATTR __noinline__
+#endif
+#ifndef FKS_HOT_ATTR
+#define FKS_HOT_ATTR
+#endif
+
 struct Sim;
 __device__ void refill_noise(Sim& s, uint32_t micro0, uint32_t M);
 __device__ __forceinline__ double noise_sample(Sim& s, uint32_t micro);
@@ -934,7 +942,7 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
  * colliding point; algorithmic bytes are counted up to that point, as the reference
  * reads them (its loop returns at the first colliding point).  Provably-free rounds
  * are not read but still counted (4 B per point, all in bounds). */
-__device__ bool env_collision(Sim& s, const double* T) {
+__device__ FKS_HOT_ATTR bool env_collision(Sim& s, const double* T) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const uint64_t skip = skippable_rounds(s, T, kSkipCheck);
@@ -1499,7 +1507,7 @@ __device__ __forceinline__ double col_sel(const double (&a)[DM], int k) {
  * with one row per lane), so every long sum is the same canonical reduction and the
  * results equal qr_solve's bit for bit, without touching scratch memory. */
 template <int DM>
-__device__ __noinline__ void qr_solve_regs(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
+__device__ FKS_QR_ATTR void qr_solve_regs(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
                                            uint32_t Rn, double* x) {
     const SimArgs& A = *Ap;
     const int D = A.R.D;
@@ -1841,7 +1849,7 @@ __device__ __noinline__ void qr_solve(const SimArgs* __restrict__ Ap, double* ld
 /* one controller step: ResolveForwardSimulation (SPCS:1546-1816).
  * returns 0 ok, 1 error; sets collided/failed; result config in res_cfg */
 template <int RT>
-__device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg, bool allow_contacts, bool* out_collided,
+__device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg, bool allow_contacts, bool* out_collided,
                             bool* out_failed, double*& Tcur, double*& Tprev) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
@@ -2003,6 +2011,213 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
 }  // namespace fksd
 
 using namespace fksd;
+
+/* workgroup prologue shared by the kernels: one LDS copy of the robot tables the
+ * inner loops read, then this wave's view of its LDS block and scratch */
+template <int RT>
+__device__ __forceinline__ void setup_wave(const SimArgs* __restrict__ args, double* lds_mem, Sim& s) {
+    const SimArgs& A = *args;
+    const RobotDev& R = A.R;
+    const int wave = (int)(threadIdx.x >> 6);
+    double* shared = lds_mem;
+    {
+        const int t = (int)threadIdx.x, nt = (int)blockDim.x;
+        uint64_t* dj = reinterpret_cast<uint64_t*>(shared + A.L.joints);
+        const uint64_t* sj = reinterpret_cast<const uint64_t*>(R.joints);
+        for (int k = t; k < R.J * kJointWords; k += nt) dj[k] = sj[k];
+        uint64_t* dc = reinterpret_cast<uint64_t*>(shared + A.L.ctrl);
+        const uint64_t* sc = reinterpret_cast<const uint64_t*>(R.ctrl);
+        for (int k = t; k < R.D * kCtrlWords; k += nt) dc[k] = sc[k];
+        int32_t* dd = reinterpret_cast<int32_t*>(shared + A.L.dofj);
+        if (RT == FKS_ROBOT_LINKED && t < R.D) dd[t] = R.dof_joint[t];
+        if (t < 12) shared[A.L.base + t] = R.base[t];
+        if (RT == FKS_ROBOT_LINKED) {
+            for (int k = t; k < 8 * R.G; k += nt)
+                shared[A.L.gbox + k] = (k % 8 == 7) ? (double)R.geom_link[k / 8] : R.geom_box[7 * (k / 8) + k % 8];
+            uint32_t* lp = reinterpret_cast<uint32_t*>(shared + A.L.gpairs);
+            for (int k = t; k < R.npairs && k < kLdsPairs; k += nt)
+                lp[k] = (uint32_t)R.pairs[2 * k] | ((uint32_t)R.pairs[2 * k + 1] << 16);
+        }
+        __syncthreads();
+    }
+    s.A = args;
+    s.shared = shared;
+    s.lds = lds_mem + A.L.shared_total + (uint64_t)wave * A.L.total;
+    s.ldsi = reinterpret_cast<int32_t*>(s.lds + A.L.ints);
+    s.scratch = A.scratch + ((uint64_t)blockIdx.x * kWavesPerGroup + (uint64_t)wave) * A.scratch_per_wave;
+    s.lane = lane_id();
+    s.stats = reinterpret_cast<uint32_t*>(s.lds + s.A->L.misc + 24);
+    s.phase = reinterpret_cast<uint64_t*>(s.lds + s.A->L.misc + 8);
+    s.joints = reinterpret_cast<const JointDev*>(shared + A.L.joints);
+    s.ctrl = reinterpret_cast<const fks_dof_controller*>(shared + A.L.ctrl);
+    s.dofj = reinterpret_cast<const int32_t*>(shared + A.L.dofj);
+    s.base = shared + A.L.base;
+    s.err = 0;
+    s.lane_bytes = 0;
+    s.self_nonempty = false;
+    s.tcur_valid = false;
+}
+
+/* SetPosition(src) into cfg (LDS): joint limits / angle wrap as SetConfig does */
+template <int RT>
+__device__ __forceinline__ void set_position(Sim& s, const double* src, double* cfg) {
+    const int ln = s.lane;
+    if constexpr (RT == FKS_ROBOT_LINKED) {
+        if (ln < s.A->R.D) {
+            const JointDev& jd = s.joints[s.dofj[ln]];
+            cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(src[ln])
+                                                        : clamp(src[ln], jd.lo, jd.hi);
+        }
+    } else if constexpr (RT == FKS_ROBOT_SE2) {
+        if (ln < 3) cfg[ln] = (ln == 2) ? fks_math::enforce_continuous_revolute_bounds(src[2]) : src[ln];
+    } else {
+        if (ln < 12) cfg[ln] = src[ln];
+    }
+    wsync();
+}
+
+/* CheckSelfCollisions (SPCS:1324-1396) at extended cells of size `res`: true iff one
+ * cell holds points of two geometries whose pair is disallowed (CheckPointsForSelfCollision,
+ * SPCS:1277-1322).  Conservative per-geometry key boxes (one lane per geometry) reject
+ * pairs; overlapping pairs compare exact keys. */
+__device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict__ Ap, const double* shared, double* lds,
+                                                       double* scratch, int ln, const double* Tc, double res) {
+    const SimArgs& A = *Ap;
+    const RobotDev& R = A.R;
+    double* box = lds + A.L.box;
+    bool bad = false;
+    if (ln < R.G) {
+        const double* gb = shared + A.L.gbox + 8 * ln;
+        const double* T = Tc + 12 * (int)gb[7];
+        double lo[3], hi[3];
+        if (gb[6] != 0.0) {
+            const D3 wc = xform3(T, D3{gb[0], gb[1], gb[2]});
+            double wh[3];
+            for (int i = 0; i < 3; ++i)
+                wh[i] = (dabs(T[4 * i]) * gb[3] + dabs(T[4 * i + 1]) * gb[4]) + dabs(T[4 * i + 2]) * gb[5];
+            const D3 gc = xform3(A.env_g.inv, wc);
+            const double gcv[3] = {gc.x, gc.y, gc.z};
+            for (int i = 0; i < 3; ++i) {
+                const double* Ir = A.env_g.inv + 4 * i;
+                const double gh = (dabs(Ir[0]) * wh[0] + dabs(Ir[1]) * wh[1]) + dabs(Ir[2]) * wh[2];
+                const double margin = 1e-6 + 1e-9 * (dabs(gcv[i]) + gh);
+                const double l = (gcv[i] - gh - margin) / res;
+                const double h = (gcv[i] + gh + margin) / res;
+                if (!(l > -1e18 && l < 1e18 && h > -1e18 && h < 1e18)) bad = true;
+                lo[i] = __builtin_trunc(l);
+                hi[i] = __builtin_trunc(h);
+            }
+        } else {
+            bad = true;
+        }
+        for (int i = 0; i < 3; ++i) {
+            box[6 * ln + i] = bad ? -__builtin_huge_val() : lo[i];
+            box[6 * ln + 3 + i] = bad ? __builtin_huge_val() : hi[i];
+        }
+    }
+    wsync();
+    bool any = false;
+    for (int k = ln; k < R.npairs; k += kWave) {
+        const int a = R.pairs[2 * k], b = R.pairs[2 * k + 1];
+        bool ov = true;
+        for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
+        any = any || ov;
+    }
+    if (!wave_any(any || bad)) return 0u;
+    /* exact keys of every point (LocationToExtendedGridIndex SPCS:1173-1181) */
+    int64_t* keys = reinterpret_cast<int64_t*>(scratch + A.SL.keys);
+    uint32_t err = 0;
+    for (int i = ln; i < R.P; i += kWave) {
+        const D4 x = xform4(Tc + 12 * (int)R.point_link[i], load_point(R, i));
+        const D4 g = xform4(A.env_g.inv, x);
+        const double q[3] = {g.x / res, g.y / res, g.z / res};
+        for (int a = 0; a < 3; ++a) {
+            int64_t k;
+            if (q[a] != q[a] || q[a] == __builtin_huge_val() || q[a] == -__builtin_huge_val()) {
+                err |= FKS_PARTICLE_ERR_KEY_RANGE;
+                k = 0;
+            } else if (q[a] >= 9.0e18) {
+                k = (int64_t)9000000000000000000ll;
+            } else if (q[a] <= -9.0e18) {
+                k = -(int64_t)9000000000000000000ll;
+            } else {
+                k = (int64_t)q[a];
+            }
+            keys[3 * i + a] = k;
+        }
+    }
+    wsync();
+    bool hit = false;
+    for (int k = 0; k < R.npairs && !wave_any(hit); ++k) {
+        const int a = R.pairs[2 * k], b = R.pairs[2 * k + 1];
+        bool ov = true;
+        for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
+        if (!ov) continue;
+        const int a0 = (int)R.geom_off[a], a1 = (int)R.geom_off[a + 1];
+        const int b0 = (int)R.geom_off[b], b1 = (int)R.geom_off[b + 1];
+        for (int i = a0 + ln; i < a1; i += kWave) {
+            const int64_t kx = keys[3 * i], ky = keys[3 * i + 1], kz = keys[3 * i + 2];
+            for (int j = b0; j < b1 && !hit; ++j) hit = (keys[3 * j] == kx) && (keys[3 * j + 1] == ky) && (keys[3 * j + 2] == kz);
+        }
+    }
+    err = wave_or(err);
+    return (err << 1) | (wave_any(hit) ? 1u : 0u);
+}
+
+/* batched CheckConfigCollision (SPCS:1398-1416): one wave per configuration,
+ * grid-stride over the batch.  A.thr_env holds inflation_ratio * res - tolerance *
+ * sdf_res (SPCS:1403 + 923), A.self_res = (inflation_ratio + 1) * res (SPCS:1404). */
+template <int RT>
+__device__ __forceinline__ void check_configs(const SimArgs* __restrict__ args, double* lds_mem) {
+    Sim s;
+    setup_wave<RT>(args, lds_mem, s);
+    const SimArgs& A = *args;
+    const RobotDev& R = A.R;
+    const int ln = s.lane;
+    double* cfg = s.lds + A.L.cfg;
+    double* T = s.lds + A.L.Tcur;
+    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerGroup;
+    uint64_t bytes_total = 0;
+    for (uint64_t c = (uint64_t)blockIdx.x * kWavesPerGroup + (threadIdx.x >> 6); c < A.n; c += stride) {
+        set_position<RT>(s, A.starts + c * (uint64_t)R.W, cfg);
+        fk<RT>(s, cfg, T);
+        /* CheckEnvironmentCollision: pairs of 64-point rounds, bytes up to the first
+         * colliding point (its loop returns there) */
+        uint64_t lane_bytes = 0;
+        bool env = false;
+        for (int base = 0; base < R.P && !env; base += 2 * kWave) {
+            uint64_t b0 = 0, b1 = 0;
+            double S, G, C;
+            const bool c0 = env_point(A, T, base + ln, &b0, &S, &G, &C);
+            const bool c1 = env_point(A, T, base + kWave + ln, &b1, &S, &G, &C);
+            const uint64_t m0 = __ballot(c0), m1 = __ballot(c1);
+            if (m0) {
+                if (ln <= __ffsll((unsigned long long)m0) - 1) lane_bytes += b0;
+                env = true;
+            } else {
+                lane_bytes += b0;
+                if (m1) {
+                    if (ln <= __ffsll((unsigned long long)m1) - 1) lane_bytes += b1;
+                    env = true;
+                } else {
+                    lane_bytes += b1;
+                }
+            }
+        }
+        uint32_t r = 0;
+        if constexpr (RT == FKS_ROBOT_LINKED) {
+            if (R.self_possible) r = config_self_collision(args, s.shared, s.lds, s.scratch, ln, T, A.self_res);
+        }
+        const uint64_t bytes = wave_sum_u64(lane_bytes);
+        if (ln == 0) {
+            A.out_collided[c] = (env || (r & 1u)) ? 1 : 0;
+            if (A.out_err) A.out_err[c] = r >> 1;
+            bytes_total += bytes;
+        }
+        wsync();
+    }
+    if (ln == 0 && bytes_total) atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes_total);
+}
 
 template <int RT>
 __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ args, double* lds_mem) {
@@ -2171,6 +2386,19 @@ extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se2(const SimArgs* __re
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se3(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
     simulate_particles<FKS_ROBOT_SE3>(args, lds_mem);
+}
+
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_check_configs_linked(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    check_configs<FKS_ROBOT_LINKED>(args, lds_mem);
+}
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_check_configs_se2(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    check_configs<FKS_ROBOT_SE2>(args, lds_mem);
+}
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_check_configs_se3(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    check_configs<FKS_ROBOT_SE3>(args, lds_mem);
 }
 
 /* device self-test of the portable libm (fks_selftest_math) */

@@ -198,6 +198,38 @@ class HipParticleContactSimulator:
                                         int(r["microsteps"][i]), int(r["resolver_iterations"][i]), int(r["error_flags"][i])))
         return out
 
+    def check_config_collisions(self, robot: RobotDescription, configs, inflation_ratio: float = 0.0) -> dict:
+        """Batched CheckConfigCollision (SPCS:1398-1416): configs (n, W) -> collided[n]
+        (bool) and error_flags[n]."""
+        self.set_robot(robot)
+        W = robot.config_width
+        arr = np.ascontiguousarray(np.asarray(configs, dtype=np.float64).reshape(-1, W))
+        n = arr.shape[0]
+        collided = np.zeros(n, dtype=np.uint8)
+        errors = np.zeros(n, dtype=np.uint32)
+        st = self._lib.fks_check_config_collision(self._ctx, _capi.as_ptr(arr, ctypes.c_double), n, float(inflation_ratio),
+                                                  _capi.as_ptr(collided, ctypes.c_uint8), _capi.as_ptr(errors, ctypes.c_uint32))
+        _capi.check(st, self._ctx, "fks_check_config_collision")
+        return {"collided": collided.astype(bool), "error_flags": errors}
+
+    def check_config_collision(self, immutable_robot: RobotDescription, config, inflation_ratio: float) -> bool:
+        """CheckConfigCollision (SPCS:1398-1416) for one configuration."""
+        return bool(self.check_config_collisions(immutable_robot, [config], inflation_ratio)["collided"][0])
+
+    def check_config_collisions_device(self, robot: RobotDescription, d_configs, n: int, inflation_ratio: float,
+                                       d_out_collided, d_out_error_flags=0, stream=0, synchronize=False):
+        """fks_check_config_collision_device: device pointers (int) on `stream`."""
+        self.set_robot(robot)
+        st = self._lib.fks_check_config_collision_device(
+            self._ctx, ctypes.c_void_p(d_configs), n, float(inflation_ratio), ctypes.c_void_p(d_out_collided),
+            ctypes.c_void_p(d_out_error_flags or None), ctypes.c_void_p(stream or None), 1 if synchronize else 0)
+        _capi.check(st, self._ctx, "fks_check_config_collision_device")
+
+    def last_check_counters(self) -> dict:
+        c = _capi.CallCounters()
+        _capi.check(self._lib.fks_get_last_check_counters(self._ctx, ctypes.byref(c)), self._ctx, "counters")
+        return c.as_dict()
+
     def forward_simulate_device(self, robot: RobotDescription, d_starts, n: int, d_targets, num_targets: int,
                                 first_particle_id: int, allow_contacts: bool, d_out_positions, d_out_collided=0,
                                 d_out_microsteps=0, d_out_resolver_iterations=0, d_out_error_flags=0, stream=0,

@@ -17,6 +17,8 @@
  *   fks_forward_simulate       -> SimpleParticleContactSimulator::ForwardSimulateRobots (SPCS:788-804)
  *   fks_reverse_simulate       -> SimpleParticleContactSimulator::ReverseSimulateRobots (SPCS:806-822)
  *   fks_forward_simulate_device-> same as fks_forward_simulate, inputs/outputs already in HBM
+ *   fks_check_config_collision -> SimpleParticleContactSimulator::CheckConfigCollision   (SPCS:1398-1416),
+ *                                 batched (one call per configuration in the reference)
  *   fks_get_statistics         -> SimpleParticleContactSimulator::GetStatistics          (SPCS:488-500)
  *   fks_reset_statistics       -> SimpleParticleContactSimulator::ResetStatistics        (SPCS:502-512)
  *   fks_reset_generators       -> SimpleParticleContactSimulator::ResetGenerators        (SPCS:457-471)
@@ -253,6 +255,25 @@ fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts,
                                        uint32_t* d_out_resolver_iterations,
                                        uint32_t* d_out_error_flags, void* stream,
                                        int32_t synchronize);
+
+/* CheckConfigCollision (SPCS:1398-1416) for a batch of n configurations (host
+ * buffers): SetPosition(config), CheckEnvironmentCollision at threshold
+ * inflation_ratio * res (SPCS:1403, 921-981) and CheckSelfCollisions at extended
+ * cells of (inflation_ratio + 1) * res (SPCS:1404, 1324-1396).  out_collided[i] = 1
+ * if configuration i collides; out_error_flags (may be NULL): FKS_PARTICLE_ERR_KEY_RANGE
+ * for non-finite points.  The reference checks one configuration per call (the
+ * planner's state-validity check); a batch of one is that call. */
+fks_status fks_check_config_collision(fks_context* ctx, const double* configs, uint64_t n,
+                                      double inflation_ratio, uint8_t* out_collided,
+                                      uint32_t* out_error_flags);
+/* Same with device buffers on the caller's stream (see fks_forward_simulate_device). */
+fks_status fks_check_config_collision_device(fks_context* ctx, const double* d_configs, uint64_t n,
+                                             double inflation_ratio, uint8_t* d_out_collided,
+                                             uint32_t* d_out_error_flags, void* stream,
+                                             int32_t synchronize);
+/* counters of the last config-check call: particles = configurations, sdf_bytes,
+ * kernel_ms, call_ms */
+fks_status fks_get_last_check_counters(const fks_context* ctx, fks_call_counters* out);
 
 /* Each forward/reverse call consumes one RNG "call index" (the reference's
  * per-thread std::mt19937_64 streams advance across calls, SPCS:850).  Ranks

@@ -40,6 +40,10 @@ def lib():
             POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_uint64, c_int32, c_int32, c_int32, POINTER(c_double),
             POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32), POINTER(C.Statistics),
             POINTER(C.CallCounters)]
+        L.oracle_check_config_collision.restype = c_int32
+        L.oracle_check_config_collision.argtypes = [
+            POINTER(C.Environment), POINTER(C.SolverParams), POINTER(C.RobotDesc), POINTER(c_double), c_uint64, c_double,
+            c_int32, POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint64)]
         L.oracle_philox4x32_10.restype = None
         L.oracle_philox4x32_10.argtypes = [POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]
         L.oracle_pid_sequence.restype = None
@@ -101,6 +105,27 @@ def forward_simulate(env, robot, solver, frequency, seed, starts, targets, allow
         raise RuntimeError(f"oracle_forward_simulate failed ({st})")
     return {"positions": out, "collided": coll.astype(bool), "microsteps": micro, "resolver_iterations": res, "error_flags": err,
             "statistics": stats.as_dict(), "counters": cc.as_dict()}
+
+
+def check_config_collision(env, robot, solver, configs, inflation_ratio=0.0, threads=0):
+    """CheckConfigCollision (SPCS:1398-1416) for each configuration on the CPU oracle."""
+    L = lib()
+    W = robot.config_width
+    configs = np.ascontiguousarray(np.asarray(configs, dtype=np.float64).reshape(-1, W))
+    n = configs.shape[0]
+    env_c, keep_env = env.to_c()
+    desc, keep_robot = robot.to_c()
+    params = solver.to_c()
+    coll = np.zeros(n, dtype=np.uint8)
+    err = np.zeros(n, dtype=np.uint32)
+    nbytes = np.zeros(n, dtype=np.uint64)
+    st = L.oracle_check_config_collision(ctypes.byref(env_c), ctypes.byref(params), ctypes.byref(desc), _p(configs, c_double), n,
+                                         float(inflation_ratio), int(threads), _p(coll, c_uint8), _p(err, c_uint32),
+                                         _p(nbytes, c_uint64))
+    del keep_env, keep_robot
+    if st != 0:
+        raise RuntimeError(f"oracle_check_config_collision failed ({st})")
+    return {"collided": coll.astype(bool), "error_flags": err, "sdf_bytes": nbytes}
 
 
 def philox(ctr, key):

@@ -603,6 +603,61 @@ class Simulator {
         return std::make_pair(collided, self);
     }
 
+    /* CheckPointsForSelfCollision SPCS:1277-1322: the points of one extended cell
+     * (geometry index, point index) collide if two of their geometries may not touch */
+    bool CheckPointsForSelfCollision(const RobotPtr& current_robot, const std::vector<std::pair<size_t, size_t>>& candidate_points) const {
+        if (candidate_points.size() <= 1) return false;
+        std::map<size_t, std::vector<size_t>> by_link;
+        for (size_t idx = 0; idx < candidate_points.size(); ++idx)
+            by_link[candidate_points[idx].first].push_back(candidate_points[idx].second);
+        if (by_link.size() < 2) return false;
+        for (auto f = by_link.begin(); f != by_link.end(); ++f)
+            for (auto s = by_link.begin(); s != by_link.end(); ++s)
+                if (f != s && !current_robot->CheckIfSelfCollisionAllowed(f->first, s->first)) return true;
+        return false;
+    }
+
+    /* CheckSelfCollisions SPCS:1324-1396 (extended cells of size check_resolution) */
+    bool CheckSelfCollisions(const RobotPtr& current_robot, const LinkGeometries& geoms, double check_resolution,
+                             ParticleCounters& pc) const {
+        if (geoms.size() == 1) return false;
+        if (geoms.size() == 2 && current_robot->CheckIfSelfCollisionAllowed(0, 1)) return false;
+        std::unordered_map<GridIndex, std::vector<std::pair<size_t, size_t>>, GridIndexHash> check_map;
+        bool any_candidate = false;
+        for (size_t link_idx = 0; link_idx < geoms.size(); ++link_idx) {
+            const std::vector<V4>& link_points = *geoms[link_idx].second.points;
+            const Iso T = current_robot->GetLinkTransform(geoms[link_idx].first);
+            for (size_t point_idx = 0; point_idx < link_points.size(); ++point_idx) {
+                const V4 p = xform4(T, link_points[point_idx]);
+                const GridIndex key = LocationToExtendedGridIndex(p, check_resolution, pc);
+                std::vector<std::pair<size_t, size_t>>& cell = check_map[key];
+                if (cell.size() > 1) {
+                    any_candidate = true;
+                } else if (cell.size() == 1) {
+                    if (cell[0].first != link_idx) any_candidate = true;
+                }
+                cell.push_back(std::make_pair(link_idx, point_idx));
+            }
+        }
+        if (!any_candidate) return false;
+        for (auto it = check_map.begin(); it != check_map.end(); ++it)
+            if (CheckPointsForSelfCollision(current_robot, it->second)) return true;
+        return false;
+    }
+
+    /* CheckConfigCollision SPCS:1398-1416 */
+    bool CheckConfigCollision(const RobotPtr& immutable_robot, const Config& config, double inflation_ratio,
+                              ParticleCounters& pc) const {
+        RobotPtr current_robot(immutable_robot->Clone());
+        current_robot->SetPosition(config);
+        const LinkGeometries& geoms = current_robot->GetLinkGeometries();
+        const double environment_collision_distance_threshold = inflation_ratio * env_geom_.res;
+        const double self_collision_check_resolution = (inflation_ratio + 1.0) * env_geom_.res;
+        const bool env_collision = CheckEnvironmentCollision(current_robot, geoms, environment_collision_distance_threshold, pc);
+        const bool self_collision = CheckSelfCollisions(current_robot, geoms, self_collision_check_resolution, pc);
+        return env_collision || self_collision;
+    }
+
     /* EstimateMaxControlInputWorkspaceMotion SPCS:1492-1544 */
     double EstimateMaxControlInputWorkspaceMotion(const RobotPtr& start_robot, const RobotPtr& end_robot) const {
         const LinkGeometries& geoms = start_robot->GetLinkGeometries();
@@ -948,6 +1003,30 @@ int oracle_forward_simulate(const fks_environment* env, const fks_solver_params*
     }
     if (out_stats) *out_stats = stats;
     if (out_counters) *out_counters = cc;
+    return 0;
+}
+
+/* CheckConfigCollision (SPCS:1398-1416) over a batch of configurations; the
+ * reference checks one configuration per call, the planner calls it per sample.
+ * out_sdf_bytes (optional): algorithmic SDF bytes per configuration. */
+int oracle_check_config_collision(const fks_environment* env, const fks_solver_params* params, const fks_robot_desc* robot_desc,
+                                  const double* configs, uint64_t n, double inflation_ratio, int32_t num_threads,
+                                  uint8_t* out_collided, uint32_t* out_error_flags, uint64_t* out_sdf_bytes) {
+    if (!env || !params || !robot_desc || (n > 0 && (!configs || !out_collided))) return 1;
+    const Simulator sim(*env, *params, 1.0, 0);
+    std::shared_ptr<RobotModel> immutable_robot(make_robot(*robot_desc));
+    if (!immutable_robot) return 1;
+    const size_t W = config_width(*robot_desc);
+    const int nthreads = (num_threads > 0) ? num_threads : omp_get_max_threads();
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+    for (int64_t idx = 0; idx < (int64_t)n; ++idx) {
+        ParticleCounters pc;
+        const Config config(configs + (size_t)idx * W, configs + (size_t)idx * W + W);
+        const bool collided = sim.CheckConfigCollision(immutable_robot, config, inflation_ratio, pc);
+        out_collided[idx] = collided ? 1 : 0;
+        if (out_error_flags) out_error_flags[idx] = pc.error_flags;
+        if (out_sdf_bytes) out_sdf_bytes[idx] = pc.sdf_bytes;
+    }
     return 0;
 }
 

@@ -18,6 +18,15 @@ def fks_lib():
     from fast_kinematic_simulator_amd import _capi
 
     build_library()
+    # torch bundles its own HIP runtime; it must initialise before libfks_hip.so's
+    # (/opt/rocm) runtime opens the device, as bench.py does, or torch finds no GPU
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            torch.zeros(1, device="cuda:0")
+    except ImportError:
+        pass
     return _capi.lib()
 
 
