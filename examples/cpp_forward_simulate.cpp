@@ -99,6 +99,22 @@ int main(int argc, char** argv) {
                         r.did_contact ? 1 : 0, r.microsteps, r.resolver_iterations, r.error_flags);
         }
         for (const auto& kv : sim->GetStatistics()) std::printf("# %s %.0f\n", kv.first.c_str(), kv.second);
+        /* the planner's validity check (CheckConfigCollision) on every reached configuration */
+        std::vector<fks::Configuration> reached;
+        for (const auto& r : results) reached.push_back(r.result_config);
+        const std::vector<bool> in_collision = sim->CheckConfigCollisions(robot, reached, 0.25);
+        for (int i = 0; i < n; ++i) std::printf("#check %d %d\n", i, in_collision[i] ? 1 : 0);
+        /* DemonstrateSimulator-style traced run of the particle that needed the most resolver iterations */
+        int worst = 0;
+        for (int i = 0; i < n; ++i)
+            if (results[i].resolver_iterations > results[worst].resolver_iterations) worst = i;
+        fks::ForwardSimulationStepTrace trace;
+        const fks::SimulationResult tr = sim->ForwardSimulateRobot(robot, starts[worst], targets[0], true, trace, true);
+        size_t configs = 0;
+        for (const auto& rs : trace.resolver_steps)
+            for (const auto& c : rs.contact_resolver_steps) configs += c.contact_resolution_steps.size();
+        std::printf("#trace %d %zu %zu %.17g %.17g %.17g %u %u\n", worst, trace.resolver_steps.size(), configs,
+                    tr.result_config[0], tr.result_config[1], tr.result_config[2], tr.microsteps, tr.resolver_iterations);
     } catch (const fks::SimulatorError& e) {
         std::fprintf(stderr, "%s\n", e.what());
         status = e.status() == FKS_ERR_NO_DEVICE ? 3 : 1;

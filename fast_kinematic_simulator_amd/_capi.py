@@ -155,6 +155,20 @@ class CallCounters(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class Trace(ctypes.Structure):
+    """fks_trace: ForwardSimulationStepTrace flattened per particle (include/fks_capi.h)."""
+    _fields_ = [
+        ("step_capacity", c_uint32),
+        ("config_capacity", c_uint32),
+        ("step_inputs", POINTER(c_double)),
+        ("step_microsteps", POINTER(c_uint32)),
+        ("configs", POINTER(c_double)),
+        ("config_tags", POINTER(c_uint32)),
+        ("num_steps", POINTER(c_uint32)),
+        ("num_configs", POINTER(c_uint32)),
+    ]
+
+
 class Obstacle(ctypes.Structure):
     _fields_ = [("pose", c_double * 12), ("extents", c_double * 3), ("object_id", c_uint32), ("reserved", c_uint32)]
 
@@ -186,6 +200,12 @@ PROTOTYPES = [
         c_int32,
         [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p, c_int32],
+    ),
+    (
+        "fks_forward_simulate_traced",
+        c_int32,
+        [c_void_p, POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_int32, POINTER(c_double), POINTER(c_uint8),
+         POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32), POINTER(Trace)],
     ),
     ("fks_check_config_collision", c_int32,
      [c_void_p, POINTER(c_double), c_uint64, c_double, POINTER(c_uint8), POINTER(c_uint32)]),

@@ -28,6 +28,9 @@
 extern "C" __global__ void fks_simulate_linked(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se2(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se3(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_linked_traced(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_se2_traced(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_se3_traced(const fksd::SimArgs* args);
 extern "C" __global__ void fks_check_configs_linked(const fksd::SimArgs* args);
 extern "C" __global__ void fks_check_configs_se2(const fksd::SimArgs* args);
 extern "C" __global__ void fks_check_configs_se3(const fksd::SimArgs* args);
@@ -47,6 +50,14 @@ sim_kernel_t check_kernel_for(int robot_type) {
 }
 
 /* the simulation kernel compiled for one robot family (FKS.cpp:4-71 factories) */
+sim_kernel_t traced_kernel_for(int robot_type) {
+    switch (robot_type) {
+        case FKS_ROBOT_SE2: return fks_simulate_se2_traced;
+        case FKS_ROBOT_SE3: return fks_simulate_se3_traced;
+        default: return fks_simulate_linked_traced;
+    }
+}
+
 sim_kernel_t kernel_for(int robot_type) {
     switch (robot_type) {
         case FKS_ROBOT_SE2: return fks_simulate_se2;
@@ -701,11 +712,24 @@ static fks_status settle(fks_context* ctx) {
     return FKS_OK;
 }
 
-fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts, uint64_t n, const double* d_targets,
-                                       uint64_t num_targets, uint64_t first_particle_id, int32_t allow_contacts,
-                                       double* d_out_positions, uint8_t* d_out_collided, uint32_t* d_out_microsteps,
-                                       uint32_t* d_out_resolver_iterations, uint32_t* d_out_error_flags, void* stream,
-                                       int32_t synchronize) {
+}  // extern "C"
+
+/* device trace buffers of a traced launch (fks_forward_simulate_traced) */
+struct TraceDev {
+    double* inputs;
+    uint32_t* micro;
+    double* cfg;
+    uint32_t* tags;
+    uint32_t* nsteps;
+    uint32_t* ncfg;
+    uint32_t step_cap, cfg_cap;
+};
+
+static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint64_t n, const double* d_targets,
+                                  uint64_t num_targets, uint64_t first_particle_id, int32_t allow_contacts,
+                                  double* d_out_positions, uint8_t* d_out_collided, uint32_t* d_out_microsteps,
+                                  uint32_t* d_out_resolver_iterations, uint32_t* d_out_error_flags, void* stream,
+                                  int32_t synchronize, const TraceDev* tr) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
     if (!ctx->has_robot) return fail(ctx, FKS_ERR_NO_ROBOT, "fks_set_robot has not been called");
     if (n > 0 && (!d_starts || !d_targets || !d_out_positions))
@@ -763,6 +787,16 @@ fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts,
     a.row_cap = 3u * (uint32_t)ctx->R.P;
     a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P);
+    if (tr) {
+        a.tr_inputs = tr->inputs;
+        a.tr_micro = tr->micro;
+        a.tr_cfg = tr->cfg;
+        a.tr_tags = tr->tags;
+        a.tr_nsteps = tr->nsteps;
+        a.tr_ncfg = tr->ncfg;
+        a.tr_step_cap = tr->step_cap;
+        a.tr_cfg_cap = tr->cfg_cap;
+    }
     /* the previous call has settled, so the pinned staging copy is free */
     *ctx->h_args = a;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice, s));
@@ -771,8 +805,8 @@ fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts,
     const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? (groups_needed > 0 ? groups_needed : 1)
                                                                                   : ctx->grid_groups);
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
-    hipLaunchKernelGGL(kernel_for(ctx->R.type), dim3(grid), dim3(64 * fksd::kWavesPerGroup), ctx->lds_bytes, s,
-                       static_cast<const fksd::SimArgs*>(ctx->d_args));
+    hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type) : kernel_for(ctx->R.type), dim3(grid),
+                       dim3(64 * fksd::kWavesPerGroup), ctx->lds_bytes, s, static_cast<const fksd::SimArgs*>(ctx->d_args));
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_counters, ctx->d_counters, fksd::kCounterWords * sizeof(unsigned long long),
@@ -782,6 +816,18 @@ fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts,
     ctx->pending_stream = s;
     if (synchronize) return settle(ctx);
     return FKS_OK;
+}
+
+extern "C" {
+
+fks_status fks_forward_simulate_device(fks_context* ctx, const double* d_starts, uint64_t n, const double* d_targets,
+                                       uint64_t num_targets, uint64_t first_particle_id, int32_t allow_contacts,
+                                       double* d_out_positions, uint8_t* d_out_collided, uint32_t* d_out_microsteps,
+                                       uint32_t* d_out_resolver_iterations, uint32_t* d_out_error_flags, void* stream,
+                                       int32_t synchronize) {
+    return simulate_device(ctx, d_starts, n, d_targets, num_targets, first_particle_id, allow_contacts, d_out_positions,
+                           d_out_collided, d_out_microsteps, d_out_resolver_iterations, d_out_error_flags, stream,
+                           synchronize, nullptr);
 }
 
 fks_status fks_check_config_collision_device(fks_context* ctx, const double* d_configs, uint64_t n, double inflation_ratio,
@@ -883,7 +929,7 @@ fks_status fks_get_last_check_counters(const fks_context* ctx, fks_call_counters
 
 static fks_status simulate_host(fks_context* ctx, const double* starts, uint64_t n, const double* targets, uint64_t num_targets,
                                 int32_t allow_contacts, double* out_positions, uint8_t* out_collided, uint32_t* out_microsteps,
-                                uint32_t* out_resolver_iterations, uint32_t* out_error_flags) {
+                                uint32_t* out_resolver_iterations, uint32_t* out_error_flags, const TraceDev* tr = nullptr) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
     if (!ctx->has_robot) return fail(ctx, FKS_ERR_NO_ROBOT, "fks_set_robot has not been called");
     if (n > 0 && (!starts || !targets || !out_positions)) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "null host buffer");
@@ -914,8 +960,8 @@ static fks_status simulate_host(fks_context* ctx, const double* starts, uint64_t
     }
     HIP_TRY(ctx, hipMemcpy(ctx->d_starts, starts, n * W * sizeof(double), hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(ctx->d_targets, targets, nt * W * sizeof(double), hipMemcpyHostToDevice));
-    st = fks_forward_simulate_device(ctx, ctx->d_starts, n, ctx->d_targets, nt, 0, allow_contacts, ctx->d_out, ctx->d_coll,
-                                     ctx->d_micro, ctx->d_res, ctx->d_err, nullptr, 1);
+    st = simulate_device(ctx, ctx->d_starts, n, ctx->d_targets, nt, 0, allow_contacts, ctx->d_out, ctx->d_coll, ctx->d_micro,
+                         ctx->d_res, ctx->d_err, nullptr, 1, tr);
     if (st != FKS_OK) return st;
     HIP_TRY(ctx, hipMemcpy(out_positions, ctx->d_out, n * W * sizeof(double), hipMemcpyDeviceToHost));
     if (out_collided) HIP_TRY(ctx, hipMemcpy(out_collided, ctx->d_coll, n, hipMemcpyDeviceToHost));
@@ -940,6 +986,69 @@ fks_status fks_reverse_simulate(fks_context* ctx, const double* starts, uint64_t
                                 uint32_t* out_resolver_iterations, uint32_t* out_error_flags) {
     return simulate_host(ctx, starts, n, targets, num_targets, allow_contacts, out_positions, out_collided, out_microsteps,
                          out_resolver_iterations, out_error_flags);
+}
+
+/* ForwardSimulateRobot with enable_tracing = true (SPCS:824-829), batched */
+fks_status fks_forward_simulate_traced(fks_context* ctx, const double* starts, uint64_t n, const double* targets,
+                                       uint64_t num_targets, int32_t allow_contacts, double* out_positions,
+                                       uint8_t* out_collided, uint32_t* out_microsteps, uint32_t* out_resolver_iterations,
+                                       uint32_t* out_error_flags, const fks_trace* trace) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    if (!ctx->has_robot) return fail(ctx, FKS_ERR_NO_ROBOT, "fks_set_robot has not been called");
+    if (!trace || !trace->num_steps || !trace->num_configs ||
+        (trace->step_capacity > 0 && (!trace->step_inputs || !trace->step_microsteps)) ||
+        (trace->config_capacity > 0 && (!trace->configs || !trace->config_tags)))
+        return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "incomplete fks_trace");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t D = (size_t)ctx->R.D, W = (size_t)ctx->R.W;
+    const size_t ns = (size_t)n * trace->step_capacity, nc = (size_t)n * trace->config_capacity;
+    TraceDev tr{};
+    tr.step_cap = trace->step_capacity;
+    tr.cfg_cap = trace->config_capacity;
+    std::vector<void*> allocs;
+    auto alloc = [&](void** p, size_t bytes) {
+        hipError_t e = hipMalloc(p, bytes > 0 ? bytes : 8);
+        if (e == hipSuccess) allocs.push_back(*p);
+        return e;
+    };
+    auto release = [&]() {
+        for (void* p : allocs) (void)hipFree(p);
+    };
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = alloc((void**)&tr.inputs, ns * 2 * D * sizeof(double));
+    if (e == hipSuccess) e = alloc((void**)&tr.micro, ns * sizeof(uint32_t));
+    if (e == hipSuccess) e = alloc((void**)&tr.cfg, nc * W * sizeof(double));
+    if (e == hipSuccess) e = alloc((void**)&tr.tags, nc * 3 * sizeof(uint32_t));
+    if (e == hipSuccess) e = alloc((void**)&tr.nsteps, (size_t)n * sizeof(uint32_t));
+    if (e == hipSuccess) e = alloc((void**)&tr.ncfg, (size_t)n * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        release();
+        return hip_fail(ctx, e, "trace buffers");
+    }
+    fks_status st = simulate_host(ctx, starts, n, targets, num_targets, allow_contacts, out_positions, out_collided,
+                                  out_microsteps, out_resolver_iterations, out_error_flags, &tr);
+    if (st == FKS_OK && n > 0) {
+        struct Copy {
+            void* dst;
+            const void* src;
+            size_t bytes;
+        } copies[] = {{trace->step_inputs, tr.inputs, ns * 2 * D * sizeof(double)},
+                      {trace->step_microsteps, tr.micro, ns * sizeof(uint32_t)},
+                      {trace->configs, tr.cfg, nc * W * sizeof(double)},
+                      {trace->config_tags, tr.tags, nc * 3 * sizeof(uint32_t)},
+                      {trace->num_steps, tr.nsteps, (size_t)n * sizeof(uint32_t)},
+                      {trace->num_configs, tr.ncfg, (size_t)n * sizeof(uint32_t)}};
+        for (const Copy& c : copies) {
+            if (c.bytes == 0) continue;
+            e = hipMemcpy(c.dst, c.src, c.bytes, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) {
+                st = hip_fail(ctx, e, "trace copy");
+                break;
+            }
+        }
+    }
+    release();
+    return st;
 }
 
 fks_status fks_set_call_index(fks_context* ctx, uint64_t call_index) {

@@ -251,6 +251,14 @@ struct SimArgs {
     LdsLayout L;               /* per-wave LDS carve-out */
     ScratchLayout SL;          /* per-wave scratch carve-out */
     double self_res;           /* batched CheckConfigCollision: extended-cell size (SPCS:1404) */
+    /* ForwardSimulationStepTrace buffers of the traced kernels (fks_trace) */
+    double* tr_inputs;
+    uint32_t* tr_micro;
+    double* tr_cfg;
+    uint32_t* tr_tags;
+    uint32_t* tr_nsteps;
+    uint32_t* tr_ncfg;
+    uint32_t tr_step_cap, tr_cfg_cap;
 };
 
 enum {

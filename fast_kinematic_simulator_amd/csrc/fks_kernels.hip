@@ -379,7 +379,43 @@ struct Sim {
     double pid_integral, pid_last; /* DOF lanes */
     bool self_nonempty;
     bool tcur_valid; /* Tcur == FK(particle configuration) from the end of the last step */
+    uint64_t local;            /* particle index within the call (traced kernels) */
+    uint32_t tr_steps, tr_cfgs; /* trace records produced so far (traced kernels) */
 };
+
+/* ForwardSimulationStepTrace records (traced kernel instantiations only) */
+template <bool TR>
+__device__ __forceinline__ void trace_config(Sim& s, const double* cfg, uint32_t micro, uint32_t kind) {
+    if constexpr (TR) {
+        const SimArgs& A = *s.A;
+        const uint32_t k = s.tr_cfgs++;
+        if (k < A.tr_cfg_cap) {
+            const uint64_t rec = s.local * (uint64_t)A.tr_cfg_cap + k;
+            if (s.lane < A.R.W) A.tr_cfg[rec * (uint64_t)A.R.W + s.lane] = cfg[s.lane];
+            if (s.lane == 0) {
+                A.tr_tags[3 * rec] = s.step;
+                A.tr_tags[3 * rec + 1] = micro;
+                A.tr_tags[3 * rec + 2] = kind;
+            }
+        }
+    }
+}
+template <bool TR>
+__device__ __forceinline__ void trace_step(Sim& s, const double* u, const double* ustep, uint32_t M) {
+    if constexpr (TR) {
+        const SimArgs& A = *s.A;
+        const uint32_t k = s.tr_steps++;
+        if (k < A.tr_step_cap) {
+            const int D = A.R.D;
+            const uint64_t rec = s.local * (uint64_t)A.tr_step_cap + k;
+            if (s.lane < D) {
+                A.tr_inputs[rec * 2ull * (uint64_t)D + s.lane] = u[s.lane];
+                A.tr_inputs[rec * 2ull * (uint64_t)D + D + s.lane] = ustep[s.lane];
+            }
+            if (s.lane == 0) A.tr_micro[rec] = M;
+        }
+    }
+}
 
 /* per-phase timers (fks_get_phase_cycles) cost ~10% of wave cycles, so they are
  * compiled in only for profiling builds (-DFKS_PHASE_TIMERS=1); the per-particle
@@ -1848,7 +1884,7 @@ __device__ __noinline__ void qr_solve(const SimArgs* __restrict__ Ap, double* ld
 
 /* one controller step: ResolveForwardSimulation (SPCS:1546-1816).
  * returns 0 ok, 1 error; sets collided/failed; result config in res_cfg */
-template <int RT>
+template <int RT, bool TR>
 __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg, bool allow_contacts, bool* out_collided,
                             bool* out_failed, double*& Tcur, double*& Tprev) {
     const SimArgs& A = *s.A;
@@ -1905,6 +1941,7 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
         }
     }
     tock(s, FKS_PHASE_STEP_SETUP, t0);
+    trace_step<TR>(s, u, ustep, M);
     bool collided = false;
     for (uint32_t micro = 0; micro < M; ++micro) {
         s.micro_count++;
@@ -1930,6 +1967,7 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
         tock(s, FKS_PHASE_MICRO_FK, t0);
         bool in_collision = check_collision<RT>(s, Tprev, Tcur);
         if (s.err) return 1;
+        trace_config<TR>(s, cfg, micro, FKS_TRACE_POST_ACTION);
         if (in_collision) collided = true;
         if (in_collision && allow_contacts) {
             if (ln < W) cfg_act[ln] = cfg[ln];
@@ -1966,8 +2004,10 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
                 tock(s, FKS_PHASE_RESOLVE_APPLY, t0);
                 in_collision = check_collision<RT>(s, Tprev, Tcur);
                 if (s.err) return 1;
+                trace_config<TR>(s, cfg_act, micro, FKS_TRACE_RESOLVER_STEP);
                 iters++;
                 if (iters > A.S.max_resolver_iterations) {
+                    trace_config<TR>(s, cfg_prev, micro, FKS_TRACE_RESOLVE_FAILED);
                     if (ln == 0) {
                         s.stats[kCntUnsuccessful]++;
                         s.stats[s.self_nonempty ? kCntUnsuccessfulSelf : kCntUnsuccessfulEnv]++;
@@ -1990,6 +2030,7 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
             if (ln < W) cfg[ln] = cfg_act[ln];
             wsync();
         } else if (in_collision && !allow_contacts) {
+            trace_config<TR>(s, cfg_prev, micro, FKS_TRACE_CONTACT_STOP);
             if (s.lane == 0) s.stats[kCntSuccessful]++;
             if (ln < W) res_cfg[ln] = cfg_prev[ln];
             wsync();
@@ -2219,7 +2260,7 @@ __device__ __forceinline__ void check_configs(const SimArgs* __restrict__ args, 
     if (ln == 0 && bytes_total) atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes_total);
 }
 
-template <int RT>
+template <int RT, bool TR>
 __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ args, double* lds_mem) {
     const SimArgs& A = *args;
     const RobotDev& R = A.R;
@@ -2274,6 +2315,9 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         wsync();
         if (local >= A.n) break;
         s.pid = A.first_pid + local;
+        s.local = local;
+        s.tr_steps = 0;
+        s.tr_cfgs = 0;
         s.err = 0;
         s.lane_bytes = 0;
         s.micro_count = 0;
@@ -2317,7 +2361,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             wsync();
             tock(s, FKS_PHASE_CONTROL, t0);
             bool rc = false, rf = false;
-            const int status = resolve_step<RT>(s, cfg, res_cfg, A.allow_contacts != 0, &rc, &rf, Tcur, Tprev);
+            const int status = resolve_step<RT, TR>(s, cfg, res_cfg, A.allow_contacts != 0, &rc, &rf, Tcur, Tprev);
             s.err = wave_or(s.err);
             if (status != 0 || s.err) break;
             if (A.allow_contacts || !rc) {
@@ -2350,6 +2394,10 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             if (A.out_micro) A.out_micro[local] = (uint32_t)s.micro_count;
             if (A.out_resolver) A.out_resolver[local] = (uint32_t)s.resolver_count;
             if (A.out_err) A.out_err[local] = s.err;
+            if constexpr (TR) {
+                A.tr_nsteps[local] = s.tr_steps;
+                A.tr_ncfg[local] = s.tr_cfgs;
+            }
             for (int k = 0; k < 8; ++k)
                 if (s.stats[k]) atomicAdd(A.counters + k, (unsigned long long)s.stats[k]);
             atomicAdd(A.counters + kCntSteps, (unsigned long long)s.step_count);
@@ -2377,15 +2425,29 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
 #define FKS_KERNEL_ATTRS __launch_bounds__(64 * kWavesPerGroup) __attribute__((amdgpu_waves_per_eu(FKS_WAVES_PER_EU)))
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
-    simulate_particles<FKS_ROBOT_LINKED>(args, lds_mem);
+    simulate_particles<FKS_ROBOT_LINKED, false>(args, lds_mem);
 }
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se2(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
-    simulate_particles<FKS_ROBOT_SE2>(args, lds_mem);
+    simulate_particles<FKS_ROBOT_SE2, false>(args, lds_mem);
 }
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se3(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
-    simulate_particles<FKS_ROBOT_SE3>(args, lds_mem);
+    simulate_particles<FKS_ROBOT_SE3, false>(args, lds_mem);
+}
+
+/* traced instantiations: ForwardSimulateRobot with enable_tracing (fks_forward_simulate_traced) */
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked_traced(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_LINKED, true>(args, lds_mem);
+}
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se2_traced(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_SE2, true>(args, lds_mem);
+}
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se3_traced(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_SE3, true>(args, lds_mem);
 }
 
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_check_configs_linked(const SimArgs* __restrict__ args) {

@@ -17,6 +17,7 @@ import numpy as np
 from . import _capi
 from .environment import SimulatorEnvironment
 from .robots import RobotDescription
+from .trace import ForwardSimulationStepTrace, TraceBuffers
 
 
 @dataclass
@@ -185,6 +186,47 @@ class HipParticleContactSimulator:
                                allow_contacts: bool) -> SimulationResult:
         """ForwardSimulateRobot (SPCS:824-829) as a batch of one."""
         return self._results(immutable_robot, [start_position], [target_position], allow_contacts, reverse=False)[0]
+
+    def forward_simulate_traced(self, robot: RobotDescription, start_positions, target_positions, allow_contacts: bool,
+                                step_capacity: Optional[int] = None, config_capacity: int = 4096):
+        """ForwardSimulateRobot with ``enable_tracing = true`` (SPCS:824-829) for a batch:
+        returns (result dict as forward_simulate_arrays, TraceBuffers).  Capacities are
+        per particle; records past them are counted, not stored (``truncated``)."""
+        self.set_robot(robot)
+        W, D = robot.config_width, robot.num_dofs
+        starts = np.ascontiguousarray(np.asarray(start_positions, dtype=np.float64).reshape(-1, W))
+        targets = np.ascontiguousarray(np.asarray(target_positions, dtype=np.float64).reshape(-1, W))
+        n = starts.shape[0]
+        if n > 0 and targets.shape[0] not in (1, n):
+            raise ValueError("target_positions must hold 1 or len(start_positions) configurations (SPCS:792)")
+        if step_capacity is None:
+            step_capacity = max(1, int(self.solver_config.forward_simulation_time * self.simulation_controller_frequency))
+        buf = TraceBuffers(n, D, W, step_capacity, config_capacity)
+        tr = buf.to_c()
+        out = np.zeros((n, W), dtype=np.float64)
+        collided = np.zeros(n, dtype=np.uint8)
+        micro = np.zeros(n, dtype=np.uint32)
+        resolver = np.zeros(n, dtype=np.uint32)
+        errors = np.zeros(n, dtype=np.uint32)
+        st = self._lib.fks_forward_simulate_traced(
+            self._ctx, _capi.as_ptr(starts, ctypes.c_double), n, _capi.as_ptr(targets, ctypes.c_double), targets.shape[0],
+            1 if allow_contacts else 0, _capi.as_ptr(out, ctypes.c_double), _capi.as_ptr(collided, ctypes.c_uint8),
+            _capi.as_ptr(micro, ctypes.c_uint32), _capi.as_ptr(resolver, ctypes.c_uint32), _capi.as_ptr(errors, ctypes.c_uint32),
+            ctypes.byref(tr))
+        _capi.check(st, self._ctx, "fks_forward_simulate_traced")
+        return ({"positions": out, "collided": collided.astype(bool), "microsteps": micro, "resolver_iterations": resolver,
+                 "error_flags": errors}, buf)
+
+    def forward_simulate_robot_traced(self, immutable_robot: RobotDescription, start_position, target_position,
+                                      allow_contacts: bool):
+        """ForwardSimulateRobot(..., trace, enable_tracing=true, ...) (SPCS:824-829):
+        (SimulationResult, ForwardSimulationStepTrace)."""
+        W = immutable_robot.config_width
+        r, buf = self.forward_simulate_traced(immutable_robot, [start_position], [target_position], allow_contacts)
+        tgt = np.asarray(target_position, dtype=np.float64).reshape(W)
+        res = SimulationResult(r["positions"][0].copy(), tgt.copy(), bool(r["collided"][0]), True, int(r["microsteps"][0]),
+                               int(r["resolver_iterations"][0]), int(r["error_flags"][0]))
+        return res, buf.particle(0)
 
     def _results(self, robot, starts, targets, allow_contacts, reverse):
         W = robot.config_width

@@ -18,6 +18,7 @@
 #ifndef FAST_KINEMATIC_SIMULATOR_AMD_HIP_PARTICLE_CONTACT_SIMULATOR_HPP
 #define FAST_KINEMATIC_SIMULATOR_AMD_HIP_PARTICLE_CONTACT_SIMULATOR_HPP
 
+#include <algorithm>
 #include <cstdint>
 #include <functional>
 #include <memory>
@@ -62,6 +63,23 @@ struct SimulationResult {
     uint32_t error_flags = 0; /* FKS_PARTICLE_ERR_* */
 };
 
+/* simple_simulator_interface::ForwardSimulationStepTrace as filled at SPCS:1583-1595,
+ * 1615-1618, 1701-1704, 1712-1715, 1776-1779.  `kinds` tags each configuration
+ * with the FKS_TRACE_* push site it came from. */
+struct ForwardSimulationContactResolverStepTrace {
+    std::vector<Configuration> contact_resolution_steps;
+    std::vector<uint32_t> kinds;
+};
+struct ForwardSimulationResolverTrace {
+    std::vector<double> control_input;      /* real_control_input = u * dt (SPCS:1549) */
+    std::vector<double> control_input_step; /* real_control_input / microsteps (SPCS:1568) */
+    std::vector<ForwardSimulationContactResolverStepTrace> contact_resolver_steps;
+};
+struct ForwardSimulationStepTrace {
+    std::vector<ForwardSimulationResolverTrace> resolver_steps;
+    bool truncated = false; /* records beyond the trace capacity were dropped */
+};
+
 /* fast_kinematic_simulator::GetDefaultSolverParameters (FKS.hpp:13-16) */
 inline fks_solver_params GetDefaultSolverParameters() {
     fks_solver_params p;
@@ -97,6 +115,7 @@ class RobotDescription {
         allowed_pairs.push_back(geometry_a);
         allowed_pairs.push_back(geometry_b);
     }
+    int32_t NumDofs() const { return type == FKS_ROBOT_SE2 ? 3 : (type == FKS_ROBOT_SE3 ? 6 : num_dofs); }
     int32_t ConfigurationWidth() const {
         return type == FKS_ROBOT_SE2 ? 3 : (type == FKS_ROBOT_SE3 ? 12 : num_dofs);
     }
@@ -133,6 +152,7 @@ class HipParticleContactSimulator {
         check(fks_create(&environment, &solver_config, simulation_controller_frequency, prng_seed, debug_level, device, &ctx),
               nullptr, "fks_create");
         ctx_.reset(ctx);
+        forward_steps_ = (uint32_t)std::max(1.0, solver_config.forward_simulation_time * simulation_controller_frequency);
     }
 
     /* SPCS:446-455 */
@@ -178,10 +198,81 @@ class HipParticleContactSimulator {
                                           const Configuration& target_position, bool allow_contacts) {
         return Simulate(immutable_robot, {start_position}, {target_position}, allow_contacts, false).front();
     }
+    /* ForwardSimulateRobot(..., trace, enable_tracing, display_fn) (SPCS:824-829): the
+     * traced kernel records the trace; without enable_tracing this is the call above */
+    SimulationResult ForwardSimulateRobot(const RobotDescription& immutable_robot, const Configuration& start_position,
+                                          const Configuration& target_position, bool allow_contacts,
+                                          ForwardSimulationStepTrace& trace, bool enable_tracing,
+                                          const DisplayFn& display_fn = {}, uint32_t config_capacity = 4096) {
+        (void)display_fn;
+        if (!enable_tracing) return ForwardSimulateRobot(immutable_robot, start_position, target_position, allow_contacts);
+        SetRobot(immutable_robot);
+        const size_t W = (size_t)immutable_robot.ConfigurationWidth(), D = (size_t)immutable_robot.NumDofs();
+        if (start_position.size() != W || target_position.size() != W)
+            throw std::invalid_argument("configuration has the wrong width");
+        const uint32_t step_cap = forward_steps_, cfg_cap = config_capacity;
+        std::vector<double> inputs((size_t)step_cap * 2 * D), configs((size_t)cfg_cap * W), out(W);
+        std::vector<uint32_t> micro(step_cap), tags((size_t)cfg_cap * 3);
+        uint32_t num_steps = 0, num_configs = 0, microsteps = 0, resolver = 0, errors = 0;
+        uint8_t collided = 0;
+        fks_trace t{step_cap, cfg_cap, inputs.data(), micro.data(), configs.data(), tags.data(), &num_steps, &num_configs};
+        check(fks_forward_simulate_traced(ctx_.get(), start_position.data(), 1, target_position.data(), 1, allow_contacts ? 1 : 0,
+                                          out.data(), &collided, &microsteps, &resolver, &errors, &t),
+              ctx_.get(), "ForwardSimulateRobot");
+        trace.truncated = trace.truncated || num_steps > step_cap || num_configs > cfg_cap;
+        const size_t base = trace.resolver_steps.size(); /* the reference appends to the caller's trace */
+        for (uint32_t k = 0; k < num_steps && k < step_cap; ++k) {
+            ForwardSimulationResolverTrace rs;
+            rs.control_input.assign(inputs.begin() + (size_t)k * 2 * D, inputs.begin() + (size_t)k * 2 * D + D);
+            rs.control_input_step.assign(inputs.begin() + (size_t)k * 2 * D + D, inputs.begin() + (size_t)(k + 1) * 2 * D);
+            trace.resolver_steps.push_back(std::move(rs));
+        }
+        int64_t last_step = -1, last_micro = -1;
+        for (uint32_t k = 0; k < num_configs && k < cfg_cap; ++k) {
+            const uint32_t st = tags[3 * k], mi = tags[3 * k + 1];
+            if (base + st >= trace.resolver_steps.size()) break;
+            ForwardSimulationResolverTrace& rs = trace.resolver_steps[base + st];
+            if ((int64_t)st != last_step || (int64_t)mi != last_micro) rs.contact_resolver_steps.emplace_back();
+            last_step = st;
+            last_micro = mi;
+            rs.contact_resolver_steps.back().contact_resolution_steps.emplace_back(configs.begin() + (size_t)k * W,
+                                                                                   configs.begin() + (size_t)(k + 1) * W);
+            rs.contact_resolver_steps.back().kinds.push_back(tags[3 * k + 2]);
+        }
+        SimulationResult r;
+        r.result_config = out;
+        r.target_config = target_position;
+        r.did_contact = collided != 0;
+        r.microsteps = microsteps;
+        r.resolver_iterations = resolver;
+        r.error_flags = errors;
+        return r;
+    }
     /* ReverseSimulateRobot (SPCS:831-836) */
     SimulationResult ReverseSimulateRobot(const RobotDescription& immutable_robot, const Configuration& start_position,
                                           const Configuration& target_position, bool allow_contacts) {
         return Simulate(immutable_robot, {start_position}, {target_position}, allow_contacts, true).front();
+    }
+
+    /* CheckConfigCollision (SPCS:1398-1416) */
+    bool CheckConfigCollision(const RobotDescription& immutable_robot, const Configuration& config, double inflation_ratio) {
+        return CheckConfigCollisions(immutable_robot, {config}, inflation_ratio).front();
+    }
+    /* the same check for a batch of configurations in one launch */
+    std::vector<bool> CheckConfigCollisions(const RobotDescription& immutable_robot, const std::vector<Configuration>& configs,
+                                            double inflation_ratio) {
+        SetRobot(immutable_robot);
+        const size_t W = (size_t)immutable_robot.ConfigurationWidth();
+        const size_t n = configs.size();
+        std::vector<double> c(n * W);
+        for (size_t i = 0; i < n; ++i) {
+            if (configs[i].size() != W) throw std::invalid_argument("configuration has the wrong width");
+            std::copy(configs[i].begin(), configs[i].end(), c.begin() + i * W);
+        }
+        std::vector<uint8_t> collided(n);
+        check(fks_check_config_collision(ctx_.get(), c.data(), n, inflation_ratio, collided.data(), nullptr), ctx_.get(),
+              "CheckConfigCollision");
+        return std::vector<bool>(collided.begin(), collided.end());
     }
 
     fks_context* context() { return ctx_.get(); }
@@ -192,6 +283,7 @@ class HipParticleContactSimulator {
     };
     std::unique_ptr<fks_context, Destroy> ctx_;
     const RobotDescription* robot_ = nullptr;
+    uint32_t forward_steps_ = 1; /* controller steps per simulation (SPCS:856): the trace's step capacity */
 
     void SetRobot(const RobotDescription& robot) {
         if (robot_ == &robot) return;

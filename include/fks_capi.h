@@ -275,6 +275,39 @@ fks_status fks_check_config_collision_device(fks_context* ctx, const double* d_c
  * kernel_ms, call_ms */
 fks_status fks_get_last_check_counters(const fks_context* ctx, fks_call_counters* out);
 
+/* ForwardSimulationStepTrace (simple_simulator_interface, filled at SPCS:1583-1595,
+ * 1615-1618, 1701-1704, 1712-1715, 1776-1779) flattened per particle:
+ *   resolver_steps[s].control_input / .control_input_step  -> step record s
+ *   resolver_steps[s].contact_resolver_steps[m].contact_resolution_steps[k]
+ *                                                          -> config records tagged (s, m, kind)
+ * in the order the reference appends them.  Buffers are caller-owned, n particles x
+ * capacity each; records beyond a capacity are counted but not stored. */
+#define FKS_TRACE_POST_ACTION 0u    /* post_action_configuration of microstep m (SPCS:1617)          */
+#define FKS_TRACE_RESOLVER_STEP 1u  /* active_configuration after a resolver iteration (SPCS:1703)  */
+#define FKS_TRACE_RESOLVE_FAILED 2u /* previous_configuration, resolver gave up (SPCS:1714)         */
+#define FKS_TRACE_CONTACT_STOP 3u   /* previous_configuration, contact with allow_contacts=false (SPCS:1778) */
+typedef struct {
+    uint32_t step_capacity;    /* step records per particle */
+    uint32_t config_capacity;  /* configuration records per particle */
+    double* step_inputs;       /* n * step_capacity * 2D: control_input (u * dt), control_input_step */
+    uint32_t* step_microsteps; /* n * step_capacity: number of microsteps of the step */
+    double* configs;           /* n * config_capacity * W */
+    uint32_t* config_tags;     /* n * config_capacity * 3: controller step, microstep, FKS_TRACE_* kind */
+    uint32_t* num_steps;       /* n: step records produced (may exceed step_capacity) */
+    uint32_t* num_configs;     /* n: configuration records produced (may exceed config_capacity) */
+} fks_trace;
+
+/* ForwardSimulateRobot(..., trace, enable_tracing = true, ...) (SPCS:824-829) for a
+ * batch: same results as fks_forward_simulate plus the trace of every particle
+ * (host buffers; the traced kernel is a separate instantiation, the untraced path
+ * does not pay for it). */
+fks_status fks_forward_simulate_traced(fks_context* ctx, const double* starts, uint64_t n,
+                                       const double* targets, uint64_t num_targets,
+                                       int32_t allow_contacts, double* out_positions,
+                                       uint8_t* out_collided, uint32_t* out_microsteps,
+                                       uint32_t* out_resolver_iterations, uint32_t* out_error_flags,
+                                       const fks_trace* trace);
+
 /* Each forward/reverse call consumes one RNG "call index" (the reference's
  * per-thread std::mt19937_64 streams advance across calls, SPCS:850).  Ranks
  * that shard one logical call must use the same index: set it explicitly. */

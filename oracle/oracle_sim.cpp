@@ -48,7 +48,31 @@ struct ParticleCounters {
     uint64_t lsq_rows = 0;
     uint32_t error_flags = 0;
     fks_statistics stats;
+    struct TraceSink* trace = nullptr; /* ForwardSimulationStepTrace of this particle (traced calls only) */
     ParticleCounters() { std::memset(&stats, 0, sizeof(stats)); }
+};
+
+/* ForwardSimulationStepTrace (simple_simulator_interface) flattened as in
+ * include/fks_capi.h fks_trace: one record per resolver_steps entry
+ * (SPCS:1583-1588) and one per contact_resolution_steps push (SPCS:1617,
+ * 1703, 1714, 1778), tagged with (controller step, microstep, kind) */
+struct TraceSink {
+    std::vector<double> step_inputs; /* per step: real_control_input, control_input_step */
+    std::vector<uint32_t> step_microsteps;
+    std::vector<double> configs;
+    std::vector<uint32_t> config_tags;
+    uint32_t step = 0;
+    void add_step(const std::vector<double>& u, const std::vector<double>& ustep, uint32_t m) {
+        step_inputs.insert(step_inputs.end(), u.begin(), u.end());
+        step_inputs.insert(step_inputs.end(), ustep.begin(), ustep.end());
+        step_microsteps.push_back(m);
+    }
+    void add_config(const std::vector<double>& q, uint32_t micro, uint32_t kind) {
+        configs.insert(configs.end(), q.begin(), q.end());
+        config_tags.push_back(step);
+        config_tags.push_back(micro);
+        config_tags.push_back(kind);
+    }
 };
 
 /* truncate toward zero like (int64_t)x; non-finite/huge values are rejected
@@ -776,6 +800,7 @@ class Simulator {
             pc.error_flags |= FKS_PARTICLE_ERR_MICROSTEP_MOTION; /* assert(false), SPCS:1570-1575 */
             return ResolveResult{robot->GetPosition(), false, false, true};
         }
+        if (pc.trace) pc.trace->add_step(real_control_input, control_input_step, number_microsteps); /* SPCS:1583-1588 */
         bool collided = false;
         std::vector<double> J, b;
         for (uint32_t micro_step = 0; micro_step < number_microsteps; ++micro_step) {
@@ -792,6 +817,7 @@ class Simulator {
             SelfMap& self_collision_map = collision_check.second;
             bool in_collision = collision_check.first;
             if (in_collision) collided = true;
+            if (pc.trace) pc.trace->add_config(post_action_configuration, micro_step, FKS_TRACE_POST_ACTION); /* SPCS:1615-1618 */
             if (in_collision && allow_contacts) {
                 Config active_configuration = post_action_configuration;
                 uint32_t resolver_iterations = 0;
@@ -827,7 +853,9 @@ class Simulator {
                     self_collision_map = new_check.second;
                     in_collision = new_check.first;
                     resolver_iterations++;
+                    if (pc.trace) pc.trace->add_config(active_configuration, micro_step, FKS_TRACE_RESOLVER_STEP); /* SPCS:1701-1704 */
                     if (resolver_iterations > solver_.max_resolver_iterations) {
+                        if (pc.trace) pc.trace->add_config(previous_configuration, micro_step, FKS_TRACE_RESOLVE_FAILED); /* SPCS:1712-1715 */
                         pc.stats.unsuccessful_resolves++;
                         if (self_collision_map.size() > 0)
                             pc.stats.unsuccessful_self_collision_resolves++;
@@ -846,6 +874,7 @@ class Simulator {
                     }
                 }
             } else if (in_collision && !allow_contacts) {
+                if (pc.trace) pc.trace->add_config(previous_configuration, micro_step, FKS_TRACE_CONTACT_STOP); /* SPCS:1776-1779 */
                 pc.stats.successful_resolves++;
                 return ResolveResult{previous_configuration, true, false, false};
             }
@@ -867,6 +896,7 @@ class Simulator {
         for (uint32_t step = 0; step < forward_simulation_steps; ++step) {
             pc.controller_steps++;
             rng.step = step;
+            if (pc.trace) pc.trace->step = step;
             const std::vector<double> control_action = robot->GenerateControlAction(target_position, simulation_controller_interval_);
             const ResolveResult result =
                 ResolveForwardSimulation(robot, control_action, simulation_controller_interval_, rng, allow_contacts, pc);
@@ -930,12 +960,12 @@ extern "C" {
 /* ForwardSimulateRobots (SPCS:788-804) on the CPU.  rng_mode 0 = counter
  * (Philox, parity with the HIP path), 1 = reference (per-OpenMP-thread
  * std::mt19937_64 seeded as SPCS:431-441).  num_threads <= 0: OpenMP default. */
-int oracle_forward_simulate(const fks_environment* env, const fks_solver_params* params, double frequency, uint64_t seed,
-                            uint64_t call_index, const fks_robot_desc* robot_desc, const double* starts, uint64_t n,
-                            const double* targets, uint64_t num_targets, uint64_t first_particle_id, int32_t allow_contacts,
-                            int32_t rng_mode, int32_t num_threads, double* out_positions, uint8_t* out_collided,
-                            uint32_t* out_microsteps, uint32_t* out_resolver_iterations, uint32_t* out_error_flags,
-                            fks_statistics* out_stats, fks_call_counters* out_counters) {
+static int forward_simulate_impl(const fks_environment* env, const fks_solver_params* params, double frequency, uint64_t seed,
+                                 uint64_t call_index, const fks_robot_desc* robot_desc, const double* starts, uint64_t n,
+                                 const double* targets, uint64_t num_targets, uint64_t first_particle_id, int32_t allow_contacts,
+                                 int32_t rng_mode, int32_t num_threads, double* out_positions, uint8_t* out_collided,
+                                 uint32_t* out_microsteps, uint32_t* out_resolver_iterations, uint32_t* out_error_flags,
+                                 fks_statistics* out_stats, fks_call_counters* out_counters, const fks_trace* trace) {
     if (!env || !params || !robot_desc || (n > 0 && (!starts || !targets || !out_positions))) return 1;
     if (n > 0 && num_targets != 1 && num_targets != n) return 1;
     if (params->resolve_correction_step_scaling_decay_iterations == 0) return 1;
@@ -953,9 +983,11 @@ int oracle_forward_simulate(const fks_environment* env, const fks_solver_params*
         for (int t = 0; t < nthreads; ++t) rngs.push_back(std::mt19937_64(seed_dist(prng)));
     }
     std::vector<ParticleCounters> counters((size_t)n);
+    std::vector<TraceSink> sinks(trace ? (size_t)n : 0);
 #pragma omp parallel for schedule(static) num_threads(nthreads)
     for (int64_t idx = 0; idx < (int64_t)n; ++idx) {
         ParticleCounters& pc = counters[(size_t)idx];
+        if (trace) pc.trace = &sinks[(size_t)idx];
         const Config start(starts + (size_t)idx * W, starts + (size_t)idx * W + W);
         const double* tp = (num_targets == n) ? targets + (size_t)idx * W : targets;
         const Config target(tp, tp + W);
@@ -977,6 +1009,23 @@ int oracle_forward_simulate(const fks_environment* env, const fks_solver_params*
         if (out_microsteps) out_microsteps[idx] = (uint32_t)pc.microsteps;
         if (out_resolver_iterations) out_resolver_iterations[idx] = (uint32_t)pc.resolver_iterations;
         if (out_error_flags) out_error_flags[idx] = pc.error_flags;
+        if (trace) {
+            const TraceSink& ts = *pc.trace;
+            const size_t D = ts.step_microsteps.empty() ? 0 : ts.step_inputs.size() / (2 * ts.step_microsteps.size());
+            const uint32_t ns = (uint32_t)ts.step_microsteps.size(), nc = (uint32_t)ts.config_tags.size() / 3;
+            trace->num_steps[idx] = ns;
+            trace->num_configs[idx] = nc;
+            for (uint32_t k = 0; k < ns && k < trace->step_capacity; ++k) {
+                const size_t rec = (size_t)idx * trace->step_capacity + k;
+                std::memcpy(trace->step_inputs + rec * 2 * D, ts.step_inputs.data() + (size_t)k * 2 * D, 2 * D * sizeof(double));
+                trace->step_microsteps[rec] = ts.step_microsteps[k];
+            }
+            for (uint32_t k = 0; k < nc && k < trace->config_capacity; ++k) {
+                const size_t rec = (size_t)idx * trace->config_capacity + k;
+                std::memcpy(trace->configs + rec * W, ts.configs.data() + (size_t)k * W, W * sizeof(double));
+                std::memcpy(trace->config_tags + rec * 3, ts.config_tags.data() + (size_t)k * 3, 3 * sizeof(uint32_t));
+            }
+        }
     }
     fks_statistics stats;
     std::memset(&stats, 0, sizeof(stats));
@@ -1004,6 +1053,30 @@ int oracle_forward_simulate(const fks_environment* env, const fks_solver_params*
     if (out_stats) *out_stats = stats;
     if (out_counters) *out_counters = cc;
     return 0;
+}
+
+int oracle_forward_simulate(const fks_environment* env, const fks_solver_params* params, double frequency, uint64_t seed,
+                            uint64_t call_index, const fks_robot_desc* robot_desc, const double* starts, uint64_t n,
+                            const double* targets, uint64_t num_targets, uint64_t first_particle_id, int32_t allow_contacts,
+                            int32_t rng_mode, int32_t num_threads, double* out_positions, uint8_t* out_collided,
+                            uint32_t* out_microsteps, uint32_t* out_resolver_iterations, uint32_t* out_error_flags,
+                            fks_statistics* out_stats, fks_call_counters* out_counters) {
+    return forward_simulate_impl(env, params, frequency, seed, call_index, robot_desc, starts, n, targets, num_targets,
+                                 first_particle_id, allow_contacts, rng_mode, num_threads, out_positions, out_collided,
+                                 out_microsteps, out_resolver_iterations, out_error_flags, out_stats, out_counters, nullptr);
+}
+
+/* ForwardSimulateRobot(..., trace, enable_tracing = true, ...) (SPCS:824-829)
+ * for a batch, the trace flattened into the caller's fks_trace buffers */
+int oracle_forward_simulate_traced(const fks_environment* env, const fks_solver_params* params, double frequency,
+                                   uint64_t seed, uint64_t call_index, const fks_robot_desc* robot_desc, const double* starts,
+                                   uint64_t n, const double* targets, uint64_t num_targets, int32_t allow_contacts,
+                                   int32_t num_threads, double* out_positions, uint8_t* out_collided, uint32_t* out_microsteps,
+                                   uint32_t* out_resolver_iterations, uint32_t* out_error_flags, const fks_trace* trace) {
+    if (!trace || !trace->num_steps || !trace->num_configs) return 1;
+    return forward_simulate_impl(env, params, frequency, seed, call_index, robot_desc, starts, n, targets, num_targets, 0,
+                                 allow_contacts, 0, num_threads, out_positions, out_collided, out_microsteps,
+                                 out_resolver_iterations, out_error_flags, nullptr, nullptr, trace);
 }
 
 /* CheckConfigCollision (SPCS:1398-1416) over a batch of configurations; the

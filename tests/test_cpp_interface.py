@@ -62,4 +62,16 @@ def test_cpp_interface_matches_python_mirror():
     assert [int(row[7]) for row in rows] == [int(v) for v in r["error_flags"]]
     # the scene makes contact: the box sits on the arm's path
     assert r["collided"].any() and r["resolver_iterations"].sum() > 0
+    checks = [int(l.split()[2]) for l in p.stdout.splitlines() if l.startswith("#check")]
+    c = sim.check_config_collisions(robot, r["positions"], 0.25)
+    assert checks == [int(v) for v in c["collided"]]
+    # the traced single-particle call (ForwardSimulateRobot with enable_tracing)
+    t = [l.split()[1:] for l in p.stdout.splitlines() if l.startswith("#trace")][0]
+    worst = int(np.argmax(r["resolver_iterations"]))
+    assert int(t[0]) == worst
+    res, trace = sim.forward_simulate_robot_traced(robot, starts[worst], [1.1, 0.2, -0.3], True)
+    nconf = sum(len(c.contact_resolution_steps) for rs in trace.resolver_steps for c in rs.contact_resolver_steps)
+    assert (int(t[1]), int(t[2])) == (len(trace.resolver_steps), nconf)
+    assert np.array_equal(np.array([float(v) for v in t[3:6]]), res.result_config)
+    assert (int(t[6]), int(t[7])) == (res.microsteps, res.resolver_iterations)
     sim.close()
