@@ -1009,6 +1009,8 @@ fks_status fks_forward_simulate_traced(fks_context* ctx, const double* starts, u
     auto alloc = [&](void** p, size_t bytes) {
         hipError_t e = hipMalloc(p, bytes > 0 ? bytes : 8);
         if (e == hipSuccess) allocs.push_back(*p);
+        /* records past a particle's count stay zero, as in the caller's view */
+        if (e == hipSuccess) e = hipMemset(*p, 0, bytes > 0 ? bytes : 8);
         return e;
     };
     auto release = [&]() {
