@@ -26,6 +26,7 @@ STATUS_NAMES = {
 
 ROBOT_LINKED, ROBOT_SE2, ROBOT_SE3 = 0, 1, 2
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_CONTINUOUS, JOINT_PRISMATIC = 0, 1, 2, 4
+OK, ERR_INVALID_ARGUMENT, ERR_HIP, ERR_NO_ROBOT, ERR_OUT_OF_MEMORY, ERR_UNSUPPORTED, ERR_NO_DEVICE = 0, 1, 2, 3, 4, 5, 6
 
 NUM_PHASES = 16
 PHASE_NAMES = ["particle", "control", "step_setup", "micro_input", "micro_fk", "env_check", "self_check", "corrections",
@@ -173,6 +174,14 @@ class Obstacle(ctypes.Structure):
     _fields_ = [("pose", c_double * 12), ("extents", c_double * 3), ("object_id", c_uint32), ("reserved", c_uint32)]
 
 
+class EnvBuildStats(ctypes.Structure):
+    _fields_ = [("cells", c_uint64), ("obstacle_samples", c_uint64), ("normal_entries", c_uint64), ("gpu_ms", c_double),
+                ("total_ms", c_double)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 # (name, restype, argtypes) of every symbol include/fks_capi.h declares
 PROTOTYPES = [
     ("fks_abi_version", c_int32, []),
@@ -224,7 +233,10 @@ PROTOTYPES = [
     ("fks_reset_total_counters", c_int32, [c_void_p]),
     ("fks_get_phase_cycles", c_int32, [c_void_p, c_int32, POINTER(c_uint64)]),
     ("fks_env_build", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), POINTER(c_void_p)]),
+    ("fks_env_build_gpu", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), c_int32,
+                                    POINTER(c_void_p), POINTER(EnvBuildStats)]),
     ("fks_env_view", c_int32, [c_void_p, POINTER(Environment)]),
+    ("fks_env_occupancy", c_int32, [c_void_p, POINTER(c_uint8), c_uint64]),
     ("fks_env_free", None, [c_void_p]),
     ("fks_selftest_math", c_int32, [c_int32, c_uint64, POINTER(c_uint64)]),
 ]

@@ -10,8 +10,9 @@
  *                                             opposite cell centre; +inf out of bounds)
  *   BuildSurfaceNormalsGrid   SEB.cpp:258-468 (SDF-gradient pass for d<0 cells, then the exact
  *                                             cuboid face/edge/corner normals, last write wins)
- * This is the input side of the hot path ("next" row f2 in SURVEY.md §8f); the
- * GPU build of it is future work.  Output layout is the fks_environment CSR.
+ * This is the input side of the hot path ("next" row f2 in SURVEY.md §8f);
+ * fks_env_gpu.hip builds the same bytes on the GPU (fks_env_build_gpu).  Output
+ * layout is the fks_environment CSR.
  */
 #include <stdint.h>
 
@@ -23,49 +24,15 @@
 #include <vector>
 
 #include "fks_capi.h"
+#include "fks_env_internal.h"
 #include "fks_portable_math.h"
 
 namespace {
 
-struct Mat34 {
-    double m[12];
-};
-
-inline double dot3(double a0, double a1, double a2, double b0, double b1, double b2) {
-    return (a0 * b0 + a1 * b1) + a2 * b2;
-}
-
-/* Isometry3d * Vector3d */
-inline void xform3(const double* T, const double p[3], double out[3]) {
-    for (int i = 0; i < 3; ++i) out[i] = dot3(T[4 * i + 0], T[4 * i + 1], T[4 * i + 2], p[0], p[1], p[2]) + T[4 * i + 3];
-}
-inline void rotate3(const double* T, const double v[3], double out[3]) {
-    for (int i = 0; i < 3; ++i) out[i] = dot3(T[4 * i + 0], T[4 * i + 1], T[4 * i + 2], v[0], v[1], v[2]);
-}
-inline void inverse34(const double* T, double* I) {
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) I[4 * i + j] = T[4 * j + i];
-    for (int i = 0; i < 3; ++i) I[4 * i + 3] = -dot3(I[4 * i + 0], I[4 * i + 1], I[4 * i + 2], T[3], T[7], T[11]);
-}
-
-struct Grid {
-    double origin[12], inv_origin[12];
-    double res, inv_res;
-    int64_t n[3];
-    bool index(const double p[3], int64_t idx[3]) const {
-        double g[3];
-        xform3(inv_origin, p, g);
-        for (int a = 0; a < 3; ++a) {
-            const double q = g[a] * inv_res;
-            if (!(q > -9.0e18 && q < 9.0e18)) return false;
-            idx[a] = (int64_t)q;
-            if (idx[a] < 0 || idx[a] >= n[a]) return false;
-        }
-        return true;
-    }
-    size_t linear(int64_t i, int64_t j, int64_t k) const { return ((size_t)i * (size_t)n[1] + (size_t)j) * (size_t)n[2] + (size_t)k; }
-    size_t cells() const { return (size_t)n[0] * (size_t)n[1] * (size_t)n[2]; }
-};
+using fks_env::Grid;
+using fks_env::inverse34;
+using fks_env::rotate3;
+using fks_env::xform3;
 
 /* 1-D squared distance transform (lower envelope of parabolas rooted at the
  * finite samples), exact on integer grids */
@@ -146,14 +113,6 @@ struct Entry {
 
 }  // namespace
 
-struct fks_env_handle {
-    fks_grid_geometry geometry;
-    std::vector<float> sdf;
-    std::vector<uint32_t> offsets;
-    std::vector<double> entries;
-    std::vector<uint8_t> occupancy;
-};
-
 extern "C" fks_status fks_env_build(const fks_obstacle* obstacles, int32_t num_obstacles, double resolution,
                                     const double* grid_origin, const int64_t* num_cells, fks_env_handle** out) {
     if (!out || !(resolution > 0.0) || num_obstacles < 0 || (num_obstacles > 0 && !obstacles)) return FKS_ERR_INVALID_ARGUMENT;
@@ -196,22 +155,7 @@ extern "C" fks_status fks_env_build(const fks_obstacle* obstacles, int32_t num_o
         std::memcpy(grid.origin, grid_origin, sizeof(grid.origin));
         for (int a = 0; a < 3; ++a) grid.n[a] = num_cells[a];
     } else {
-        /* SEB.cpp:128-149: minimum point keyed half a cell out, plus a 3-cell border */
-        if (!init) {
-            for (int a = 0; a < 3; ++a) {
-                mn[a] = 0.0;
-                mx[a] = 10.0;
-            }
-        } else {
-            for (int a = 0; a < 3; ++a) {
-                mn[a] -= resolution * 0.5;
-                mn[a] -= resolution * 3.0;
-                mx[a] += resolution * 3.0;
-            }
-        }
-        const double I[12] = {1, 0, 0, mn[0], 0, 1, 0, mn[1], 0, 0, 1, mn[2]};
-        std::memcpy(grid.origin, I, sizeof(I));
-        for (int a = 0; a < 3; ++a) grid.n[a] = (int64_t)std::ceil((mx[a] - mn[a]) / resolution);
+        fks_env::auto_bounds(init, mn, mx, resolution, grid);
     }
     for (int a = 0; a < 3; ++a)
         if (grid.n[a] < 2 || grid.n[a] > 4096) return FKS_ERR_INVALID_ARGUMENT;
@@ -301,20 +245,8 @@ extern "C" fks_status fks_env_build(const fks_obstacle* obstacles, int32_t num_o
                         count += it->second.size();
                     } else if (env->sdf[c] < 0.0f) {
                         /* pass 1 (SEB.cpp:263-277): SDF gradient (edge gradients enabled), entry 0 */
-                        const int64_t id3[3] = {i, j, k};
-                        double g[3];
-                        for (int a = 0; a < 3; ++a) {
-                            int64_t lo[3] = {i, j, k}, hi[3] = {i, j, k};
-                            lo[a] = (id3[a] - 1 > 0) ? id3[a] - 1 : 0;
-                            hi[a] = (id3[a] + 1 < grid.n[a] - 1) ? id3[a] + 1 : grid.n[a] - 1;
-                            const double inv = 1.0 / (resolution * (double)(hi[a] - lo[a]));
-                            const float diff = sdf_at(hi[0], hi[1], hi[2]) - sdf_at(lo[0], lo[1], lo[2]);
-                            g[a] = (double)diff * inv;
-                        }
-                        const double gn = fks_math::dsqrt((g[0] * g[0] + g[1] * g[1]) + g[2] * g[2]);
                         Entry E;
-                        for (int b = 0; b < 3; ++b) E.e[b] = 0.0;
-                        for (int b = 0; b < 3; ++b) E.e[3 + b] = (gn > 2.220446049250313e-16) ? g[b] / gn : g[b];
+                        fks_env::gradient_entry(grid, i, j, k, sdf_at, E.e);
                         env->entries.insert(env->entries.end(), E.e, E.e + 6);
                         count += 1;
                     }
@@ -342,6 +274,12 @@ extern "C" fks_status fks_env_view(const fks_env_handle* env, fks_environment* o
     out->sdf_oob_value = std::numeric_limits<float>::infinity();
     out->normal_offsets = env->offsets.data();
     out->normal_entries = env->entries.data();
+    return FKS_OK;
+}
+
+extern "C" fks_status fks_env_occupancy(const fks_env_handle* env, uint8_t* out, uint64_t num_cells) {
+    if (!env || (num_cells > 0 && !out) || num_cells != (uint64_t)env->occupancy.size()) return FKS_ERR_INVALID_ARGUMENT;
+    if (num_cells) std::memcpy(out, env->occupancy.data(), (size_t)num_cells);
     return FKS_OK;
 }
 

@@ -83,9 +83,12 @@ class SimulatorEnvironment:
 
 
 def build_complete_environment(obstacles: Sequence[ObstacleConfig], resolution: float, origin=None,
-                               num_cells=None) -> SimulatorEnvironment:
+                               num_cells=None, device: Optional[int] = None, stats: Optional[dict] = None) -> SimulatorEnvironment:
     """BuildCompleteEnvironment(obstacles, resolution) (SEB.cpp:470-476).  With
-    `origin` (3x4) and `num_cells` the grid is that fixed box (e.g. 256^3)."""
+    `origin` (3x4) and `num_cells` the grid is that fixed box (e.g. 256^3).
+    device=None builds on the host (fks_env_build); device=g builds on HIP device g
+    (fks_env_build_gpu, the same bytes).  `stats`, if given, receives the GPU
+    build's sizes and timings."""
     L = _capi.lib()
     arr = (_capi.Obstacle * max(1, len(obstacles)))()
     for i, ob in enumerate(obstacles):
@@ -100,8 +103,16 @@ def build_complete_environment(obstacles: Sequence[ObstacleConfig], resolution: 
         n_arr = np.ascontiguousarray(np.asarray(num_cells, dtype=np.int64))
         o_ptr = _capi.as_ptr(o_arr, ctypes.c_double)
         n_ptr = _capi.as_ptr(n_arr, ctypes.c_int64)
-    st = L.fks_env_build(arr, len(obstacles), float(resolution), o_ptr, n_ptr, ctypes.byref(handle))
-    _capi.check(st, None, "fks_env_build")
+    if device is None:
+        st = L.fks_env_build(arr, len(obstacles), float(resolution), o_ptr, n_ptr, ctypes.byref(handle))
+        _capi.check(st, None, "fks_env_build")
+    else:
+        bs = _capi.EnvBuildStats()
+        st = L.fks_env_build_gpu(arr, len(obstacles), float(resolution), o_ptr, n_ptr, int(device), ctypes.byref(handle),
+                                 ctypes.byref(bs))
+        _capi.check(st, None, "fks_env_build_gpu")
+        if stats is not None:
+            stats.update(bs.as_dict())
     try:
         view = _capi.Environment()
         _capi.check(L.fks_env_view(handle, ctypes.byref(view)), None, "fks_env_view")
@@ -112,6 +123,15 @@ def build_complete_environment(obstacles: Sequence[ObstacleConfig], resolution: 
         nent = int(offsets[-1])
         entries = np.ctypeslib.as_array(view.normal_entries, shape=(6 * nent,)).copy() if nent else np.zeros(0)
         oob = float(view.sdf_oob_value)
+        occupancy = _env_occupancy(handle, ncells)
     finally:
         L.fks_env_free(handle)
-    return SimulatorEnvironment(geom, sdf, offsets, entries, oob)
+    return SimulatorEnvironment(geom, sdf, offsets, entries, oob, occupancy)
+
+
+def _env_occupancy(handle, ncells):
+    """The collision grid of a built environment (fks_env_occupancy)."""
+    L = _capi.lib()
+    out = np.zeros(ncells, dtype=np.uint8)
+    _capi.check(L.fks_env_occupancy(handle, _capi.as_ptr(out, ctypes.c_uint8), ncells), None, "fks_env_occupancy")
+    return out

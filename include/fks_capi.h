@@ -367,8 +367,25 @@ typedef struct fks_env_handle fks_env_handle;
 fks_status fks_env_build(const fks_obstacle* obstacles, int32_t num_obstacles,
                          double resolution, const double* grid_origin,
                          const int64_t* num_cells, fks_env_handle** out);
+/* The same environment built on the GPU (obstacle rasterisation, exact squared EDT,
+ * surface-normal CSR: fks_env_gpu.hip); bit-identical to fks_env_build.  The result
+ * is copied back into a host handle (fks_env_view / fks_env_free as above).
+ * stats (optional): sizes and the device time of the build. */
+typedef struct {
+    uint64_t cells;
+    uint64_t obstacle_samples;
+    uint64_t normal_entries;
+    double gpu_ms;   /* device time: rasterise + EDT + SDF + CSR (HIP events) */
+    double total_ms; /* host wall time of the call incl. allocation and copy-back */
+} fks_env_build_stats;
+fks_status fks_env_build_gpu(const fks_obstacle* obstacles, int32_t num_obstacles,
+                             double resolution, const double* grid_origin,
+                             const int64_t* num_cells, int32_t device, fks_env_handle** out,
+                             fks_env_build_stats* stats);
 /* Fill a view whose pointers stay valid until fks_env_free. */
 fks_status fks_env_view(const fks_env_handle* env, fks_environment* out);
+/* The collision grid (1 = filled cell), z-fastest, num_cells = nx * ny * nz. */
+fks_status fks_env_occupancy(const fks_env_handle* env, uint8_t* out, uint64_t num_cells);
 void fks_env_free(fks_env_handle* env);
 
 /* Device self-test of the portable libm against the host (bit equality). */
