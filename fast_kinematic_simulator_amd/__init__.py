@@ -6,8 +6,8 @@ as hand-written HIP kernels for gfx950 behind the C-ABI in include/fks_capi.h.
 """
 from ._capi import FksError, lib
 from .environment import ObstacleConfig, SimulatorEnvironment, build_complete_environment
-from .robots import (ControllerConfig, Joint, RobotDescription, make_linked_robot, make_se2_robot, make_se3_robot, se3_pose,
-                     transform34)
+from .robots import (ControllerConfig, Joint, RobotDescription, SampledActuatorModel, make_linked_robot,
+                     make_sampled_actuator_model, make_se2_robot, make_se3_robot, se3_pose, transform34)
 from .simulator import (HipParticleContactSimulator, SimulationResult, SimulatorSolverParameters, get_default_solver_parameters,
                         make_linked_simulator, make_se2_simulator, make_se3_simulator)
 

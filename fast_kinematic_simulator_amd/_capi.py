@@ -103,6 +103,16 @@ class JointDesc(ctypes.Structure):
     ]
 
 
+class SampledActuator(ctypes.Structure):
+    """fks_sampled_actuator: SampledUncertainVelocityActuator bins (UNC:123-281)."""
+    _fields_ = [
+        ("num_bins", c_uint32),
+        ("bin_elements", c_uint32),
+        ("bin_bounds", POINTER(c_double)),
+        ("bin_samples", POINTER(c_double)),
+    ]
+
+
 class RobotDesc(ctypes.Structure):
     _fields_ = [
         ("robot_type", c_int32),
@@ -119,6 +129,7 @@ class RobotDesc(ctypes.Structure):
         ("allowed_pairs", POINTER(c_int32)),
         ("controllers", POINTER(DofController)),
         ("distance_weights", POINTER(c_double)),
+        ("sampled_actuators", POINTER(SampledActuator)),
     ]
 
 

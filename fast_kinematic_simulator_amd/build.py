@@ -69,7 +69,9 @@ def build_example(force: bool = False) -> str:
     os.makedirs(out_dir, exist_ok=True)
     target = os.path.join(out_dir, "cpp_forward_simulate")
     hdr = os.path.join(ROOT, "include", "fast_kinematic_simulator_amd", "hip_particle_contact_simulator.hpp")
-    if not force and os.path.exists(target) and all(os.path.getmtime(target) >= os.path.getmtime(p) for p in (src, hdr, lib)):
+    capi = os.path.join(ROOT, "include", "fks_capi.h")
+    if not force and os.path.exists(target) and all(os.path.getmtime(target) >= os.path.getmtime(p)
+                                                    for p in (src, hdr, capi, lib)):
         return target
     cmd = ["g++", "-std=c++17", "-O2", "-Wall", f"-I{os.path.join(ROOT, 'include')}", src, "-o", target, f"-L{PKG}",
            "-lfks_hip", "-Wl,-rpath,$ORIGIN/../fast_kinematic_simulator_amd", "-Wl,-rpath-link,/opt/rocm/lib"]

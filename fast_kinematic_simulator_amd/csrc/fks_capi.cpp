@@ -593,6 +593,20 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
         weights.push_back(d->distance_weights ? d->distance_weights[0] : 1.0);
         weights.push_back(d->distance_weights ? d->distance_weights[1] : 1.0);
     }
+    /* SampledUncertainVelocityActuator tables (UNC:123-281), validated before the old robot goes */
+    if (d->sampled_actuators) {
+        for (int k = 0; k < R.D; ++k) {
+            const fks_sampled_actuator& a = d->sampled_actuators[k];
+            if (a.num_bins == 0) continue;
+            if (a.bin_elements == 0 || !a.bin_bounds || !a.bin_samples)
+                return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "sampled actuator needs bounds and >= 1 sample per bin");
+            for (uint64_t i = 0; i < 2ull * a.num_bins; ++i)
+                if (std::isnan(a.bin_bounds[i])) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "NaN sampled-actuator bin bound");
+            for (uint64_t i = 0; i < (uint64_t)a.num_bins * a.bin_elements; ++i)
+                if (!std::isfinite(a.bin_samples[i]))
+                    return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "non-finite sampled-actuator sample");
+        }
+    }
     free_robot(ctx);
     auto up = [&](auto** dptr, const auto* host, size_t count) -> hipError_t {
         hipError_t e = dev_upload(dptr, host, count);
@@ -640,6 +654,27 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     R.weights = dw;
     R.rounds = drounds;
     R.dof_lever = dlever;
+    R.sampled_mask = 0;
+    R.sampled = nullptr;
+    if (d->sampled_actuators) {
+        std::vector<fksd::SampledDev> sd((size_t)R.D);
+        for (int k = 0; k < R.D; ++k) {
+            const fks_sampled_actuator& a = d->sampled_actuators[k];
+            std::memset(&sd[k], 0, sizeof(sd[k]));
+            if (a.num_bins == 0) continue;
+            double *dbounds = nullptr, *dsamples = nullptr;
+            HIP_TRY(ctx, up(&dbounds, a.bin_bounds, 2 * (size_t)a.num_bins));
+            HIP_TRY(ctx, up(&dsamples, a.bin_samples, (size_t)a.num_bins * a.bin_elements));
+            sd[k].nbins = a.num_bins;
+            sd[k].elems = a.bin_elements;
+            sd[k].bounds = dbounds;
+            sd[k].samples = dsamples;
+            R.sampled_mask |= 1ull << k;
+        }
+        fksd::SampledDev* dsd = nullptr;
+        HIP_TRY(ctx, up(&dsd, sd.data(), sd.size()));
+        R.sampled = dsd;
+    }
     /* launch geometry: one wave per workgroup, as many resident waves as fit */
     const fksd::LdsLayout L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds);
     ctx->lds_bytes = ((size_t)L.shared_total + (size_t)fksd::kWavesPerGroup * L.total) * sizeof(double);

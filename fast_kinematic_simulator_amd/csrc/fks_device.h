@@ -58,6 +58,13 @@ struct RoundDev {
 constexpr int kRoundState = 16;
 constexpr int kLdsPairs = 128; /* disallowed geometry pairs cached in LDS (the rest are read from HBM) */
 
+/* one dof's SampledUncertainVelocityActuator tables (fks_sampled_actuator) */
+struct SampledDev {
+    uint32_t nbins, elems;
+    const double* bounds;  /* 2 per bin */
+    const double* samples; /* elems per bin */
+};
+
 struct RobotDev {
     int32_t type, L, J, G, D, P, W, npairs;
     int32_t self_possible;
@@ -83,6 +90,9 @@ struct RobotDev {
      * unknown.  Lets the microstep-motion check of SPCS:1570-1575 be proven instead
      * of recomputed. */
     const double* dof_lever;
+    /* dofs whose actuator is a SampledUncertainVelocityActuator (bit d), their tables */
+    uint64_t sampled_mask;
+    const SampledDev* sampled;
 };
 
 /* LDS carve-out (in doubles), identical on host and device.  A workgroup holds

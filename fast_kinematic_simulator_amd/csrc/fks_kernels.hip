@@ -324,6 +324,18 @@ __device__ double tn_sample(uint32_t k0, uint32_t k1, uint64_t particle, uint32_
     return 0.0;
 }
 
+/* SampledUncertainVelocityActuator pick (UNC:236-237): uniform index into a bin of
+ * `elems` samples from the first Philox block of the (particle, step, micro, dof)
+ * counter; which bin it indexes depends on the clamped command (apply_input). */
+__device__ double sampled_pick(uint32_t k0, uint32_t k1, uint64_t particle, uint32_t step, uint32_t micro, uint32_t dof,
+                               uint32_t elems) {
+    uint32_t c[4] = {(uint32_t)particle, step, micro, ((uint32_t)(particle >> 32) << 16) | ((dof & 0xffu) << 8)};
+    philox4x32_10(c, k0, k1);
+    uint32_t pick = (uint32_t)(u53(c[0], c[1]) * (double)elems);
+    if (pick >= elems) pick = elems - 1u;
+    return (double)pick;
+}
+
 /* Actuator noise does not depend on the particle state, so the samples of the next
  * floor(64 / D) microsteps are drawn at once, one lane per (microstep, dof), into LDS;
  * noise_sample() consumes them (and their error bits) in the DOF lanes. */
@@ -447,7 +459,11 @@ __device__ __noinline__ void refill_noise_lanes(const SimArgs* __restrict__ Ap, 
         const uint32_t m = micro0 + (uint32_t)(ln / D);
         if (m < M) {
             uint32_t e = 0;
-            nz[ln] = tn_sample(A.key0, A.key1, pid, step, m, (uint32_t)(ln % D), &e);
+            const uint32_t dof = (uint32_t)(ln % D);
+            if ((A.R.sampled_mask >> dof) & 1ull)
+                nz[ln] = sampled_pick(A.key0, A.key1, pid, step, m, dof, A.R.sampled[dof].elems);
+            else
+                nz[ln] = tn_sample(A.key0, A.key1, pid, step, m, dof, &e);
             ne[ln] = e;
         }
     }
@@ -633,6 +649,27 @@ __device__ void fk(Sim& s, const double* cfg, double* T) {
     }
 }
 
+/* noisy actuator of dof `dof` on its clamped command `real` (TNUVA:568-596):
+ * TruncatedNormalUncertainVelocityActuator (UNC:77-90), or the sampled one
+ * (UNC:270-279: first matching bin, then the picked sample) */
+__device__ __forceinline__ double actuator_noisy(Sim& s, const fks_dof_controller& ct, int dof, double real, uint32_t micro) {
+    const double ns = noise_sample(s, micro);
+    const RobotDev& R = s.A->R;
+    if ((R.sampled_mask >> dof) & 1ull) {
+        const SampledDev sd = R.sampled[dof];
+        for (uint32_t b = 0; b < sd.nbins; ++b)
+            if (real >= sd.bounds[2 * b] && real <= sd.bounds[2 * b + 1])
+                return real + sd.samples[(uint64_t)b * sd.elems + (uint32_t)ns];
+        s.err |= FKS_PARTICLE_ERR_NO_NOISE_BIN;
+        return real + 0.0;
+    }
+    const double vmax = dabs(ct.velocity_limit);
+    const double prop = dabs(ct.max_actuator_proportional_noise) * dabs(real);
+    const double floor_noise = dabs(ct.max_actuator_minimum_noise) * vmax;
+    const double bound = dmax(prop, floor_noise);
+    return real + ns * bound;
+}
+
 /* ---------------- robot control-input application (TNUVA ApplyControlInput) ----------------
  * cfg_out = apply(cfg_in, input) with clamp (+ noise if noisy).  Lane d < D owns dof d. */
 template <int RT>
@@ -645,12 +682,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
             const fks_dof_controller& ct = s.ctrl[ln];
             const double vmax = dabs(ct.velocity_limit);
             double real = clamp(input[ln], -vmax, vmax);
-            if (noisy) {
-                const double prop = dabs(ct.max_actuator_proportional_noise) * dabs(real);
-                const double floor_noise = dabs(ct.max_actuator_minimum_noise) * vmax;
-                const double bound = dmax(prop, floor_noise);
-                real = real + noise_sample(s, micro) * bound;
-            }
+            if (noisy) real = actuator_noisy(s, ct, ln, real, micro);
             const JointDev& jd = s.joints[s.dofj[ln]];
             const double raw = cfg_in[ln] + real;
             double v;
@@ -669,12 +701,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
             const fks_dof_controller& ct = s.ctrl[ln];
             const double vmax = dabs(ct.velocity_limit);
             double real = clamp(input[ln], -vmax, vmax);
-            if (noisy) {
-                const double prop = dabs(ct.max_actuator_proportional_noise) * dabs(real);
-                const double floor_noise = dabs(ct.max_actuator_minimum_noise) * vmax;
-                const double bound = dmax(prop, floor_noise);
-                real = real + noise_sample(s, micro) * bound;
-            }
+            if (noisy) real = actuator_noisy(s, ct, ln, real, micro);
             double v = cfg_in[ln] + real;
             if (ln == 2) v = fks_math::enforce_continuous_revolute_bounds(v);
             cfg_out[ln] = v;
@@ -686,12 +713,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
             const fks_dof_controller& ct = s.ctrl[ln];
             const double vmax = dabs(ct.velocity_limit);
             double real = clamp(input[ln], -vmax, vmax);
-            if (noisy) {
-                const double prop = dabs(ct.max_actuator_proportional_noise) * dabs(real);
-                const double floor_noise = dabs(ct.max_actuator_minimum_noise) * vmax;
-                const double bound = dmax(prop, floor_noise);
-                real = real + noise_sample(s, micro) * bound;
-            }
+            if (noisy) real = actuator_noisy(s, ct, ln, real, micro);
             tw[ln] = real;
         }
         wsync();

@@ -45,6 +45,58 @@ class ControllerConfig:
 
 
 @dataclass
+class SampledActuatorModel:
+    """JointUncertaintySampleModel (UNC:123) for a SampledUncertainVelocityActuator:
+    bins[k] = (lower, upper) of commanded velocity with `samples[k]` velocity errors
+    (every bin the same number of samples, as DownsampleBin makes them, UNC:125-138)."""
+
+    bounds: np.ndarray   # (num_bins, 2)
+    samples: np.ndarray  # (num_bins, bin_elements)
+
+    def to_c(self):
+        b = np.ascontiguousarray(self.bounds, dtype=np.float64).reshape(-1, 2)
+        smp = np.ascontiguousarray(self.samples, dtype=np.float64).reshape(b.shape[0], -1)
+        return _capi.SampledActuator(b.shape[0], smp.shape[1], _capi.as_ptr(b, ctypes.c_double),
+                                     _capi.as_ptr(smp, ctypes.c_double)), [b, smp]
+
+
+def make_sampled_actuator_model(data, actuator_limit: float, num_bins: int, bin_elements: int,
+                                seed: int = 0) -> SampledActuatorModel:
+    """LoadModel (UNC:156-221) on (commanded velocity, velocity error) pairs -- a CSV
+    path or an (n, 2) array.  Bins split [-limit, limit] into num_bins equal steps, the
+    outer two open to -inf / +inf; each pair goes to the first bin holding its command
+    (GetMatchingBin, UNC:140-154); each bin is resampled with replacement to
+    bin_elements entries (DownsampleBin, UNC:125-138: the reference seeds from
+    std::random_device, here from `seed`)."""
+    if isinstance(data, str):
+        data = np.loadtxt(data, delimiter=",", dtype=np.float64, ndmin=2)
+    data = np.asarray(data, dtype=np.float64).reshape(-1, 2)
+    bin_size = (actuator_limit * 2.0) / float(num_bins)
+    bounds = []
+    previous_bin_upper = -actuator_limit
+    for idx in range(num_bins):
+        lower = -np.inf if idx == 0 else previous_bin_upper
+        upper = np.inf if idx >= num_bins - 1 else previous_bin_upper + bin_size
+        previous_bin_upper = upper
+        bounds.append((lower, upper))
+    contents = [[] for _ in range(num_bins)]
+    for commanded, error in data:
+        for k, (lo, hi) in enumerate(bounds):
+            if lo <= commanded <= hi:
+                contents[k].append(error)
+                break
+        else:
+            raise ValueError(f"Value {commanded} is not in any bin")
+    rng = np.random.default_rng(seed)
+    samples = np.zeros((num_bins, bin_elements))
+    for k, items in enumerate(contents):
+        if not items:
+            raise ValueError(f"bin {k} has no data to downsample")
+        samples[k] = np.asarray(items)[rng.integers(0, len(items), size=bin_elements)]
+    return SampledActuatorModel(np.array(bounds, dtype=np.float64), samples)
+
+
+@dataclass
 class Joint:
     """simple_linked_robot_model::RobotJoint: parent/child link, fixed origin
     (parent link frame -> joint frame, 3x4 row-major), axis, type, limits."""
@@ -86,6 +138,8 @@ class RobotDescription:
     distance_weights: List[float]
     base_transform: np.ndarray = field(default_factory=lambda: IDENTITY34.copy())
     name: str = "robot"
+    # per dof: None (truncated-normal actuator) or a SampledUncertainVelocityActuator model
+    sampled_actuators: Optional[List[Optional[SampledActuatorModel]]] = None
 
     @property
     def num_dofs(self) -> int:
@@ -154,6 +208,16 @@ class RobotDescription:
         desc.allowed_pairs = _capi.as_ptr(pairs, ctypes.c_int32) if len(pairs) else None
         desc.controllers = ctypes.cast(ctrl, ctypes.POINTER(_capi.DofController))
         desc.distance_weights = _capi.as_ptr(weights, ctypes.c_double)
+        if self.sampled_actuators is not None:
+            if len(self.sampled_actuators) != self.num_dofs:
+                raise ValueError("sampled_actuators needs one entry (model or None) per dof")
+            sarr = (_capi.SampledActuator * self.num_dofs)()
+            for k, m in enumerate(self.sampled_actuators):
+                if m is not None:
+                    sarr[k], k_keep = m.to_c()
+                    keep += k_keep
+            keep.append(sarr)
+            desc.sampled_actuators = ctypes.cast(sarr, ctypes.POINTER(_capi.SampledActuator))
         return desc, keep
 
 

@@ -102,6 +102,9 @@ class RobotDescription {
     std::vector<int32_t> allowed_pairs; /* geometry index pairs */
     std::vector<fks_dof_controller> controllers;
     std::vector<double> distance_weights;
+    /* empty, or one per dof: SampledUncertainVelocityActuator bins (num_bins 0 = truncated
+     * normal); the bound/sample arrays they point to must outlive the simulator calls */
+    std::vector<fks_sampled_actuator> sampled_actuators;
 
     /* geometry `g` of link `link`: points as (x, y, z, w) quadruples */
     int32_t AddGeometry(int32_t link, const std::vector<double>& xyzw) {
@@ -120,7 +123,7 @@ class RobotDescription {
         return type == FKS_ROBOT_SE2 ? 3 : (type == FKS_ROBOT_SE3 ? 12 : num_dofs);
     }
     fks_robot_desc View() const {
-        fks_robot_desc d;
+        fks_robot_desc d{};
         d.robot_type = type;
         d.num_links = num_links;
         d.num_joints = (int32_t)joints.size();
@@ -135,6 +138,7 @@ class RobotDescription {
         d.allowed_pairs = allowed_pairs.empty() ? nullptr : allowed_pairs.data();
         d.controllers = controllers.data();
         d.distance_weights = distance_weights.empty() ? nullptr : distance_weights.data();
+        d.sampled_actuators = sampled_actuators.empty() ? nullptr : sampled_actuators.data();
         return d;
     }
 };

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define FKS_ABI_VERSION 1
+#define FKS_ABI_VERSION 2
 
 typedef enum {
     FKS_OK = 0,
@@ -75,6 +75,7 @@ typedef enum {
 #define FKS_PARTICLE_ERR_KEY_RANGE 0x20u         /* non-finite point in the self-collision grid          */
 #define FKS_PARTICLE_ERR_MICROSTEP_CAP 0x40u     /* microsteps per controller step exceeded 2^20         */
 #define FKS_PARTICLE_ERR_SELF_SINGULAR 0x80u     /* NaN self-collision correction (assert SPCS:1151-1153) */
+#define FKS_PARTICLE_ERR_NO_NOISE_BIN 0x100u     /* sampled actuator: no bin holds the command (UNC:152-153) */
 
 /* capacities of the self-collision impulse solve (both the HIP path and the oracle
  * flag FKS_PARTICLE_ERR_SELF_CAPACITY beyond them) */
@@ -137,6 +138,19 @@ typedef struct {
     double max_actuator_minimum_noise;
 } fks_dof_controller;
 
+/* SampledUncertainVelocityActuator (UNC:123-281): bins of observed velocity errors
+ * keyed by commanded velocity (JointUncertaintySampleModel, UNC:123).  Bin k covers
+ * [bin_bounds[2k], bin_bounds[2k+1]]; the first bin holding the clamped command
+ * wins (GetMatchingBin, UNC:140-154) and one of its bin_elements samples, picked
+ * uniformly, is added to it (GetNoiseValue, UNC:228-243).  num_bins == 0 keeps the
+ * truncated-normal actuator of fks_dof_controller for that dof. */
+typedef struct {
+    uint32_t num_bins;
+    uint32_t bin_elements;
+    const double* bin_bounds;  /* num_bins x (lower, upper) */
+    const double* bin_samples; /* num_bins x bin_elements */
+} fks_sampled_actuator;
+
 /* simple_linked_robot_model::RobotJoint */
 typedef struct {
     int32_t parent_link;
@@ -175,6 +189,8 @@ typedef struct {
     const int32_t* allowed_pairs;
     const fks_dof_controller* controllers;
     const double* distance_weights;
+    /* NULL, or num_dofs entries: per-dof SampledUncertainVelocityActuator (ABI 2) */
+    const fks_sampled_actuator* sampled_actuators;
 } fks_robot_desc;
 
 /* SimpleParticleContactSimulator statistics counters (SPCS:392-400, 488-500) */

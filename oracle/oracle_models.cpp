@@ -49,7 +49,8 @@ LinkedRobot::LinkedRobot(const fks_robot_desc& d) {
         allowed_self_collisions_.insert(
             std::make_pair((size_t)d.allowed_pairs[2 * i], (size_t)d.allowed_pairs[2 * i + 1]));
     for (size_t k = 0; k < num_active_joints_; ++k) {
-        joint_controller_groups_.push_back(JointControllerGroup(d.controllers[k]));
+        joint_controller_groups_.push_back(
+            JointControllerGroup(d.controllers[k], d.sampled_actuators ? d.sampled_actuators + k : nullptr));
         joint_distance_weights_.push_back(d.distance_weights ? d.distance_weights[k] : 1.0);
     }
     config_.assign(num_active_joints_, 0.0);
@@ -212,7 +213,8 @@ bool LinkedRobot::CheckIfSelfCollisionAllowed(size_t a, size_t b) const {
 SE2Robot::SE2Robot(const fks_robot_desc& d) {
     std::vector<std::string> names{"link_0"};
     link_geometries_ = make_link_geometries(d, names);
-    for (int i = 0; i < 3; ++i) axis_[i] = JointControllerGroup(d.controllers[i]);
+    for (int i = 0; i < 3; ++i)
+        axis_[i] = JointControllerGroup(d.controllers[i], d.sampled_actuators ? d.sampled_actuators + i : nullptr);
     position_weight_ = d.distance_weights ? d.distance_weights[0] : 1.0;
     rotation_weight_ = d.distance_weights ? d.distance_weights[1] : 1.0;
     config_.assign(3, 0.0);
@@ -292,7 +294,8 @@ const Config& SE2Robot::ResetPosition(const Config& position) {
 SE3Robot::SE3Robot(const fks_robot_desc& d) {
     std::vector<std::string> names{"link_0"};
     link_geometries_ = make_link_geometries(d, names);
-    for (int i = 0; i < 6; ++i) axis_[i] = JointControllerGroup(d.controllers[i]);
+    for (int i = 0; i < 6; ++i)
+        axis_[i] = JointControllerGroup(d.controllers[i], d.sampled_actuators ? d.sampled_actuators + i : nullptr);
     position_weight_ = d.distance_weights ? d.distance_weights[0] : 1.0;
     rotation_weight_ = d.distance_weights ? d.distance_weights[1] : 1.0;
     config_.assign(12, 0.0);

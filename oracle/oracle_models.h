@@ -4,6 +4,7 @@
  * Restatement of the reference's robot, controller and noise models:
  *   simple_pid_controller::SimplePIDController        PID:53-136
  *   TruncatedNormalUncertainVelocityActuator           UNC:48-121
+ *   SampledUncertainVelocityActuator, GetMatchingBin   UNC:123-281
  *   arc_helpers::TruncatedNormalDistribution           (absent dependency; TYPE_1
  *       naive accept-reject restated, the only case the actuator reaches: bounds
  *       [-1,1] at sigma 0.5 -> standardized [-2,2], UNC:61, TNUVA:469)
@@ -167,13 +168,114 @@ class TruncatedNormalUncertainVelocityActuator {
     double velocity_limit_, acceleration_limit_, proportional_noise_bound_, minimum_noise_bound_;
 };
 
+/* ---------------- sampled actuator (UNC:123-281) ---------------- */
+/* JointUncertaintySampleModel (UNC:123): ((lower, upper), velocity errors) per bin */
+typedef std::vector<std::pair<std::pair<double, double>, std::vector<double>>> JointUncertaintySampleModel;
+
+/* GetMatchingBin (UNC:140-154): first bin whose closed interval holds the value;
+ * the reference asserts when none does (here: error flag, returns false) */
+inline bool GetMatchingBin(const JointUncertaintySampleModel& bins, double commanded_velocity, size_t* idx) {
+    for (size_t i = 0; i < bins.size(); ++i) {
+        const std::pair<double, double>& bin_bounds = bins[i].first;
+        if (commanded_velocity >= bin_bounds.first && commanded_velocity <= bin_bounds.second) {
+            *idx = i;
+            return true;
+        }
+    }
+    return false;
+}
+
+/* counter-mode uniform_int_distribution(0, size - 1): first Philox block of the
+ * (particle, step, micro, dof) counter, as the HIP kernel's sampled_pick */
+inline size_t counter_pick(const NoiseContext& ctx, uint32_t dof, size_t size) {
+    Philox4 c;
+    c.v[0] = (uint32_t)ctx.particle;
+    c.v[1] = ctx.step;
+    c.v[2] = ctx.micro;
+    c.v[3] = ((uint32_t)(ctx.particle >> 32) << 16) | ((dof & 0xffu) << 8);
+    const Philox4 r = philox4x32_10(c, ctx.key0, ctx.key1);
+    uint32_t pick = (uint32_t)(u53(r.v[0], r.v[1]) * (double)(uint32_t)size);
+    if (pick >= (uint32_t)size) pick = (uint32_t)size - 1u;
+    return (size_t)pick;
+}
+
+class SampledUncertainVelocityActuator {
+  public:
+    SampledUncertainVelocityActuator(std::shared_ptr<const JointUncertaintySampleModel> model_ptr, double max_velocity)
+        : actuator_limit_(fks_math::dabs(max_velocity)), model_ptr_(model_ptr) {}
+    /* UNC:257-264 */
+    double GetControlValue(double control_input) const {
+        double real_control_input = fks_math::dmin(actuator_limit_, control_input);
+        real_control_input = fks_math::dmax(-actuator_limit_, real_control_input);
+        return real_control_input;
+    }
+    /* UNC:266-279 */
+    double GetControlValue(double control_input, NoiseContext& ctx, uint32_t dof) const {
+        const double real_control_input = GetControlValue(control_input);
+        const double noise = GetNoiseValue(real_control_input, ctx, dof);
+        return real_control_input + noise;
+    }
+
+  private:
+    /* UNC:228-243.  The reference takes the RNG BY VALUE, so reference mode draws
+     * from a copy and leaves the thread's generator where it was. */
+    double GetNoiseValue(double commanded_velocity, NoiseContext& ctx, uint32_t dof) const {
+        if (!model_ptr_) return 0.0;
+        size_t bin_idx = 0;
+        if (!GetMatchingBin(*model_ptr_, commanded_velocity, &bin_idx)) {
+            *ctx.error_flags |= FKS_PARTICLE_ERR_NO_NOISE_BIN;
+            return 0.0;
+        }
+        const std::vector<double>& best_match_bin = (*model_ptr_)[bin_idx].second;
+        size_t pick_idx;
+        if (ctx.mode == RNG_COUNTER) {
+            pick_idx = counter_pick(ctx, dof, best_match_bin.size());
+        } else {
+            std::mt19937_64 rng = *ctx.mt;
+            std::uniform_int_distribution<size_t> pick_dist(0, best_match_bin.size() - 1);
+            pick_idx = pick_dist(rng);
+        }
+        return best_match_bin[pick_idx];
+    }
+    double actuator_limit_;
+    std::shared_ptr<const JointUncertaintySampleModel> model_ptr_;
+};
+
+/* the dof's actuator: truncated-normal (TNUVA:128-130, 318-323, 469) or, when the
+ * robot description carries one, the sampled actuator */
+class ActuatorModel {
+  public:
+    ActuatorModel() {}
+    ActuatorModel(const fks_dof_controller& c, const fks_sampled_actuator* sa)
+        : tn_(c.velocity_limit, c.acceleration_limit, c.max_actuator_proportional_noise, c.max_actuator_minimum_noise, 0.5) {
+        if (sa && sa->num_bins > 0) {
+            std::shared_ptr<JointUncertaintySampleModel> m(new JointUncertaintySampleModel());
+            for (uint32_t b = 0; b < sa->num_bins; ++b) {
+                std::vector<double> samples(sa->bin_samples + (size_t)b * sa->bin_elements,
+                                            sa->bin_samples + (size_t)(b + 1) * sa->bin_elements);
+                m->push_back(std::make_pair(std::make_pair(sa->bin_bounds[2 * b], sa->bin_bounds[2 * b + 1]), samples));
+            }
+            sampled_ = std::make_shared<SampledUncertainVelocityActuator>(m, c.velocity_limit);
+        }
+    }
+    double GetControlValue(double control_input) const {
+        return sampled_ ? sampled_->GetControlValue(control_input) : tn_.GetControlValue(control_input);
+    }
+    double GetControlValue(double control_input, NoiseContext& ctx, uint32_t dof) {
+        return sampled_ ? sampled_->GetControlValue(control_input, ctx, dof) : tn_.GetControlValue(control_input, ctx, dof);
+    }
+
+  private:
+    TruncatedNormalUncertainVelocityActuator tn_;
+    std::shared_ptr<const SampledUncertainVelocityActuator> sampled_;
+};
+
 struct JointControllerGroup {
     SimplePIDController controller;
-    TruncatedNormalUncertainVelocityActuator actuator;
+    ActuatorModel actuator;
     JointControllerGroup() {}
-    explicit JointControllerGroup(const fks_dof_controller& c)
-        : controller(c.kp, c.ki, c.kd, c.integral_clamp),
-          actuator(c.velocity_limit, c.acceleration_limit, c.max_actuator_proportional_noise, c.max_actuator_minimum_noise, 0.5) {}
+    JointControllerGroup(const fks_dof_controller& c, const fks_sampled_actuator* sa)
+        : controller(c.kp, c.ki, c.kd, c.integral_clamp), actuator(c, sa) {}
 };
 
 /* PointSphereGeometry with POINTS */
