@@ -2081,7 +2081,7 @@ template <int RT>
 __device__ __forceinline__ void setup_wave(const SimArgs* __restrict__ args, double* lds_mem, Sim& s) {
     const SimArgs& A = *args;
     const RobotDev& R = A.R;
-    const int wave = (int)(threadIdx.x >> 6);
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform: LDS bases stay in SGPRs */
     double* shared = lds_mem;
     {
         const int t = (int)threadIdx.x, nt = (int)blockDim.x;
@@ -2286,7 +2286,7 @@ template <int RT, bool TR>
 __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ args, double* lds_mem) {
     const SimArgs& A = *args;
     const RobotDev& R = A.R;
-    const int wave = (int)(threadIdx.x >> 6);
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform: LDS bases stay in SGPRs */
     double* shared = lds_mem;
     {
         /* one copy per workgroup of the robot tables read in the inner loops */
