@@ -31,6 +31,17 @@ METRIC = "particle-microsteps/sec, 7-DOF arm vs 256³ SDF, at 1/2/4/8 MI355X"
 UNIT = "particle-microsteps/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s spec)
 PARTICLES_PER_GPU = 65536
+# the other BASELINE.json configs, runnable with --workload for side measurements
+# (the headline line is cfg3): base particle count of the config, default per GPU, description
+WORKLOADS = {
+    "cfg1": (32, 32, "cfg1: SE(2) 3-DOF planar robot (64 points), 64^3 grid @ 0.0625 m, 50 controller steps"),
+    "cfg2": (4096, 4096, "cfg2: 6-DOF UR5-style arm (7 links x 64 points), 128^3 SDF @ 0.02 m, 100 controller steps"),
+    "cfg3": (65536, 65536, "cfg3: 7-DOF linked arm (8 links x 64 points), 256^3 SDF @ 0.01 m, 200 controller steps"),
+    "cfg4": (1048576, 131072, "cfg4: SE(3) free flyer (256 points), 256^3 SDF @ 0.01 m, 100 controller steps"),
+    "cfg5": (1048576, 131072, "cfg5: dual-arm 14-DOF linked robot (17 links x 64 points), 512^3 SDF @ 0.005 m, "
+                              "200 controller steps"),
+}
+KERNELS = {0: "fks_simulate_linked", 1: "fks_simulate_se2", 2: "fks_simulate_se3"}
 
 
 def log(msg):
@@ -50,8 +61,8 @@ def cpu_baseline(wl, sample_particles: int, threads: int):
     dt = time.perf_counter() - t0
     micro = int(r["counters"]["microsteps"])
     return {"value": micro / dt, "unit": UNIT, "cores": threads, "kind": "port",
-            "sample": f"first {len(starts)} particles of cfg3 x 200 controller steps ({micro} microsteps, {dt:.1f} s), "
-                      f"oracle in reference-RNG mode, OpenMP {threads} threads"}
+            "sample": f"first {len(starts)} particles of {wl.name} x {wl.steps} controller steps ({micro} microsteps, "
+                      f"{dt:.1f} s), oracle in reference-RNG mode, OpenMP {threads} threads"}
 
 
 def config_check_bench(sim, wl, dev, n=1 << 20, reps=3, cpu_sample=16384, threads=16, with_cpu=True):
@@ -112,7 +123,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--particles", type=int, default=PARTICLES_PER_GPU, help="particles per GPU")
+    ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS),
+                    help="BASELINE.json config (the headline metric is cfg3)")
+    ap.add_argument("--particles", type=int, default=0, help="particles per GPU (default: the workload's)")
     ap.add_argument("--cpu-sample", type=int, default=2048, help="particles in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config-check", action="store_true", help="skip the batched CheckConfigCollision line")
@@ -137,14 +150,17 @@ def main():
     from fast_kinematic_simulator_amd._capi import PHASE_COUNTS
     from fast_kinematic_simulator_amd.sharding import gather_outcomes, pack_outcomes, shard_bounds
 
-    n_total = args.particles * world
+    base, per_gpu, workload_desc = WORKLOADS[args.workload]
+    n_total = (args.particles or per_gpu) * world
     lo, hi = shard_bounds(n_total, world, rank)
     n_local = hi - lo
-    wl = W.cfg3(scale=n_total / 65536.0)
+    wl = W.WORKLOADS[args.workload](scale=n_total / float(base))
     t0 = time.perf_counter()
-    env = wl.environment()
-    log(f"[rank {rank}] environment 256^3 built in {time.perf_counter() - t0:.1f}s "
-        f"({int(env.normal_offsets[-1])} surface-normal entries)")
+    env_stats = {}
+    env = W.SCENES[args.workload](device=local_rank, stats=env_stats)  # fks_env_build_gpu (same bytes as the host build)
+    wl._env = env
+    log(f"[rank {rank}] environment {env_stats['cells']} cells built on the GPU in {env_stats['gpu_ms']:.1f} ms device "
+        f"time ({time.perf_counter() - t0:.2f}s call, {int(env.normal_offsets[-1])} surface-normal entries)")
     sim = make_linked_simulator(env, wl.solver, wl.controller_frequency, wl.seed, device=local_rank)
     sim.set_robot(wl.robot)
     Wd = wl.robot.config_width
@@ -214,16 +230,19 @@ def main():
         avg_kernel_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3
         bytes_per_launch = tot["sdf_bytes"] / calls
         achieved = bytes_per_launch / avg_kernel_s / 1e9
-        traffic = load_traffic()
+        traffic = load_traffic() if args.workload == "cfg3" else None  # the PMC summary is of the cfg3 kernel
         cpu = None
         if not args.no_cpu_baseline:
             threads = max(1, min(16, os.cpu_count() or 1))
             t0 = time.perf_counter()
-            cpu = cpu_baseline(W.cfg3(scale=args.cpu_sample / 65536.0), args.cpu_sample, threads)
+            sample = min(args.cpu_sample, n_total)
+            cwl = W.WORKLOADS[args.workload](scale=sample / float(base))
+            cwl._env = env
+            cpu = cpu_baseline(cwl, sample, threads)
             log(f"cpu baseline {cpu['value']:.0f} {UNIT} in {time.perf_counter() - t0:.1f}s")
         value = all_micro / elapsed
         cc = None
-        if not args.no_config_check:
+        if not args.no_config_check and args.workload == "cfg3":
             cc = config_check_bench(sim, wl, dev, with_cpu=not args.no_cpu_baseline)
             log(f"config check {cc['value']:.3e} configs/s")
         line = {
@@ -238,10 +257,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded cfg3 scene: table + 5 pillars, starts = nominal + U(+-0.05 rad))",
+            "data": f"synthetic (seeded {args.workload} scene and start perturbations, workloads.py)",
             "config": {
-                "workload": "cfg3: 7-DOF linked arm (8 links x 64 points), 256^3 SDF @ 0.01 m, 65536 particles x 200 "
-                            "controller steps per GPU, allow_contacts, RCCL gather of outcomes to rank 0",
+                "workload": f"{workload_desc}, {n_local} particles per GPU, allow_contacts, RCCL gather of outcomes "
+                            f"to rank 0",
                 "particles_per_gpu": n_local,
                 "particles_total": n_local * world,
                 "controller_steps": wl.steps,
@@ -259,7 +278,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "fks_simulate_linked",
+                "kernel": KERNELS[wl.robot.robot_type],
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },

@@ -215,6 +215,36 @@ __device__ __forceinline__ void inverse34(const double* T, double* I) {
 
 /* ---------------- wave primitives ---------------- */
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63u); }
+
+/* global-memory view of a pointer read out of SimArgs: the loads become global_load
+ * (SGPR base + offset addressing, vmcnt only) instead of flat loads, which also count
+ * against lgkmcnt and so serialise against every LDS wait */
+#define FKS_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ const FKS_GLOBAL T* gp(const T* p) {
+    return (const FKS_GLOBAL T*)p;
+}
+template <typename T>
+__device__ __forceinline__ FKS_GLOBAL T* gpw(T* p) {
+    return (FKS_GLOBAL T*)p;
+}
+__device__ __forceinline__ RoundDev load_round(const RoundDev* p, int r) {
+    const FKS_GLOBAL RoundDev* g = gp(p) + r;
+    RoundDev o;
+    o.link = g->link;
+    o.npts = g->npts;
+    o.radius = g->radius;
+    return o;
+}
+__device__ __forceinline__ SampledDev load_sampled(const SampledDev* p, int d) {
+    const FKS_GLOBAL SampledDev* g = gp(p) + d;
+    SampledDev o;
+    o.nbins = g->nbins;
+    o.elems = g->elems;
+    o.bounds = g->bounds;
+    o.samples = g->samples;
+    return o;
+}
 /* 64-bit lane moves: DPP within rows of 16, readlane across rows */
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
@@ -302,23 +332,36 @@ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
     const uint64_t bits = (((uint64_t)a << 32) | (uint64_t)b) >> 11;
     return (double)bits * (1.0 / 9007199254740992.0);
 }
-/* truncated normal TN(0, 0.5) on [-1, 1]: TYPE_1 accept-reject over polar normals */
+/* truncated normal TN(0, 0.5) on [-1, 1]: TYPE_1 accept-reject over polar normals.
+ * The attempts are those of the oracle (counter_truncated_normal) in the same order;
+ * the loop is split so that a wave first advances every lane to its next attempt
+ * inside the unit disc (Philox only) and then takes the logarithm once for all
+ * lanes, instead of once per attempt that any lane is still rejecting. */
 __device__ double tn_sample(uint32_t k0, uint32_t k1, uint64_t particle, uint32_t step, uint32_t micro, uint32_t dof,
                             uint32_t* err) {
     const double mean = 0.0, stddev = 0.5, lo = -2.0, hi = 2.0;
-    for (uint32_t attempt = 0; attempt < 64; ++attempt) {
-        uint32_t c[4] = {(uint32_t)particle, step, micro,
-                         ((uint32_t)(particle >> 32) << 16) | ((dof & 0xffu) << 8) | attempt};
-        philox4x32_10(c, k0, k1);
-        const double x = 2.0 * u53(c[0], c[1]) - 1.0;
-        const double y = 2.0 * u53(c[2], c[3]) - 1.0;
-        const double r2 = x * x + y * y;
-        if (r2 > 1.0 || r2 == 0.0) continue;
+    uint32_t attempt = 0;
+    while (attempt < 64u) {
+        double x, y, r2;
+        for (;;) {
+            uint32_t c[4] = {(uint32_t)particle, step, micro,
+                             ((uint32_t)(particle >> 32) << 16) | ((dof & 0xffu) << 8) | attempt};
+            philox4x32_10(c, k0, k1);
+            x = 2.0 * u53(c[0], c[1]) - 1.0;
+            y = 2.0 * u53(c[2], c[3]) - 1.0;
+            r2 = x * x + y * y;
+            if (!(r2 > 1.0 || r2 == 0.0)) break;
+            if (++attempt >= 64u) {
+                *err |= FKS_PARTICLE_ERR_RNG_EXHAUSTED;
+                return 0.0;
+            }
+        }
         const double mult = dsqrt(-2.0 * fks_math::log(r2) / r2);
         const double n1 = (y * mult) * 1.0 + 0.0;
         const double n2 = (x * mult) * 1.0 + 0.0;
         if ((n1 <= hi) && (n1 >= lo)) return mean + stddev * n1;
         if ((n2 <= hi) && (n2 >= lo)) return mean + stddev * n2;
+        ++attempt;
     }
     *err |= FKS_PARTICLE_ERR_RNG_EXHAUSTED;
     return 0.0;
@@ -461,7 +504,7 @@ __device__ __noinline__ void refill_noise_lanes(const SimArgs* __restrict__ Ap, 
             uint32_t e = 0;
             const uint32_t dof = (uint32_t)(ln % D);
             if ((A.R.sampled_mask >> dof) & 1ull)
-                nz[ln] = sampled_pick(A.key0, A.key1, pid, step, m, dof, A.R.sampled[dof].elems);
+                nz[ln] = sampled_pick(A.key0, A.key1, pid, step, m, dof, load_sampled(A.R.sampled, (int)dof).elems);
             else
                 nz[ln] = tn_sample(A.key0, A.key1, pid, step, m, dof, &e);
             ne[ln] = e;
@@ -497,12 +540,12 @@ __device__ double estimate_distance(const SimArgs& A, const D4& p, bool* inb, ui
         lo[a] = (idx[a] - 1 > 0) ? idx[a] - 1 : 0;
         hi[a] = ((int64_t)idx[a] + 1 < g.n[a] - 1) ? idx[a] + 1 : (int32_t)(g.n[a] - 1);
         const double inv = 1.0 / (g.res * (double)(hi[a] - lo[a]));
-        const float diff = A.sdf[grid_linear(g, hi[0], hi[1], hi[2])] - A.sdf[grid_linear(g, lo[0], lo[1], lo[2])];
+        const float diff = gp(A.sdf)[grid_linear(g, hi[0], hi[1], hi[2])] - gp(A.sdf)[grid_linear(g, lo[0], lo[1], lo[2])];
         grad[a] = (double)diff * inv;
     }
     const D3 c = xform3(g.org, D3{g.res * ((double)idx[0] + 0.5), g.res * ((double)idx[1] + 0.5), g.res * ((double)idx[2] + 0.5)});
     const double dx = p.x - c.x, dy = p.y - c.y, dz = p.z - c.z;
-    const double nominal = (double)A.sdf[grid_linear(g, idx[0], idx[1], idx[2])];
+    const double nominal = (double)gp(A.sdf)[grid_linear(g, idx[0], idx[1], idx[2])];
     const double corrected = (nominal >= 0.0) ? nominal - (g.res * 0.5) : nominal + (g.res * 0.5);
     const double adjustment = (dx * grad[0] + dy * grad[1]) + dz * grad[2];
     const double estimate = corrected + adjustment;
@@ -517,7 +560,7 @@ __device__ bool lookup_normal(const SimArgs& A, const D4& loc, const D4& dir, D3
     int32_t idx[3];
     if (!A.has_normals || !grid_index(A.nrm_g, loc, idx)) return false;
     const uint32_t lin = grid_linear(A.nrm_g, idx[0], idx[1], idx[2]);
-    const uint32_t begin = A.noff[lin], end = A.noff[lin + 1];
+    const uint32_t begin = gp(A.noff)[lin], end = gp(A.noff)[lin + 1];
     *bytes += 8;
     if (begin == end) return true;
     *bytes += 48ull * (uint64_t)(end - begin);
@@ -530,7 +573,7 @@ __device__ bool lookup_normal(const SimArgs& A, const D4& loc, const D4& dir, D3
     int64_t best = -1;
     double best_dot = -__builtin_huge_val();
     for (uint32_t e = begin; e < end; ++e) {
-        const double* ent = A.nent + 6ull * e;
+        const FKS_GLOBAL double* ent = gp(A.nent) + 6ull * e;
         const double dot = (ent[0] * ux + ent[1] * uy) + ent[2] * uz;
         if (dot > best_dot) {
             best_dot = dot;
@@ -541,14 +584,15 @@ __device__ bool lookup_normal(const SimArgs& A, const D4& loc, const D4& dir, D3
         *err |= FKS_PARTICLE_ERR_ZERO_DIRECTION;
         return true;
     }
-    const double* ent = A.nent + 6ull * (uint64_t)best;
+    const FKS_GLOBAL double* ent = gp(A.nent) + 6ull * (uint64_t)best;
     *out = D3{ent[3], ent[4], ent[5]};
     return true;
 }
 
 __device__ __forceinline__ D4 load_point(const RobotDev& R, int i) {
-    const double2* p2 = reinterpret_cast<const double2*>(R.points + 4ull * (uint64_t)i);
-    const double2 a = p2[0], b = p2[1];
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    const FKS_GLOBAL f64x2* p2 = gp(reinterpret_cast<const f64x2*>(R.points + 4ull * (uint64_t)i));
+    const f64x2 a = p2[0], b = p2[1];
     return D4{a.x, a.y, b.x, b.y};
 }
 
@@ -656,10 +700,10 @@ __device__ __forceinline__ double actuator_noisy(Sim& s, const fks_dof_controlle
     const double ns = noise_sample(s, micro);
     const RobotDev& R = s.A->R;
     if ((R.sampled_mask >> dof) & 1ull) {
-        const SampledDev sd = R.sampled[dof];
+        const SampledDev sd = load_sampled(R.sampled, dof);
         for (uint32_t b = 0; b < sd.nbins; ++b)
-            if (real >= sd.bounds[2 * b] && real <= sd.bounds[2 * b + 1])
-                return real + sd.samples[(uint64_t)b * sd.elems + (uint32_t)ns];
+            if (real >= gp(sd.bounds)[2 * b] && real <= gp(sd.bounds)[2 * b + 1])
+                return real + gp(sd.samples)[(uint64_t)b * sd.elems + (uint32_t)ns];
         s.err |= FKS_PARTICLE_ERR_NO_NOISE_BIN;
         return real + 0.0;
     }
@@ -789,7 +833,7 @@ __device__ double config_distance(Sim& s, const double* cfg, const double* targe
             const JointDev& jd = s.joints[s.dofj[k]];
             const double sd = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(target[k] - cfg[k])
                                                                 : target[k] - cfg[k];
-            const double d = R.weights[k] * dabs(sd);
+            const double d = gp(R.weights)[k] * dabs(sd);
             sum = sum + d * d;
         }
         return dsqrt(sum);
@@ -797,7 +841,7 @@ __device__ double config_distance(Sim& s, const double* cfg, const double* targe
         const double dx = target[0] - cfg[0];
         const double dy = target[1] - cfg[1];
         const double dr = fks_math::enforce_continuous_revolute_bounds(target[2] - cfg[2]);
-        return R.weights[0] * dsqrt(dx * dx + dy * dy) + R.weights[1] * dabs(dr);
+        return gp(R.weights)[0] * dsqrt(dx * dx + dy * dy) + gp(R.weights)[1] * dabs(dr);
     } else {
         double P[12], Pi[12], Tg[12], Dm[12], tw[6];
         for (int k = 0; k < 12; ++k) {
@@ -809,7 +853,7 @@ __device__ double config_distance(Sim& s, const double* cfg, const double* targe
         compose34(Pi, Tg, Dm);
         log_twist34(Dm, tw);
         const double angle = dsqrt((tw[3] * tw[3] + tw[4] * tw[4]) + tw[5] * tw[5]);
-        return R.weights[0] * dsqrt((dx * dx + dy * dy) + dz * dz) + R.weights[1] * angle;
+        return gp(R.weights)[0] * dsqrt((dx * dx + dy * dy) + dz * dz) + gp(R.weights)[1] * angle;
     }
 }
 
@@ -863,7 +907,7 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
     bool sk = false;
     const int ln = s.lane;
     if (ln < R.nrounds) {
-        const RoundDev& rd = R.rounds[ln];
+        const RoundDev rd = load_round(R.rounds, ln);
         const double* st = s.lds + A.L.rstate + kRoundState * ln;
         if (rd.link >= 0 && st[12] > kInvalidRound) {
             const double b = rigid_motion_bound(T + 12 * rd.link, st, rd.radius) * A.sdf_g.inv_res; /* cells */
@@ -892,7 +936,7 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
 __device__ __forceinline__ void round_update(Sim& s, int r, const double* T, double S, double G, double C) {
     const SimArgs& A = *s.A;
     if (!A.skip_enabled || r >= kWave || r >= A.R.nrounds) return;
-    const RoundDev& rd = A.R.rounds[r];
+    const RoundDev rd = load_round(A.R.rounds, r);
     if (rd.link < 0) return;
     const double smin = wave_min(S), gmin = wave_min(G), cmin = wave_min(C);
     double* st = s.lds + A.L.rstate + kRoundState * r;
@@ -911,7 +955,7 @@ __device__ __forceinline__ double round_max_motion(const RobotDev& R, const doub
     const int i = kWave * r + ln;
     if (i >= R.P) return 0.0;
     const D4 p = load_point(R, i);
-    const int link = R.point_link[i];
+    const int link = gp(R.point_link)[i];
     const D4 a = xform4(TA + 12 * link, p), b = xform4(TB + 12 * link, p);
     return sqnorm4(D4{b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w});
 }
@@ -930,7 +974,7 @@ __device__ double max_point_motion(Sim& s, const double* TA, const double* TB) {
     }
     double ub = 0.0;
     if (ln < nr) {
-        const RoundDev& rd = R.rounds[ln];
+        const RoundDev rd = load_round(R.rounds, ln);
         ub = (rd.link >= 0) ? rigid_motion_bound(TB + 12 * rd.link, TA + 12 * rd.link, rd.radius) : __builtin_huge_val();
     }
     const double top = wave_max_nonneg(ub);
@@ -956,7 +1000,7 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
     const RobotDev& R = A.R;
     if (i >= R.P) return false;
     const D4 p = load_point(R, i);
-    const int link = R.point_link[i];
+    const int link = gp(R.point_link)[i];
     const D4 x = xform4(T + 12 * link, p);
     const GridDev& g = A.sdf_g;
     const D4 q = xform4(g.inv, x);
@@ -975,7 +1019,7 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
     }
     float d = A.oob;
     if (ok) {
-        d = A.sdf[grid_linear(g, idx[0], idx[1], idx[2])];
+        d = gp(A.sdf)[grid_linear(g, idx[0], idx[1], idx[2])];
         *b += 4;
         *S = (double)d;
         *G = margin;
@@ -1104,7 +1148,7 @@ __device__ __noinline__ uint32_t extract_cell(const SimArgs* __restrict__ Ap, do
     int gbeg[kMaxGeoms], gend[kMaxGeoms];
     int ng = 0;
     for (int m = 0; m < nm; ++m) {
-        const int g = R.point_geom[members[m]];
+        const int g = gp(R.point_geom)[members[m]];
         if (ng == 0 || geo[ng - 1] != g) {
             if (ng == kMaxGeoms) break;
             geo[ng] = g;
@@ -1119,7 +1163,7 @@ __device__ __noinline__ uint32_t extract_cell(const SimArgs* __restrict__ Ap, do
     for (int a = 0; a < ng; ++a) present |= 1ull << geo[a];
     int ncollide_links = 0;
     for (int a = 0; a < ng; ++a) {
-        const uint64_t disallowed = present & ~R.allowed_mask[geo[a]] & ~(1ull << geo[a]);
+        const uint64_t disallowed = present & ~gp(R.allowed_mask)[geo[a]] & ~(1ull << geo[a]);
         if (disallowed) ncollide_links++;
     }
     if (ncollide_links < 2) return 0;
@@ -1130,10 +1174,10 @@ __device__ __noinline__ uint32_t extract_cell(const SimArgs* __restrict__ Ap, do
     const double tm = A.time_multiplier;
     D4 mom[FKS_MAX_SELF_LINKS];
     for (int a = 0; a < ng; ++a) {
-        const uint64_t disallowed = present & ~R.allowed_mask[geo[a]] & ~(1ull << geo[a]);
+        const uint64_t disallowed = present & ~gp(R.allowed_mask)[geo[a]] & ~(1ull << geo[a]);
         mom[a] = D4{0.0, 0.0, 0.0, 0.0};
         if (!disallowed) continue;
-        const int link = R.geom_link[geo[a]];
+        const int link = gp(R.geom_link)[geo[a]];
         for (int m = gbeg[a]; m < gend[a]; ++m) {
             const D4 p = load_point(R, members[m]);
             const D4 pv = xform4(Tp + 12 * link, p), cv = xform4(Tc + 12 * link, p);
@@ -1142,13 +1186,13 @@ __device__ __noinline__ uint32_t extract_cell(const SimArgs* __restrict__ Ap, do
         }
     }
     for (int a = 0; a < ng; ++a) {
-        const uint64_t disallowed = present & ~R.allowed_mask[geo[a]] & ~(1ull << geo[a]);
+        const uint64_t disallowed = present & ~gp(R.allowed_mask)[geo[a]] & ~(1ull << geo[a]);
         if (!disallowed) continue;
         int others[FKS_MAX_SELF_LINKS];
         int n = 0;
         for (int b = 0; b < ng; ++b)
             if ((disallowed >> geo[b]) & 1ull) others[n++] = b;
-        const int link = R.geom_link[geo[a]];
+        const int link = gp(R.geom_link)[geo[a]];
         const D4 link_loc = xform4(Tp + 12 * link, load_point(R, members[gbeg[a]]));
         const double cnt = (double)(gend[a] - gbeg[a]);
         const D4 link_vel{mom[a].x / cnt, mom[a].y / cnt, mom[a].z / cnt, mom[a].w / cnt};
@@ -1172,7 +1216,7 @@ __device__ __noinline__ uint32_t extract_cell(const SimArgs* __restrict__ Ap, do
         for (int k = 0; k < ccols * n; ++k) N[k] = 0.0;
         for (int c = 0; c < n; ++c) {
             const int ob = others[c];
-            const int olink = R.geom_link[geo[ob]];
+            const int olink = gp(R.geom_link)[geo[ob]];
             const D4 oloc = xform4(Tp + 12 * olink, load_point(R, members[gbeg[ob]]));
             const D4 cn = safe_normal4(D4{oloc.x - link_loc.x, oloc.y - link_loc.y, oloc.z - link_loc.z, oloc.w - link_loc.w});
             N[(c * 3 + 0) * n + c] = cn.x;
@@ -1180,10 +1224,10 @@ __device__ __noinline__ uint32_t extract_cell(const SimArgs* __restrict__ Ap, do
             N[(c * 3 + 2) * n + c] = cn.z;
         }
         for (int k = 0; k < rows * rows; ++k) M[k] = 0.0;
-        const double lm = R.geom_mass[geo[a]];
+        const double lm = gp(R.geom_mass)[geo[a]];
         for (int d = 0; d < 3; ++d) M[d * rows + d] = lm;
         for (int l = 1; l <= n; ++l) {
-            const double om = R.geom_mass[geo[others[l - 1]]];
+            const double om = gp(R.geom_mass)[geo[others[l - 1]]];
             for (int d = 0; d < 3; ++d) M[(l * 3 + d) * rows + (l * 3 + d)] = om;
         }
         V[0] = link_vel.x;
@@ -1289,8 +1333,8 @@ __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
             a = (int)(ab & 0xffffu);
             b = (int)(ab >> 16);
         } else {
-            a = R.pairs[2 * k];
-            b = R.pairs[2 * k + 1];
+            a = gp(R.pairs)[2 * k];
+            b = gp(R.pairs)[2 * k + 1];
         }
         bool ov = true;
         for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
@@ -1317,7 +1361,7 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
     int32_t* list = reinterpret_cast<int32_t*>(scratch + SL.list);
     for (int i = ln; i < R.P; i += kWave) {
         const D4 p = load_point(R, i);
-        const int link = R.point_link[i];
+        const int link = gp(R.point_link)[i];
         const D4 x = xform4(Tc + 12 * link, p);
         const D4 g = xform4(A.env_g.inv, x);
         const double q[3] = {g.x / A.env_g.res, g.y / A.env_g.res, g.z / A.env_g.res};
@@ -1341,12 +1385,12 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
     wsync();
     /* exact candidate marking over pairs whose boxes overlap */
     for (int k = 0; k < R.npairs; ++k) {
-        const int a = R.pairs[2 * k], b = R.pairs[2 * k + 1];
+        const int a = gp(R.pairs)[2 * k], b = gp(R.pairs)[2 * k + 1];
         bool ov = true;
         for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
         if (!ov) continue;
-        const int a0 = (int)R.geom_off[a], a1 = (int)R.geom_off[a + 1];
-        const int b0 = (int)R.geom_off[b], b1 = (int)R.geom_off[b + 1];
+        const int a0 = (int)gp(R.geom_off)[a], a1 = (int)gp(R.geom_off)[a + 1];
+        const int b0 = (int)gp(R.geom_off)[b], b1 = (int)gp(R.geom_off)[b + 1];
         for (int i = a0 + ln; i < a1; i += kWave) {
             const int64_t kx = keys[3 * i], ky = keys[3 * i + 1], kz = keys[3 * i + 2];
             bool hit = false;
@@ -1442,10 +1486,10 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
     const int ln = s.lane;
     const int D = R.D;
     const ScratchLayout& SL = A.SL;
-    double* J = s.scratch + SL.J;
-    double* bv = s.scratch + SL.b;
-    const double* corr = s.scratch + SL.corr;
-    const double* flag = s.scratch + SL.flag;
+    FKS_GLOBAL double* J = gpw(s.scratch) + SL.J;
+    FKS_GLOBAL double* bv = gpw(s.scratch) + SL.b;
+    const FKS_GLOBAL double* corr = gp(s.scratch) + SL.corr;
+    const FKS_GLOBAL double* flag = gp(s.scratch) + SL.flag;
     const uint32_t rc = A.row_cap;
     joint_frames<RT>(s, Tc);
     const double* axw = s.lds + s.A->L.axis_w;
@@ -1469,7 +1513,7 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
         int link = 0;
         if (i < R.P) {
             const D4 p = load_point(R, i);
-            link = R.point_link[i];
+            link = gp(R.point_link)[i];
             xc = xform4(Tc + 12 * link, p);
             const bool has_self = s.self_nonempty && flag[i] != 0.0;
             bool inb = false;
@@ -1502,7 +1546,7 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
             bv[row + 1] = pcorr.y;
             bv[row + 2] = pcorr.z;
             if constexpr (RT == FKS_ROBOT_LINKED) {
-                const uint64_t mask = R.link_dof_mask[link];
+                const uint64_t mask = gp(R.link_dof_mask)[link];
                 for (int d = 0; d < D; ++d) {
                     D3 col{0.0, 0.0, 0.0};
                     if ((mask >> d) & 1ull) {
@@ -1570,8 +1614,8 @@ __device__ FKS_QR_ATTR void qr_solve_regs(const SimArgs* __restrict__ Ap, double
     const SimArgs& A = *Ap;
     const int D = A.R.D;
     const uint32_t rc = A.row_cap;
-    const double* Jm = scratch + A.SL.J;
-    const double* bv = scratch + A.SL.b;
+    const FKS_GLOBAL double* Jm = gp(scratch) + A.SL.J;
+    const FKS_GLOBAL double* bv = gp(scratch) + A.SL.b;
     double* colsq = lds + A.L.colsq;
     double* hco = lds + A.L.hcoef;
     int32_t* perm = reinterpret_cast<int32_t*>(lds + A.L.ints);
@@ -1949,7 +1993,7 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
      * already prove it. */
     bool proven = false;
     if constexpr (RT == FKS_ROBOT_LINKED) {
-        const double term = (ln < D) ? dabs(ustep[ln]) * R.dof_lever[ln] : 0.0;
+        const double term = (ln < D) ? dabs(ustep[ln]) * gp(R.dof_lever)[ln] : 0.0;
         const double bound = bfly_sum(0.0 + term);
         proven = bound * (1.0 + 1e-6) + 1e-12 < A.allowed_micro;
     }
@@ -2092,14 +2136,14 @@ __device__ __forceinline__ void setup_wave(const SimArgs* __restrict__ args, dou
         const uint64_t* sc = reinterpret_cast<const uint64_t*>(R.ctrl);
         for (int k = t; k < R.D * kCtrlWords; k += nt) dc[k] = sc[k];
         int32_t* dd = reinterpret_cast<int32_t*>(shared + A.L.dofj);
-        if (RT == FKS_ROBOT_LINKED && t < R.D) dd[t] = R.dof_joint[t];
+        if (RT == FKS_ROBOT_LINKED && t < R.D) dd[t] = gp(R.dof_joint)[t];
         if (t < 12) shared[A.L.base + t] = R.base[t];
         if (RT == FKS_ROBOT_LINKED) {
             for (int k = t; k < 8 * R.G; k += nt)
-                shared[A.L.gbox + k] = (k % 8 == 7) ? (double)R.geom_link[k / 8] : R.geom_box[7 * (k / 8) + k % 8];
+                shared[A.L.gbox + k] = (k % 8 == 7) ? (double)gp(R.geom_link)[k / 8] : gp(R.geom_box)[7 * (k / 8) + k % 8];
             uint32_t* lp = reinterpret_cast<uint32_t*>(shared + A.L.gpairs);
             for (int k = t; k < R.npairs && k < kLdsPairs; k += nt)
-                lp[k] = (uint32_t)R.pairs[2 * k] | ((uint32_t)R.pairs[2 * k + 1] << 16);
+                lp[k] = (uint32_t)gp(R.pairs)[2 * k] | ((uint32_t)gp(R.pairs)[2 * k + 1] << 16);
         }
         __syncthreads();
     }
@@ -2181,7 +2225,7 @@ __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict
     wsync();
     bool any = false;
     for (int k = ln; k < R.npairs; k += kWave) {
-        const int a = R.pairs[2 * k], b = R.pairs[2 * k + 1];
+        const int a = gp(R.pairs)[2 * k], b = gp(R.pairs)[2 * k + 1];
         bool ov = true;
         for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
         any = any || ov;
@@ -2191,7 +2235,7 @@ __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict
     int64_t* keys = reinterpret_cast<int64_t*>(scratch + A.SL.keys);
     uint32_t err = 0;
     for (int i = ln; i < R.P; i += kWave) {
-        const D4 x = xform4(Tc + 12 * (int)R.point_link[i], load_point(R, i));
+        const D4 x = xform4(Tc + 12 * (int)gp(R.point_link)[i], load_point(R, i));
         const D4 g = xform4(A.env_g.inv, x);
         const double q[3] = {g.x / res, g.y / res, g.z / res};
         for (int a = 0; a < 3; ++a) {
@@ -2212,12 +2256,12 @@ __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict
     wsync();
     bool hit = false;
     for (int k = 0; k < R.npairs && !wave_any(hit); ++k) {
-        const int a = R.pairs[2 * k], b = R.pairs[2 * k + 1];
+        const int a = gp(R.pairs)[2 * k], b = gp(R.pairs)[2 * k + 1];
         bool ov = true;
         for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
         if (!ov) continue;
-        const int a0 = (int)R.geom_off[a], a1 = (int)R.geom_off[a + 1];
-        const int b0 = (int)R.geom_off[b], b1 = (int)R.geom_off[b + 1];
+        const int a0 = (int)gp(R.geom_off)[a], a1 = (int)gp(R.geom_off)[a + 1];
+        const int b0 = (int)gp(R.geom_off)[b], b1 = (int)gp(R.geom_off)[b + 1];
         for (int i = a0 + ln; i < a1; i += kWave) {
             const int64_t kx = keys[3 * i], ky = keys[3 * i + 1], kz = keys[3 * i + 2];
             for (int j = b0; j < b1 && !hit; ++j) hit = (keys[3 * j] == kx) && (keys[3 * j + 1] == ky) && (keys[3 * j + 2] == kz);
@@ -2298,14 +2342,14 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         const uint64_t* sc = reinterpret_cast<const uint64_t*>(R.ctrl);
         for (int k = t; k < R.D * kCtrlWords; k += nt) dc[k] = sc[k];
         int32_t* dd = reinterpret_cast<int32_t*>(shared + A.L.dofj);
-        if (RT == FKS_ROBOT_LINKED && t < R.D) dd[t] = R.dof_joint[t];
+        if (RT == FKS_ROBOT_LINKED && t < R.D) dd[t] = gp(R.dof_joint)[t];
         if (t < 12) shared[A.L.base + t] = R.base[t];
         if (RT == FKS_ROBOT_LINKED) {
             for (int k = t; k < 8 * R.G; k += nt)
-                shared[A.L.gbox + k] = (k % 8 == 7) ? (double)R.geom_link[k / 8] : R.geom_box[7 * (k / 8) + k % 8];
+                shared[A.L.gbox + k] = (k % 8 == 7) ? (double)gp(R.geom_link)[k / 8] : gp(R.geom_box)[7 * (k / 8) + k % 8];
             uint32_t* lp = reinterpret_cast<uint32_t*>(shared + A.L.gpairs);
             for (int k = t; k < R.npairs && k < kLdsPairs; k += nt)
-                lp[k] = (uint32_t)R.pairs[2 * k] | ((uint32_t)R.pairs[2 * k + 1] << 16);
+                lp[k] = (uint32_t)gp(R.pairs)[2 * k] | ((uint32_t)gp(R.pairs)[2 * k + 1] << 16);
         }
         __syncthreads(); /* the only workgroup barrier: waves run independently afterwards */
     }
