@@ -292,7 +292,10 @@ __device__ __forceinline__ double wave_max_nonneg(double v) {
     const double a = (r1 > r0) ? r1 : r0, b = (r3 > r2) ? r3 : r2;
     return (b > a) ? b : a;
 }
+/* OR over the wave's lanes.  Error bits are rare: one ballot answers the common
+ * all-zero case without the six dependent LDS-crossbar shuffles. */
 __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+    if (__ballot(v != 0u) == 0ull) return 0u;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v |= (uint32_t)__shfl_xor((int)v, off, 64);
     return v;
@@ -491,7 +494,10 @@ __device__ __forceinline__ void count_event(Sim& s, int slot, uint64_t n) {
         if (s.lane == 0) s.phase[slot] += n;
 }
 
-__device__ __noinline__ void refill_noise_lanes(const SimArgs* __restrict__ Ap, double* lds, int ln, uint64_t pid, uint32_t step,
+#ifndef FKS_REFILL_ATTR
+#define FKS_REFILL_ATTR __noinline__
+#endif
+__device__ FKS_REFILL_ATTR void refill_noise_lanes(const SimArgs* __restrict__ Ap, double* lds, int ln, uint64_t pid, uint32_t step,
                                                 uint32_t micro0, uint32_t M) {
     const SimArgs& A = *Ap;
     const int D = A.R.D;
