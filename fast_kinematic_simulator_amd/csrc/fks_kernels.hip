@@ -1773,6 +1773,207 @@ __device__ FKS_QR_ATTR void qr_solve_regs(const SimArgs* __restrict__ Ap, double
     wsync();
 }
 
+/* canonical 64-lane sum (bfly_sum) of partials that only rows r < RM can hold, all
+ * in one lane: the butterfly is the perfect binary tree over the lanes in index
+ * order, and the lanes >= RM contribute +0.0 (the last "+ 0.0" is the (r0 + r1) +
+ * (r2 + r3) of bfly_sum with r1 = r2 = r3 = +0.0) */
+template <int RM>
+__device__ __forceinline__ double lane_tree_sum(const double (&p)[RM]) {
+    static_assert(RM == 8 || RM == 16, "tree over 8 or 16 rows");
+    double l1[RM / 2];
+#pragma unroll
+    for (int i = 0; i < RM / 2; ++i) l1[i] = p[2 * i] + p[2 * i + 1];
+    double l2[RM / 4];
+#pragma unroll
+    for (int i = 0; i < RM / 4; ++i) l2[i] = l1[2 * i] + l1[2 * i + 1];
+    double t = (l2[0] + l2[1]);
+    if constexpr (RM == 16) t = t + ((l2[2] + l2[3]));
+    return t + 0.0;
+}
+
+/* ColPivHouseholderQR::solve for Rn <= RM rows with one COLUMN per lane (lane c < D
+ * holds column c, lane D the right-hand side): every reduction over rows is then a
+ * short in-lane tree (lane_tree_sum, the same canonical order as bfly_sum) instead
+ * of a wave butterfly, and the D - k - 1 column updates of step k run side by side
+ * in their lanes.  Same arithmetic as qr_solve_regs / qr_solve, bit for bit. */
+template <int RM>
+__device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
+                                           uint32_t Rn, double* x) {
+    const SimArgs& A = *Ap;
+    const int D = A.R.D;
+    const uint32_t rc = A.row_cap;
+    const FKS_GLOBAL double* Jm = gp(scratch) + A.SL.J;
+    const FKS_GLOBAL double* bv = gp(scratch) + A.SL.b;
+    double* colsq = lds + A.L.colsq;
+    double* hco = lds + A.L.hcoef;
+    int32_t* perm = reinterpret_cast<int32_t*>(lds + A.L.ints);
+    int32_t* transp = perm + kMaxDofs;
+    const bool isc = ln < D, isb = ln == D;
+    double a[RM];
+#pragma unroll
+    for (int r = 0; r < RM; ++r)
+        a[r] = ((uint32_t)r < Rn) ? (isc ? Jm[(uint64_t)ln * rc + r] : (isb ? bv[r] : 0.0)) : 0.0;
+    if (ln < D) x[ln] = 0.0;
+    if (D == 0) {
+        wsync();
+        return;
+    }
+    {
+        double p[RM];
+#pragma unroll
+        for (int r = 0; r < RM; ++r) p[r] = ((uint32_t)r < Rn) ? 0.0 + a[r] * a[r] : 0.0;
+        const double cs = lane_tree_sum<RM>(p);
+        if (isc) colsq[ln] = cs;
+    }
+    wsync();
+    double maxsq = colsq[0];
+    for (int k = 1; k < D; ++k)
+        if (colsq[k] > maxsq) maxsq = colsq[k];
+    const double eps = 2.220446049250313e-16;
+    const double threshold_helper = maxsq * (eps * eps) / (double)Rn;
+    const int size = ((int)Rn < D) ? (int)Rn : D;
+    int nz = size;
+    for (int k = 0; k < size; ++k) {
+        int biggest = k;
+        double bsq = colsq[k];
+        for (int c2 = k + 1; c2 < D; ++c2)
+            if (colsq[c2] > bsq) {
+                bsq = colsq[c2];
+                biggest = c2;
+            }
+        {
+            double p[RM];
+#pragma unroll
+            for (int r = 0; r < RM; ++r) p[r] = ((uint32_t)r < Rn && r >= k) ? 0.0 + a[r] * a[r] : 0.0;
+            bsq = readlane_f64(lane_tree_sum<RM>(p), biggest);
+        }
+        if (nz == size && bsq < threshold_helper * (double)(Rn - (uint32_t)k)) nz = k;
+        wsync();
+        if (ln == 0) {
+            colsq[biggest] = bsq;
+            transp[k] = biggest;
+        }
+        if (k != biggest) {
+            /* lanes k and biggest trade columns */
+            const int src = (ln == k) ? biggest : ((ln == biggest) ? k : ln);
+#pragma unroll
+            for (int r = 0; r < RM; ++r)
+                if ((uint32_t)r < Rn) a[r] = __shfl(a[r], src, 64);
+            if (ln == 0) {
+                const double t = colsq[k];
+                colsq[k] = colsq[biggest];
+                colsq[biggest] = t;
+            }
+        }
+        wsync();
+        /* Householder vector of column k, computed in lane k and broadcast */
+        double tau, beta;
+        {
+            double c0 = 0.0;
+#pragma unroll
+            for (int r = 0; r < RM; ++r)
+                if (r == k) c0 = a[r];
+            double p[RM];
+#pragma unroll
+            for (int r = 0; r < RM; ++r) p[r] = ((uint32_t)r < Rn && r > k) ? 0.0 + a[r] * a[r] : 0.0;
+            const double tail = (Rn - (uint32_t)k == 1u) ? 0.0 : lane_tree_sum<RM>(p);
+            if (tail <= 2.2250738585072014e-308) {
+                tau = 0.0;
+                beta = c0;
+                if (ln == k) {
+#pragma unroll
+                    for (int r = 0; r < RM; ++r)
+                        if (r > k) a[r] = 0.0;
+                }
+            } else {
+                beta = dsqrt(c0 * c0 + tail);
+                if (c0 >= 0.0) beta = -beta;
+                const double denom = c0 - beta;
+                if (ln == k) {
+#pragma unroll
+                    for (int r = 0; r < RM; ++r)
+                        if (r > k && (uint32_t)r < Rn) a[r] = a[r] / denom;
+                }
+                tau = (beta - c0) / beta;
+            }
+            if (ln == k) {
+#pragma unroll
+                for (int r = 0; r < RM; ++r)
+                    if (r == k) a[r] = beta;
+            }
+            tau = readlane_f64(tau, k);
+        }
+        if (ln == 0) hco[k] = tau;
+        double v[RM];
+#pragma unroll
+        for (int r = 0; r < RM; ++r) v[r] = (r > k && (uint32_t)r < Rn) ? readlane_f64(a[r], k) : 0.0;
+        /* apply H_k to the columns right of k (and, while the rank holds, to the rhs) */
+        const bool upd = (isc && ln > k) || (isb && k < nz);
+        if (upd) {
+            double akk = 0.0;
+#pragma unroll
+            for (int r = 0; r < RM; ++r)
+                if (r == k) akk = a[r];
+            if (Rn - (uint32_t)k == 1u) {
+                akk = akk * (1.0 - tau);
+            } else if (tau != 0.0) {
+                double p[RM];
+#pragma unroll
+                for (int r = 0; r < RM; ++r) p[r] = (r > k && (uint32_t)r < Rn) ? 0.0 + v[r] * a[r] : 0.0;
+                const double t = lane_tree_sum<RM>(p) + akk;
+                akk = akk - tau * t;
+#pragma unroll
+                for (int r = 0; r < RM; ++r)
+                    if (r > k && (uint32_t)r < Rn) a[r] = a[r] - (tau * v[r]) * t;
+            }
+#pragma unroll
+            for (int r = 0; r < RM; ++r)
+                if (r == k) a[r] = akk;
+            /* colsq downdate with the updated row k */
+            if (isc) colsq[ln] = colsq[ln] - akk * akk;
+        }
+        wsync();
+    }
+    if (ln == 0) {
+        for (int i = 0; i < D; ++i) perm[i] = i;
+        for (int k = 0; k < size; ++k) {
+            const int t = perm[k];
+            perm[k] = perm[transp[k]];
+            perm[transp[k]] = t;
+        }
+    }
+    wsync();
+    if (nz == 0) return;
+    /* column-oriented back substitution on the nz x nz upper triangle (uniform values) */
+    double bu[RM];
+#pragma unroll
+    for (int r = 0; r < RM; ++r) bu[r] = ((uint32_t)r < Rn) ? readlane_f64(a[r], D) : 0.0;
+    for (int ii = nz - 1; ii >= 0; --ii) {
+        double ci = 0.0;
+#pragma unroll
+        for (int r = 0; r < RM; ++r)
+            if (r == ii) ci = bu[r];
+        if (ci != 0.0) {
+            double rii = 0.0;
+#pragma unroll
+            for (int r = 0; r < RM; ++r)
+                if (r == ii) rii = readlane_f64(a[r], ii);
+            const double vq = ci / rii;
+#pragma unroll
+            for (int r = 0; r < RM; ++r) {
+                if (r == ii) bu[r] = vq;
+                if (r < ii) bu[r] = bu[r] - vq * readlane_f64(a[r], ii);
+            }
+        }
+    }
+    double mine = 0.0;
+#pragma unroll
+    for (int r = 0; r < RM; ++r)
+        if (r == ln) mine = bu[r];
+    if (ln < nz) x[perm[ln]] = mine;
+    wsync();
+}
+
 /* ColPivHouseholderQR::solve (Eigen 3.2 / 3.3-beta1), rows lane-strided; x -> LDS */
 __device__ __noinline__ void qr_solve(const SimArgs* __restrict__ Ap, double* lds, double* scratch, int ln, uint32_t Rn, double* x) {
     const SimArgs& A = *Ap;
@@ -2055,7 +2256,11 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
                 tock(s, FKS_PHASE_CORRECTIONS, t0);
                 if (s.err) return 1;
                 t0 = tick();
-                if (Rn <= (uint32_t)kWave && R.D <= 8)
+                if (Rn <= 8u && R.D < kWave)
+                    qr_solve_cols<8>(s.A, s.lds, s.scratch, ln, Rn, x);
+                else if (Rn <= 16u && R.D < kWave)
+                    qr_solve_cols<16>(s.A, s.lds, s.scratch, ln, Rn, x);
+                else if (Rn <= (uint32_t)kWave && R.D <= 8)
                     qr_solve_regs<8>(s.A, s.lds, s.scratch, ln, Rn, x);
                 else if (RT == FKS_ROBOT_LINKED && Rn <= (uint32_t)kWave && R.D <= 16)
                     qr_solve_regs<RT == FKS_ROBOT_LINKED ? 16 : 8>(s.A, s.lds, s.scratch, ln, Rn, x);
