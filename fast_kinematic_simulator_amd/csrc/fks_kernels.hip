@@ -1791,6 +1791,32 @@ __device__ __forceinline__ double lane_tree_sum(const double (&p)[RM]) {
     return t + 0.0;
 }
 
+/* max over the wave of v (pass -inf for lanes that do not take part) */
+__device__ __forceinline__ double wave_max_any(double v) {
+    double o = dpp_f64<kDppXor1>(v);
+    v = (o > v) ? o : v;
+    o = dpp_f64<kDppXor2>(v);
+    v = (o > v) ? o : v;
+    o = dpp_f64<kDppHalfMirror>(v);
+    v = (o > v) ? o : v;
+    o = dpp_f64<kDppMirror>(v);
+    v = (o > v) ? o : v;
+    const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16), r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
+    const double a = (r1 > r0) ? r1 : r0, b = (r3 > r2) ? r3 : r2;
+    return (b > a) ? b : a;
+}
+/* the serial scan "best = first; for i > first: if (val[i] > best) take i" over the
+ * lanes first..last-1 (lane i holds val[i]), as one wave reduction: the first lane
+ * holding the maximum of the non-NaN values, or `first` when val[first] is NaN or
+ * already the maximum */
+__device__ __forceinline__ int wave_first_argmax(double val, int ln, int first, int last) {
+    const double vf = readlane_f64(val, first);
+    const bool part = ln > first && ln < last && !__builtin_isnan(val);
+    const double m = wave_max_any(part ? val : -__builtin_huge_val());
+    if (__builtin_isnan(vf) || !(m > vf)) return first;
+    return __ffsll((unsigned long long)__ballot(part && val == m)) - 1;
+}
+
 /* ColPivHouseholderQR::solve for Rn <= RM rows with one COLUMN per lane (lane c < D
  * holds column c, lane D the right-hand side): every reduction over rows is then a
  * short in-lane tree (lane_tree_sum, the same canonical order as bfly_sum) instead
@@ -1804,8 +1830,6 @@ __device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double
     const uint32_t rc = A.row_cap;
     const FKS_GLOBAL double* Jm = gp(scratch) + A.SL.J;
     const FKS_GLOBAL double* bv = gp(scratch) + A.SL.b;
-    double* colsq = lds + A.L.colsq;
-    double* hco = lds + A.L.hcoef;
     int32_t* perm = reinterpret_cast<int32_t*>(lds + A.L.ints);
     int32_t* transp = perm + kMaxDofs;
     const bool isc = ln < D, isb = ln == D;
@@ -1818,29 +1842,28 @@ __device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double
         wsync();
         return;
     }
+    /* squared column norms, one per column lane (the colsq vector of the solvers above) */
+    double cs;
     {
         double p[RM];
 #pragma unroll
         for (int r = 0; r < RM; ++r) p[r] = ((uint32_t)r < Rn) ? 0.0 + a[r] * a[r] : 0.0;
-        const double cs = lane_tree_sum<RM>(p);
-        if (isc) colsq[ln] = cs;
+        cs = lane_tree_sum<RM>(p);
     }
-    wsync();
-    double maxsq = colsq[0];
-    for (int k = 1; k < D; ++k)
-        if (colsq[k] > maxsq) maxsq = colsq[k];
+    /* maxsq = colsq[0]; for k: if (colsq[k] > maxsq) maxsq = colsq[k] */
+    double maxsq;
+    {
+        const double c0 = readlane_f64(cs, 0);
+        const double m = wave_max_any((isc && ln > 0 && !__builtin_isnan(cs)) ? cs : -__builtin_huge_val());
+        maxsq = (__builtin_isnan(c0) || !(m > c0)) ? c0 : m;
+    }
     const double eps = 2.220446049250313e-16;
     const double threshold_helper = maxsq * (eps * eps) / (double)Rn;
     const int size = ((int)Rn < D) ? (int)Rn : D;
     int nz = size;
     for (int k = 0; k < size; ++k) {
-        int biggest = k;
-        double bsq = colsq[k];
-        for (int c2 = k + 1; c2 < D; ++c2)
-            if (colsq[c2] > bsq) {
-                bsq = colsq[c2];
-                biggest = c2;
-            }
+        const int biggest = wave_first_argmax(cs, ln, k, D);
+        double bsq;
         {
             double p[RM];
 #pragma unroll
@@ -1848,24 +1871,16 @@ __device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double
             bsq = readlane_f64(lane_tree_sum<RM>(p), biggest);
         }
         if (nz == size && bsq < threshold_helper * (double)(Rn - (uint32_t)k)) nz = k;
-        wsync();
-        if (ln == 0) {
-            colsq[biggest] = bsq;
-            transp[k] = biggest;
-        }
+        if (ln == 0) transp[k] = biggest;
+        if (ln == biggest) cs = bsq;
         if (k != biggest) {
-            /* lanes k and biggest trade columns */
+            /* lanes k and biggest trade columns (and their squared norms) */
             const int src = (ln == k) ? biggest : ((ln == biggest) ? k : ln);
 #pragma unroll
             for (int r = 0; r < RM; ++r)
                 if ((uint32_t)r < Rn) a[r] = __shfl(a[r], src, 64);
-            if (ln == 0) {
-                const double t = colsq[k];
-                colsq[k] = colsq[biggest];
-                colsq[biggest] = t;
-            }
+            cs = __shfl(cs, src, 64);
         }
-        wsync();
         /* Householder vector of column k, computed in lane k and broadcast */
         double tau, beta;
         {
@@ -1903,7 +1918,6 @@ __device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double
             }
             tau = readlane_f64(tau, k);
         }
-        if (ln == 0) hco[k] = tau;
         double v[RM];
 #pragma unroll
         for (int r = 0; r < RM; ++r) v[r] = (r > k && (uint32_t)r < Rn) ? readlane_f64(a[r], k) : 0.0;
@@ -1930,9 +1944,8 @@ __device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double
             for (int r = 0; r < RM; ++r)
                 if (r == k) a[r] = akk;
             /* colsq downdate with the updated row k */
-            if (isc) colsq[ln] = colsq[ln] - akk * akk;
+            if (isc) cs = cs - akk * akk;
         }
-        wsync();
     }
     if (ln == 0) {
         for (int i = 0; i < D; ++i) perm[i] = i;
