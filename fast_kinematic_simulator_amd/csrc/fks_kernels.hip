@@ -2285,12 +2285,20 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
                 fk<RT>(s, cfg_tmp, Ttmp);
                 const double est = max_point_motion(s, Tcur, Ttmp);
                 const double step_fraction = dmax(est / A.allowed_micro, 1.0);
-                if (ln < D) real[ln] = (x[ln] / step_fraction) * dabs(scaling);
-                wsync();
-                apply_input<RT>(s, cfg_act, real, cfg_tmp, false, 0);
-                if (ln < W) cfg_act[ln] = cfg_tmp[ln];
-                wsync();
-                fk<RT>(s, cfg_act, Tcur);
+                if (step_fraction == 1.0 && dabs(scaling) == 1.0) {
+                    /* real_correction_step = (x / 1) * 1 == x bit for bit (SPCS:1681-1682): the
+                     * corrected configuration is cfg_tmp and its transforms are Ttmp */
+                    if (ln < W) cfg_act[ln] = cfg_tmp[ln];
+                    for (int e = ln; e < 12 * R.L; e += kWave) Tcur[e] = Ttmp[e];
+                    wsync();
+                } else {
+                    if (ln < D) real[ln] = (x[ln] / step_fraction) * dabs(scaling);
+                    wsync();
+                    apply_input<RT>(s, cfg_act, real, cfg_tmp, false, 0);
+                    if (ln < W) cfg_act[ln] = cfg_tmp[ln];
+                    wsync();
+                    fk<RT>(s, cfg_act, Tcur);
+                }
                 tock(s, FKS_PHASE_RESOLVE_APPLY, t0);
                 in_collision = check_collision<RT>(s, Tprev, Tcur);
                 if (s.err) return 1;
