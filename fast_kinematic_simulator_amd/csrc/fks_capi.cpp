@@ -85,6 +85,7 @@ GridDev make_grid(const fks_grid_geometry& g) {
     d.res = g.resolution;
     d.inv_res = 1.0 / g.resolution;
     for (int a = 0; a < 3; ++a) d.n[a] = g.num_cells[a];
+    for (int w = 0; w < 3; ++w) d.inv_res_span[w] = 1.0 / (g.resolution * (double)w);
     return d;
 }
 

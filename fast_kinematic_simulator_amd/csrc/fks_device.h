@@ -33,6 +33,9 @@ struct GridDev {
     double inv[12]; /* inverse origin */
     double res, inv_res;
     int64_t n[3];
+    /* 1 / (res * d) for the gradient stencil widths d = 0, 1, 2 of EstimateDistance4d
+     * (the same correctly rounded division, done once on the host) */
+    double inv_res_span[3];
 };
 
 struct JointDev {

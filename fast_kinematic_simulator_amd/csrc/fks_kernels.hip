@@ -545,7 +545,7 @@ __device__ double estimate_distance(const SimArgs& A, const D4& p, bool* inb, ui
         int32_t lo[3] = {idx[0], idx[1], idx[2]}, hi[3] = {idx[0], idx[1], idx[2]};
         lo[a] = (idx[a] - 1 > 0) ? idx[a] - 1 : 0;
         hi[a] = ((int64_t)idx[a] + 1 < g.n[a] - 1) ? idx[a] + 1 : (int32_t)(g.n[a] - 1);
-        const double inv = 1.0 / (g.res * (double)(hi[a] - lo[a]));
+        const double inv = g.inv_res_span[hi[a] - lo[a]]; /* 1.0 / (g.res * (hi - lo)), hi - lo in {0, 1, 2} */
         const float diff = gp(A.sdf)[grid_linear(g, hi[0], hi[1], hi[2])] - gp(A.sdf)[grid_linear(g, lo[0], lo[1], lo[2])];
         grad[a] = (double)diff * inv;
     }
@@ -1308,9 +1308,11 @@ __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
             for (int i = 0; i < 3; ++i) {
                 const double* Ir = A.env_g.inv + 4 * i;
                 const double gh = (dabs(Ir[0]) * wh[0] + dabs(Ir[1]) * wh[1]) + dabs(Ir[2]) * wh[2];
+                /* conservative box: the margin (>= 1e-6 m) dwarfs the rounding of a
+                 * multiplication by 1/res instead of the exact pass's division */
                 const double margin = 1e-6 + 1e-9 * (dabs(gcv[i]) + gh);
-                const double l = (gcv[i] - gh - margin) / A.env_g.res;
-                const double h = (gcv[i] + gh + margin) / A.env_g.res;
+                const double l = (gcv[i] - gh - margin) * A.env_g.inv_res;
+                const double h = (gcv[i] + gh + margin) * A.env_g.inv_res;
                 if (!(l > -1e18 && l < 1e18 && h > -1e18 && h < 1e18)) bad = true;
                 lo[i] = __builtin_trunc(l);
                 hi[i] = __builtin_trunc(h);
