@@ -293,6 +293,7 @@ def main():
         print(json.dumps(line), flush=True)
     sim.close()
     if dist is not None:
+        dist.barrier()  # rank 0 ran the CPU baseline and the config-check line after the timed region
         dist.destroy_process_group()
 
 
