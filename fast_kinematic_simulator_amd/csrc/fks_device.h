@@ -105,7 +105,7 @@ struct RobotDev {
  * `total` doubles that follows. */
 constexpr int kWavesPerGroup = 4;
 struct LdsLayout {
-    uint32_t joints, ctrl, base, dofj, gbox, gpairs, shared_total;
+    uint32_t joints, ctrl, base, dofj, gbox, gpairs, rounds, shared_total;
     uint32_t rstate, noise, noise_err, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u,
         ustep, x, real, axis_w, orig_w, colsq, hcoef, box, misc, ints, total;
 };
@@ -131,6 +131,8 @@ inline
     l.gpairs = o; /* first kLdsPairs disallowed pairs, a | b << 16 */
     o += (uint32_t)kLdsPairs / 2;
     o = (o + 1u) & ~1u;
+    l.rounds = o; /* per 64-point round r < 64: (double)link, radius (RoundDev) */
+    o += 2u * (uint32_t)(NR < 1 ? 1 : (NR > 64 ? 64 : NR));
     l.shared_total = o;
     /* per wave */
     o = 0;

@@ -904,6 +904,15 @@ __device__ __forceinline__ double wave_min(double v) {
 constexpr double kInvalidRound = -1.0e308;
 enum { kSkipCheck = 1, kSkipCorrections = 2 };
 
+/* (link, radius) of round r < 64 from the workgroup's LDS copy of R.rounds */
+__device__ __forceinline__ RoundDev lds_round(const Sim& s, int r) {
+    RoundDev o;
+    o.link = (int32_t)s.shared[s.A->L.rounds + 2 * r];
+    o.npts = 0;
+    o.radius = s.shared[s.A->L.rounds + 2 * r + 1];
+    return o;
+}
+
 /* which rounds (bit r, r < 64) may skip the env check / the correction estimate at
  * transforms T; lane r evaluates round r */
 __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, int what) {
@@ -913,7 +922,7 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
     bool sk = false;
     const int ln = s.lane;
     if (ln < R.nrounds) {
-        const RoundDev rd = load_round(R.rounds, ln);
+        const RoundDev rd = lds_round(s, ln);
         const double* st = s.lds + A.L.rstate + kRoundState * ln;
         if (rd.link >= 0 && st[12] > kInvalidRound) {
             const double b = rigid_motion_bound(T + 12 * rd.link, st, rd.radius) * A.sdf_g.inv_res; /* cells */
@@ -942,7 +951,7 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
 __device__ __forceinline__ void round_update(Sim& s, int r, const double* T, double S, double G, double C) {
     const SimArgs& A = *s.A;
     if (!A.skip_enabled || r >= kWave || r >= A.R.nrounds) return;
-    const RoundDev rd = load_round(A.R.rounds, r);
+    const RoundDev rd = lds_round(s, r);
     if (rd.link < 0) return;
     const double smin = wave_min(S), gmin = wave_min(G), cmin = wave_min(C);
     double* st = s.lds + A.L.rstate + kRoundState * r;
@@ -980,7 +989,7 @@ __device__ double max_point_motion(Sim& s, const double* TA, const double* TB) {
     }
     double ub = 0.0;
     if (ln < nr) {
-        const RoundDev rd = load_round(R.rounds, ln);
+        const RoundDev rd = lds_round(s, ln);
         ub = (rd.link >= 0) ? rigid_motion_bound(TB + 12 * rd.link, TA + 12 * rd.link, rd.radius) : __builtin_huge_val();
     }
     const double top = wave_max_nonneg(ub);
@@ -2379,6 +2388,11 @@ __device__ __forceinline__ void setup_wave(const SimArgs* __restrict__ args, dou
             for (int k = t; k < R.npairs && k < kLdsPairs; k += nt)
                 lp[k] = (uint32_t)gp(R.pairs)[2 * k] | ((uint32_t)gp(R.pairs)[2 * k + 1] << 16);
         }
+        if (t < R.nrounds && t < kWave) {
+            const RoundDev rd = load_round(R.rounds, t);
+            shared[A.L.rounds + 2 * t] = (double)rd.link;
+            shared[A.L.rounds + 2 * t + 1] = rd.radius;
+        }
         __syncthreads();
     }
     s.A = args;
@@ -2584,6 +2598,11 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             uint32_t* lp = reinterpret_cast<uint32_t*>(shared + A.L.gpairs);
             for (int k = t; k < R.npairs && k < kLdsPairs; k += nt)
                 lp[k] = (uint32_t)gp(R.pairs)[2 * k] | ((uint32_t)gp(R.pairs)[2 * k + 1] << 16);
+        }
+        if (t < R.nrounds && t < kWave) {
+            const RoundDev rd = load_round(R.rounds, t);
+            shared[A.L.rounds + 2 * t] = (double)rd.link;
+            shared[A.L.rounds + 2 * t + 1] = rd.radius;
         }
         __syncthreads(); /* the only workgroup barrier: waves run independently afterwards */
     }
