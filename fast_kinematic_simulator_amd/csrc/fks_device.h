@@ -148,8 +148,20 @@ inline
     o += 12u * L;
     l.Ttmp = o;
     o += 12u * L;
-    l.jm = o;
-    o += 12u * (J > 0 ? J : 1);
+    /* one region, two lifetimes: the joint motion matrices live only inside fk(); the
+     * world joint frames (Jacobian), QR column norms / Householder coefficients and the
+     * self-collision boxes only between fk() calls */
+    {
+        const uint32_t motion = 12u * (uint32_t)(J > 0 ? J : 1);
+        const uint32_t others = 8u * (uint32_t)D + 6u * (uint32_t)(G > 0 ? G : 1);
+        l.jm = o;
+        l.axis_w = o;
+        l.orig_w = o + 3u * D;
+        l.colsq = o + 6u * D;
+        l.hcoef = o + 7u * D;
+        l.box = o + 8u * D;
+        o += (motion > others) ? motion : others;
+    }
     l.cfg = o;
     o += W;
     l.cfg_work = o;
@@ -172,16 +184,6 @@ inline
     o += D;
     l.real = o;
     o += D;
-    l.axis_w = o;
-    o += 3u * D;
-    l.orig_w = o;
-    o += 3u * D;
-    l.colsq = o;
-    o += D;
-    l.hcoef = o;
-    o += D;
-    l.box = o;
-    o += 6u * G;
     l.misc = o;
     o += 32;
     l.ints = o; /* int32 region: perm[64], transpositions[64], 16 spare words */
