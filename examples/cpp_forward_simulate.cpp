@@ -115,6 +115,11 @@ int main(int argc, char** argv) {
             for (const auto& c : rs.contact_resolver_steps) configs += c.contact_resolution_steps.size();
         std::printf("#trace %d %zu %zu %.17g %.17g %.17g %u %u\n", worst, trace.resolver_steps.size(), configs,
                     tr.result_config[0], tr.result_config[1], tr.result_config[2], tr.microsteps, tr.resolver_iterations);
+        /* host-side helpers of the interface */
+        const std::array<double, 4> p3 = sim->Get3dPointForConfig(robot, results[worst].result_config);
+        std::printf("#point %.17g %.17g %.17g\n", p3[0], p3[1], p3[2]);
+        const auto markers = sim->MakeControlInputDisplayRep(robot, starts[0], {0.1, -0.2, 0.3}, {{0.f, 1.f, 0.f, 1.f}}, 7, "u");
+        std::printf("#marker %s %zu\n", markers[0].type.c_str(), markers[0].points.size());
     } catch (const fks::SimulatorError& e) {
         std::fprintf(stderr, "%s\n", e.what());
         status = e.status() == FKS_ERR_NO_DEVICE ? 3 : 1;

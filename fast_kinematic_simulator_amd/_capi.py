@@ -26,6 +26,7 @@ STATUS_NAMES = {
 
 ROBOT_LINKED, ROBOT_SE2, ROBOT_SE3 = 0, 1, 2
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_CONTINUOUS, JOINT_PRISMATIC = 0, 1, 2, 4
+KIN_LINK_TRANSFORMS, KIN_POINTS, KIN_APPLY_CONTROL_INPUT = 0, 1, 2
 OK, ERR_INVALID_ARGUMENT, ERR_HIP, ERR_NO_ROBOT, ERR_OUT_OF_MEMORY, ERR_UNSUPPORTED, ERR_NO_DEVICE = 0, 1, 2, 3, 4, 5, 6
 
 NUM_PHASES = 16
@@ -232,6 +233,8 @@ PROTOTYPES = [
     ("fks_check_config_collision_device", c_int32,
      [c_void_p, c_void_p, c_uint64, c_double, c_void_p, c_void_p, c_void_p, c_int32]),
     ("fks_get_last_check_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
+    ("fks_kinematics", c_int32, [c_void_p, c_int32, POINTER(c_double), c_uint64, POINTER(c_double), POINTER(c_double)]),
+    ("fks_robot_sizes", c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     ("fks_set_call_index", c_int32, [c_void_p, c_uint64]),
     ("fks_get_call_index", c_uint64, [c_void_p]),
     ("fks_get_statistics", c_int32, [c_void_p, POINTER(Statistics)]),

@@ -34,6 +34,9 @@ extern "C" __global__ void fks_simulate_se3_traced(const fksd::SimArgs* args);
 extern "C" __global__ void fks_check_configs_linked(const fksd::SimArgs* args);
 extern "C" __global__ void fks_check_configs_se2(const fksd::SimArgs* args);
 extern "C" __global__ void fks_check_configs_se3(const fksd::SimArgs* args);
+extern "C" __global__ void fks_kinematics_linked(const fksd::SimArgs* args);
+extern "C" __global__ void fks_kinematics_se2(const fksd::SimArgs* args);
+extern "C" __global__ void fks_kinematics_se3(const fksd::SimArgs* args);
 extern "C" __global__ void fks_math_probe(const double* a, const double* b, double* out, uint64_t n);
 
 namespace {
@@ -1087,6 +1090,80 @@ fks_status fks_forward_simulate_traced(fks_context* ctx, const double* starts, u
     }
     release();
     return st;
+}
+
+fks_status fks_robot_sizes(const fks_context* ctx, int32_t* num_links, int32_t* num_points, int32_t* num_dofs,
+                           int32_t* config_width) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    if (!ctx->has_robot) return FKS_ERR_NO_ROBOT;
+    if (num_links) *num_links = ctx->R.L;
+    if (num_points) *num_points = ctx->R.P;
+    if (num_dofs) *num_dofs = ctx->R.D;
+    if (config_width) *config_width = ctx->R.W;
+    return FKS_OK;
+}
+
+/* FK / world points / clean control input of a batch (include/fks_capi.h) */
+fks_status fks_kinematics(fks_context* ctx, int32_t mode, const double* configs, uint64_t n, const double* inputs,
+                          double* out) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    if (!ctx->has_robot) return fail(ctx, FKS_ERR_NO_ROBOT, "fks_set_robot has not been called");
+    if (mode != FKS_KIN_LINK_TRANSFORMS && mode != FKS_KIN_POINTS && mode != FKS_KIN_APPLY_CONTROL_INPUT)
+        return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "unknown kinematics mode");
+    if (n > 0 && (!configs || !out || (mode == FKS_KIN_APPLY_CONTROL_INPUT && !inputs)))
+        return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "null host buffer");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    fks_status st = settle(ctx);
+    if (st != FKS_OK) return st;
+    if (n == 0) return FKS_OK;
+    const size_t W = (size_t)ctx->R.W, D = (size_t)ctx->R.D;
+    const size_t per_out = (mode == FKS_KIN_LINK_TRANSFORMS) ? 12 * (size_t)ctx->R.L
+                                                             : (mode == FKS_KIN_POINTS ? 3 * (size_t)ctx->R.P : W);
+    double *d_cfg = nullptr, *d_in = nullptr, *d_out = nullptr;
+    auto release = [&]() {
+        if (d_cfg) (void)hipFree(d_cfg);
+        if (d_in) (void)hipFree(d_in);
+        if (d_out) (void)hipFree(d_out);
+    };
+    hipError_t e = dev_upload(&d_cfg, configs, (size_t)n * W);
+    if (e == hipSuccess && mode == FKS_KIN_APPLY_CONTROL_INPUT) e = dev_upload(&d_in, inputs, (size_t)n * D);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_out, (size_t)n * per_out * sizeof(double));
+    if (e != hipSuccess) {
+        release();
+        return hip_fail(ctx, e, "kinematics buffers");
+    }
+    fksd::SimArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.sdf_g = ctx->sdf_g;
+    a.nrm_g = ctx->nrm_g;
+    a.env_g = ctx->env_g;
+    a.R = ctx->R;
+    a.S = ctx->params;
+    a.starts = d_cfg;
+    a.targets = d_in;
+    a.n = n;
+    a.scratch = ctx->d_scratch;
+    a.scratch_per_wave = ctx->scratch_per_wave;
+    a.row_cap = 3u * (uint32_t)ctx->R.P;
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds);
+    a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P);
+    a.kin_mode = mode;
+    a.kin_out = d_out;
+    *ctx->h_args = a;
+    e = hipMemcpy(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        const uint64_t groups_needed = (n + fksd::kWavesPerGroup - 1) / fksd::kWavesPerGroup;
+        const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? groups_needed : ctx->grid_groups);
+        sim_kernel_t k = (ctx->R.type == FKS_ROBOT_SE2) ? fks_kinematics_se2
+                                                        : (ctx->R.type == FKS_ROBOT_SE3 ? fks_kinematics_se3 : fks_kinematics_linked);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * fksd::kWavesPerGroup), ctx->lds_bytes, nullptr,
+                           static_cast<const fksd::SimArgs*>(ctx->d_args));
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, (size_t)n * per_out * sizeof(double), hipMemcpyDeviceToHost);
+    release();
+    if (e != hipSuccess) return hip_fail(ctx, e, "fks_kinematics");
+    return FKS_OK;
 }
 
 fks_status fks_set_call_index(fks_context* ctx, uint64_t call_index) {

@@ -276,6 +276,10 @@ struct SimArgs {
     uint32_t* tr_nsteps;
     uint32_t* tr_ncfg;
     uint32_t tr_step_cap, tr_cfg_cap;
+    /* fks_kinematics: FKS_KIN_* mode, per-configuration inputs (targets) and output */
+    int32_t kin_mode;
+    int32_t kin_pad;
+    double* kin_out;
 };
 
 enum {

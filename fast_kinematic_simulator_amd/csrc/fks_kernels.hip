@@ -2574,6 +2574,47 @@ __device__ __forceinline__ void check_configs(const SimArgs* __restrict__ args, 
     if (ln == 0 && bytes_total) atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes_total);
 }
 
+/* fks_kinematics (host-side helpers of the reference interface: GetLinkTransform for
+ * Get3dPointForConfig SPCS:776-786, the point positions of MakeConfigurationDisplayRep
+ * SPCS:634-688, the clean ApplyControlInput of MakeControlInputDisplayRep SPCS:719-774):
+ * one wave per configuration, SetPosition then FK / point transforms / clean input */
+template <int RT>
+__device__ __forceinline__ void kinematics(const SimArgs* __restrict__ args, double* lds_mem) {
+    Sim s;
+    setup_wave<RT>(args, lds_mem, s);
+    const SimArgs& A = *args;
+    const RobotDev& R = A.R;
+    const int ln = s.lane;
+    double* cfg = s.lds + A.L.cfg;
+    double* out_cfg = s.lds + A.L.cfg_tmp;
+    double* T = s.lds + A.L.Tcur;
+    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerGroup;
+    for (uint64_t c = (uint64_t)blockIdx.x * kWavesPerGroup + (threadIdx.x >> 6); c < A.n; c += stride) {
+        set_position<RT>(s, A.starts + c * (uint64_t)R.W, cfg);
+        if (A.kin_mode == FKS_KIN_APPLY_CONTROL_INPUT) {
+            double* in = s.lds + A.L.u;
+            if (ln < R.D) in[ln] = A.targets[c * (uint64_t)R.D + ln];
+            wsync();
+            apply_input<RT>(s, cfg, in, out_cfg, false, 0);
+            if (ln < R.W) A.kin_out[c * (uint64_t)R.W + ln] = out_cfg[ln];
+        } else {
+            fk<RT>(s, cfg, T);
+            if (A.kin_mode == FKS_KIN_LINK_TRANSFORMS) {
+                for (int e = ln; e < 12 * R.L; e += kWave) A.kin_out[c * 12ull * (uint64_t)R.L + e] = T[e];
+            } else {
+                for (int i = ln; i < R.P; i += kWave) {
+                    const D4 x = xform4(T + 12 * gp(R.point_link)[i], load_point(R, i));
+                    double* o = A.kin_out + (c * (uint64_t)R.P + (uint64_t)i) * 3ull;
+                    o[0] = x.x;
+                    o[1] = x.y;
+                    o[2] = x.z;
+                }
+            }
+        }
+        wsync();
+    }
+}
+
 template <int RT, bool TR>
 __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ args, double* lds_mem) {
     const SimArgs& A = *args;
@@ -2780,6 +2821,19 @@ extern "C" __global__ void FKS_KERNEL_ATTRS fks_check_configs_se2(const SimArgs*
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_check_configs_se3(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
     check_configs<FKS_ROBOT_SE3>(args, lds_mem);
+}
+
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_kinematics_linked(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    kinematics<FKS_ROBOT_LINKED>(args, lds_mem);
+}
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_kinematics_se2(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    kinematics<FKS_ROBOT_SE2>(args, lds_mem);
+}
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_kinematics_se3(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    kinematics<FKS_ROBOT_SE3>(args, lds_mem);
 }
 
 /* device self-test of the portable libm (fks_selftest_math) */

@@ -51,6 +51,7 @@ class SimulatorEnvironment:
         self.normal_entries = np.ascontiguousarray(normal_entries, dtype=np.float64)
         self.oob_value = float(oob_value)
         self.occupancy = occupancy
+        self.frame = "world"  # TaggedObjectCollisionMapGrid::GetFrame (SPCS:519)
 
     @property
     def resolution(self) -> float:

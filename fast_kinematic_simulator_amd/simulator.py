@@ -272,6 +272,108 @@ class HipParticleContactSimulator:
         _capi.check(self._lib.fks_get_last_check_counters(self._ctx, ctypes.byref(c)), self._ctx, "counters")
         return c.as_dict()
 
+    # ---- kinematics helpers of the interface (fks_kinematics) ----
+    def _kinematics(self, robot: RobotDescription, mode: int, configs, inputs=None) -> np.ndarray:
+        self.set_robot(robot)
+        W = robot.config_width
+        cfg = np.ascontiguousarray(np.asarray(configs, dtype=np.float64).reshape(-1, W))
+        n = cfg.shape[0]
+        links, points, dofs = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _capi.check(self._lib.fks_robot_sizes(self._ctx, ctypes.byref(links), ctypes.byref(points), ctypes.byref(dofs), None),
+                    self._ctx, "fks_robot_sizes")
+        shape = {_capi.KIN_LINK_TRANSFORMS: (n, links.value, 3, 4), _capi.KIN_POINTS: (n, points.value, 3),
+                 _capi.KIN_APPLY_CONTROL_INPUT: (n, W)}[mode]
+        out = np.zeros(shape, dtype=np.float64)
+        u = None
+        if mode == _capi.KIN_APPLY_CONTROL_INPUT:
+            u = np.ascontiguousarray(np.asarray(inputs, dtype=np.float64).reshape(n, dofs.value))
+        st = self._lib.fks_kinematics(self._ctx, mode, _capi.as_ptr(cfg, ctypes.c_double), n,
+                                      _capi.as_ptr(u, ctypes.c_double) if u is not None else None,
+                                      _capi.as_ptr(out, ctypes.c_double))
+        _capi.check(st, self._ctx, "fks_kinematics")
+        return out
+
+    def link_transforms(self, robot: RobotDescription, configs) -> np.ndarray:
+        """GetLinkTransform of every link after SetPosition: (n, links, 3, 4)."""
+        return self._kinematics(robot, _capi.KIN_LINK_TRANSFORMS, configs)
+
+    def world_points(self, robot: RobotDescription, configs) -> np.ndarray:
+        """Every link point in the world frame, geometry order: (n, points, 3)."""
+        return self._kinematics(robot, _capi.KIN_POINTS, configs)
+
+    def apply_control_input(self, robot: RobotDescription, configs, control_inputs) -> np.ndarray:
+        """SetPosition + clean ApplyControlInput (TNUVA:538-566): (n, W)."""
+        return self._kinematics(robot, _capi.KIN_APPLY_CONTROL_INPUT, configs, control_inputs)
+
+    def get_frame(self) -> str:
+        """GetFrame (SPCS:517-520)."""
+        return self.environment.frame
+
+    def get_resolution(self) -> float:
+        return float(self.environment.resolution)
+
+    def get_random_generator(self) -> np.random.Generator:
+        """GetRandomGenerator (SPCS:473-481) for the caller's own sampling.  The
+        simulation's actuation noise does not come from it: that is the counter RNG keyed
+        by (seed, call index, particle, step, microstep, dof), DESIGN.md §2.1."""
+        if getattr(self, "_host_rng", None) is None:
+            self._host_rng = np.random.default_rng(self.prng_seed)
+        return self._host_rng
+
+    def get_3d_point_for_config(self, immutable_robot: RobotDescription, config) -> np.ndarray:
+        """Get3dPointForConfig (SPCS:776-786): the origin of the last geometry's link."""
+        T = self.link_transforms(immutable_robot, [config])[0, immutable_robot.geometry_link[-1]]
+        return np.array([T[0, 3], T[1, 3], T[2, 3], 1.0])
+
+    def make_configuration_display_rep(self, immutable_robot: RobotDescription, configuration, color,
+                                       starting_index: int, config_marker_ns: str) -> List[dict]:
+        """MakeConfigurationDisplayRep for POINTS geometries (SPCS:634-688): one SPHERE_LIST
+        marker of every link point, black where the link-frame point is the zero vector."""
+        pts = self.world_points(immutable_robot, [configuration])[0]
+        res = self.get_resolution()
+        m = _marker(config_marker_ns, starting_index, "SPHERE_LIST", self.get_frame(), (res, res, res), color)
+        m["points"] = pts.tolist()
+        link_pts = immutable_robot.points
+        black = [0.0, 0.0, 0.0, 1.0]
+        m["colors"] = [black if float(np.linalg.norm(p)) == 0.0 else list(color) for p in link_pts]
+        return [m]
+
+    def make_control_input_display_rep(self, immutable_robot: RobotDescription, configuration, control_input, color,
+                                       starting_index: int, control_input_marker_ns: str) -> List[dict]:
+        """MakeControlInputDisplayRep (SPCS:719-774): a LINE_LIST from every point at
+        `configuration` to the same point after the clean control input."""
+        after = self.apply_control_input(immutable_robot, [configuration], [control_input])
+        pts = self.world_points(immutable_robot, np.concatenate([np.asarray(configuration, dtype=np.float64).reshape(1, -1),
+                                                                 after], axis=0))
+        res = self.get_resolution() * 0.5
+        m = _marker(control_input_marker_ns, starting_index, "LINE_LIST", self.get_frame(), (res, res, res), color)
+        m["points"] = np.stack([pts[0], pts[1]], axis=1).reshape(-1, 3).tolist()
+        m["colors"] = [list(color)] * (2 * pts.shape[1])
+        return [m]
+
+    def make_environment_display_rep(self) -> List[dict]:
+        """MakeEnvironmentDisplayRep (SPCS:559-586), reduced to what this repository holds:
+        the filled cells of the collision grid ("sim_environment") and the SDF cells
+        colored by sign ("sim_environment_sdf").  sdf_tools' connected-component and
+        convex-segment exports have no counterpart here."""
+        env = self.environment
+        g = env.geometry
+        n = tuple(int(v) for v in g.num_cells)
+        o = np.asarray(g.origin, dtype=np.float64).reshape(3, 4)
+        idx = np.stack(np.unravel_index(np.arange(int(np.prod(n))), n), axis=1).astype(np.float64)
+        centers = (idx + 0.5) * g.resolution @ o[:, :3].T + o[:, 3]
+        res = float(g.resolution)
+        markers = []
+        occ = env.occupancy if env.occupancy is not None else (env.sdf < 0).astype(np.uint8)
+        m = _marker("sim_environment", 1, "CUBE_LIST", self.get_frame(), (res, res, res), [1.0, 0.0, 0.0, 1.0])
+        m["points"] = centers[occ.astype(bool)].tolist()
+        markers.append(m)
+        s = _marker("sim_environment_sdf", 1, "CUBE_LIST", self.get_frame(), (res, res, res), [1.0, 1.0, 1.0, 1.0])
+        s["points"] = centers.tolist()
+        s["colors"] = [[1.0, 0.0, 0.0, 1.0] if v < 0 else [0.0, 0.0, 1.0, 1.0] for v in env.sdf]
+        markers.append(s)
+        return markers
+
     def forward_simulate_device(self, robot: RobotDescription, d_starts, n: int, d_targets, num_targets: int,
                                 first_particle_id: int, allow_contacts: bool, d_out_positions, d_out_collided=0,
                                 d_out_microsteps=0, d_out_resolver_iterations=0, d_out_error_flags=0, stream=0,
@@ -285,6 +387,13 @@ class HipParticleContactSimulator:
             ctypes.c_void_p(d_out_microsteps or None), ctypes.c_void_p(d_out_resolver_iterations or None),
             ctypes.c_void_p(d_out_error_flags or None), ctypes.c_void_p(stream or None), 1 if synchronize else 0)
         _capi.check(st, self._ctx, "fks_forward_simulate_device")
+
+
+def _marker(ns, marker_id, marker_type, frame, scale, color):
+    """A visualization_msgs::Marker as a plain dict (ROS is not part of this repository)."""
+    return {"ns": ns, "id": int(marker_id), "type": marker_type, "action": "ADD", "frame_id": frame,
+            "frame_locked": False, "scale": [float(v) for v in scale], "color": list(color),
+            "pose": {"position": [0.0, 0.0, 0.0], "orientation": [0.0, 0.0, 0.0, 1.0]}, "points": None, "colors": None}
 
 
 def _make(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level, device=0):

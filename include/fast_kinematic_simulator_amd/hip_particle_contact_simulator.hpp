@@ -19,7 +19,10 @@
 #define FAST_KINEMATIC_SIMULATOR_AMD_HIP_PARTICLE_CONTACT_SIMULATOR_HPP
 
 #include <algorithm>
+#include <array>
 #include <cstdint>
+#include <limits>
+#include <random>
 #include <functional>
 #include <memory>
 #include <stdexcept>
@@ -78,6 +81,19 @@ struct ForwardSimulationResolverTrace {
 struct ForwardSimulationStepTrace {
     std::vector<ForwardSimulationResolverTrace> resolver_steps;
     bool truncated = false; /* records beyond the trace capacity were dropped */
+};
+
+/* visualization_msgs::Marker reduced to plain data (ROS is not part of this
+ * repository): what the reference's display helpers fill in */
+struct Marker {
+    std::string ns;
+    int32_t id = 0;
+    std::string type; /* "SPHERE_LIST", "LINE_LIST" */
+    std::string frame_id;
+    std::array<double, 3> scale{{0.0, 0.0, 0.0}};
+    std::array<float, 4> color{{0.0f, 0.0f, 0.0f, 1.0f}};
+    std::vector<std::array<double, 3>> points;
+    std::vector<std::array<float, 4>> colors;
 };
 
 /* fast_kinematic_simulator::GetDefaultSolverParameters (FKS.hpp:13-16) */
@@ -157,6 +173,97 @@ class HipParticleContactSimulator {
               nullptr, "fks_create");
         ctx_.reset(ctx);
         forward_steps_ = (uint32_t)std::max(1.0, solver_config.forward_simulation_time * simulation_controller_frequency);
+        resolution_ = environment.collision_map.resolution;
+        /* ResetGenerators (SPCS:457-471): the first per-thread generator */
+        std::mt19937_64 prng(prng_seed);
+        std::uniform_int_distribution<uint64_t> seed_dist(0, std::numeric_limits<uint64_t>::max());
+        rng_ = std::mt19937_64(seed_dist(prng));
+    }
+
+    /* GetFrame (SPCS:517-520) */
+    std::string GetFrame() const { return frame_; }
+    void SetFrame(const std::string& frame) { frame_ = frame; }
+    /* GetRandomGenerator (SPCS:473-481), for the caller's own sampling; the simulation's
+     * noise is the counter RNG keyed by (seed, call, particle, step, microstep, dof) */
+    std::mt19937_64& GetRandomGenerator() { return rng_; }
+
+    /* fks_kinematics over a batch: FKS_KIN_LINK_TRANSFORMS -> links x 12 per config,
+     * FKS_KIN_POINTS -> points x 3, FKS_KIN_APPLY_CONTROL_INPUT -> config width */
+    std::vector<double> Kinematics(const RobotDescription& robot, int32_t mode, const std::vector<Configuration>& configs,
+                                   const std::vector<std::vector<double>>& inputs = {}) {
+        SetRobot(robot);
+        int32_t links = 0, points = 0, dofs = 0, width = 0;
+        check(fks_robot_sizes(ctx_.get(), &links, &points, &dofs, &width), ctx_.get(), "fks_robot_sizes");
+        const size_t n = configs.size(), W = (size_t)width;
+        std::vector<double> c(n * W), u;
+        for (size_t i = 0; i < n; ++i) {
+            if (configs[i].size() != W) throw std::invalid_argument("configuration has the wrong width");
+            std::copy(configs[i].begin(), configs[i].end(), c.begin() + i * W);
+        }
+        if (mode == FKS_KIN_APPLY_CONTROL_INPUT) {
+            if (inputs.size() != n) throw std::invalid_argument("one control input per configuration");
+            for (const auto& in : inputs) {
+                if (in.size() != (size_t)dofs) throw std::invalid_argument("control input has the wrong width");
+                u.insert(u.end(), in.begin(), in.end());
+            }
+        }
+        const size_t per = mode == FKS_KIN_LINK_TRANSFORMS ? 12u * (size_t)links : (mode == FKS_KIN_POINTS ? 3u * (size_t)points : W);
+        std::vector<double> out(n * per);
+        check(fks_kinematics(ctx_.get(), mode, c.data(), n, u.empty() ? nullptr : u.data(), out.data()), ctx_.get(),
+              "fks_kinematics");
+        return out;
+    }
+
+    /* Get3dPointForConfig (SPCS:776-786): origin of the last geometry's link, w = 1 */
+    std::array<double, 4> Get3dPointForConfig(const RobotDescription& immutable_robot, const Configuration& config) {
+        const std::vector<double> T = Kinematics(immutable_robot, FKS_KIN_LINK_TRANSFORMS, {config});
+        const size_t l = (size_t)immutable_robot.geometry_link.back();
+        return {{T[12 * l + 3], T[12 * l + 7], T[12 * l + 11], 1.0}};
+    }
+
+    /* MakeConfigurationDisplayRep for POINTS geometries (SPCS:634-688) */
+    std::vector<Marker> MakeConfigurationDisplayRep(const RobotDescription& immutable_robot, const Configuration& configuration,
+                                                    const std::array<float, 4>& color, int32_t starting_index,
+                                                    const std::string& config_marker_ns) {
+        const std::vector<double> pts = Kinematics(immutable_robot, FKS_KIN_POINTS, {configuration});
+        Marker m;
+        m.ns = config_marker_ns;
+        m.id = starting_index;
+        m.type = "SPHERE_LIST";
+        m.frame_id = frame_;
+        m.scale = {{resolution_, resolution_, resolution_}};
+        m.color = color;
+        for (size_t i = 0; i < pts.size() / 3; ++i) {
+            m.points.push_back({{pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]}});
+            const double* p = immutable_robot.points.data() + 4 * i;
+            const bool zero = (p[0] * p[0] + p[1] * p[1] + p[2] * p[2] + p[3] * p[3]) == 0.0;
+            m.colors.push_back(zero ? std::array<float, 4>{{0.0f, 0.0f, 0.0f, 1.0f}} : color);
+        }
+        return {m};
+    }
+
+    /* MakeControlInputDisplayRep (SPCS:719-774): each point before and after the clean input */
+    std::vector<Marker> MakeControlInputDisplayRep(const RobotDescription& immutable_robot, const Configuration& configuration,
+                                                   const std::vector<double>& control_input, const std::array<float, 4>& color,
+                                                   int32_t starting_index, const std::string& control_input_marker_ns) {
+        const std::vector<double> after = Kinematics(immutable_robot, FKS_KIN_APPLY_CONTROL_INPUT, {configuration}, {control_input});
+        const std::vector<double> pts =
+            Kinematics(immutable_robot, FKS_KIN_POINTS, {configuration, Configuration(after.begin(), after.end())});
+        const size_t P = pts.size() / 6;
+        Marker m;
+        m.ns = control_input_marker_ns;
+        m.id = starting_index;
+        m.type = "LINE_LIST";
+        m.frame_id = frame_;
+        m.scale = {{resolution_ * 0.5, resolution_ * 0.5, resolution_ * 0.5}};
+        m.color = color;
+        for (size_t i = 0; i < P; ++i) {
+            m.points.push_back({{pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]}});
+            m.points.push_back({{pts[3 * (P + i)], pts[3 * (P + i) + 1], pts[3 * (P + i) + 2]}});
+            m.colors.push_back(color);
+            m.colors.push_back(color);
+        }
+        return {m};
     }
 
     /* SPCS:446-455 */
@@ -288,6 +395,9 @@ class HipParticleContactSimulator {
     std::unique_ptr<fks_context, Destroy> ctx_;
     const RobotDescription* robot_ = nullptr;
     uint32_t forward_steps_ = 1; /* controller steps per simulation (SPCS:856): the trace's step capacity */
+    double resolution_ = 0.0;
+    std::string frame_ = "world";
+    std::mt19937_64 rng_;
 
     void SetRobot(const RobotDescription& robot) {
         if (robot_ == &robot) return;

@@ -324,6 +324,25 @@ fks_status fks_forward_simulate_traced(fks_context* ctx, const double* starts, u
                                        uint32_t* out_resolver_iterations, uint32_t* out_error_flags,
                                        const fks_trace* trace);
 
+/* Kinematics of a batch of configurations (host buffers), the pieces the reference's
+ * host-side helpers build on, computed with the simulation kernels' own FK:
+ *   FKS_KIN_LINK_TRANSFORMS     out: n x num_links x 12 (3x4 row-major link transforms
+ *                               after SetPosition; GetLinkTransform, used by
+ *                               Get3dPointForConfig SPCS:776-786)
+ *   FKS_KIN_POINTS              out: n x num_points x 3 (link points in the world frame,
+ *                               geometry order; MakeConfigurationDisplayRep SPCS:634-688)
+ *   FKS_KIN_APPLY_CONTROL_INPUT inputs: n x num_dofs; out: n x config width (the clean
+ *                               ApplyControlInput of MakeControlInputDisplayRep,
+ *                               SPCS:719-774, TNUVA:538-566) */
+#define FKS_KIN_LINK_TRANSFORMS 0
+#define FKS_KIN_POINTS 1
+#define FKS_KIN_APPLY_CONTROL_INPUT 2
+fks_status fks_kinematics(fks_context* ctx, int32_t mode, const double* configs, uint64_t n, const double* inputs,
+                          double* out);
+/* sizes of the robot set with fks_set_robot (any pointer may be NULL) */
+fks_status fks_robot_sizes(const fks_context* ctx, int32_t* num_links, int32_t* num_points, int32_t* num_dofs,
+                           int32_t* config_width);
+
 /* Each forward/reverse call consumes one RNG "call index" (the reference's
  * per-thread std::mt19937_64 streams advance across calls, SPCS:850).  Ranks
  * that shard one logical call must use the same index: set it explicitly. */

@@ -63,6 +63,8 @@ def lib():
                                                POINTER(c_uint8), POINTER(ctypes.c_float)]
         L.oracle_link_transforms.restype = c_int32
         L.oracle_link_transforms.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), POINTER(c_double)]
+        L.oracle_apply_control_input.restype = c_int32
+        L.oracle_apply_control_input.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), POINTER(c_double), POINTER(c_double)]
         L.oracle_point_jacobian.restype = c_int32
         L.oracle_point_jacobian.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), c_int32, POINTER(c_double), POINTER(c_double)]
         L.oracle_se3_exp.restype = None
@@ -216,6 +218,16 @@ def link_transforms(robot, config):
     cfg = np.ascontiguousarray(config, dtype=np.float64)
     out = np.zeros((len(robot.geometry_points), 12))
     lib().oracle_link_transforms(ctypes.byref(desc), _p(cfg, c_double), _p(out, c_double))
+    return out
+
+
+def apply_control_input(robot, config, control_input):
+    """SetPosition + clean ApplyControlInput (TNUVA:538-566) on the CPU."""
+    desc, keep = robot.to_c()
+    cfg = np.ascontiguousarray(config, dtype=np.float64)
+    u = np.ascontiguousarray(control_input, dtype=np.float64)
+    out = np.zeros(robot.config_width)
+    lib().oracle_apply_control_input(ctypes.byref(desc), _p(cfg, c_double), _p(u, c_double), _p(out, c_double))
     return out
 
 

@@ -1164,6 +1164,19 @@ int oracle_link_transforms(const fks_robot_desc* robot_desc, const double* confi
     return 0;
 }
 
+/* SetPosition(config) then the clean ApplyControlInput(input) (TNUVA:538-566, SE2
+ * 152-177, SE3 348-382): the configuration MakeControlInputDisplayRep draws to */
+int oracle_apply_control_input(const fks_robot_desc* robot_desc, const double* config, const double* input, double* out) {
+    std::unique_ptr<RobotModel> robot(make_robot(*robot_desc));
+    if (!robot) return 1;
+    const size_t W = config_width(*robot_desc);
+    robot->SetPosition(Config(config, config + W));
+    robot->ApplyControlInput(std::vector<double>(input, input + robot->NumDofs()));
+    const Config& q = robot->GetPosition();
+    std::memcpy(out, q.data(), W * sizeof(double));
+    return 0;
+}
+
 /* point Jacobian (3 x D row-major) of point p (4 doubles) on geometry g */
 int oracle_point_jacobian(const fks_robot_desc* robot_desc, const double* config, int32_t geometry, const double* p, double* out) {
     std::unique_ptr<RobotModel> robot(make_robot(*robot_desc));

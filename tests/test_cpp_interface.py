@@ -74,4 +74,9 @@ def test_cpp_interface_matches_python_mirror():
     assert (int(t[1]), int(t[2])) == (len(trace.resolver_steps), nconf)
     assert np.array_equal(np.array([float(v) for v in t[3:6]]), res.result_config)
     assert (int(t[6]), int(t[7])) == (res.microsteps, res.resolver_iterations)
+    # Get3dPointForConfig and MakeControlInputDisplayRep through the C++ header
+    p3 = [float(v) for v in [l.split()[1:] for l in p.stdout.splitlines() if l.startswith("#point")][0]]
+    assert np.array_equal(np.array(p3), sim.get_3d_point_for_config(robot, r["positions"][worst])[:3])
+    mk = [l.split()[1:] for l in p.stdout.splitlines() if l.startswith("#marker")][0]
+    assert mk == ["LINE_LIST", str(2 * robot.num_points)]
     sim.close()
