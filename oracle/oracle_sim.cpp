@@ -736,9 +736,6 @@ class Simulator {
                 const V4 prev_loc = xform4(Tp, lp);
                 const V4 cur_loc = xform4(Tc, lp);
                 const std::pair<double, bool> sdf_check = sdf_.EstimateDistance4d(cur_loc, &pc.sdf_bytes);
-                if (std::getenv("FKS_ORACLE_TRACE2") && sdf_check.first < resolution_distance_threshold_ && sdf_check.second)
-                    std::fprintf(stderr, "   pt g%zu i%zu cur (%.4f %.4f %.4f) prev (%.4f %.4f %.4f) est %.4f\n", link_idx, point_idx,
-                                 cur_loc.x, cur_loc.y, cur_loc.z, prev_loc.x, prev_loc.y, prev_loc.z, sdf_check.first);
                 if (sdf_check.first < resolution_distance_threshold_ && sdf_check.second) {
                     const V4 motion{cur_loc.x - prev_loc.x, cur_loc.y - prev_loc.y, cur_loc.z - prev_loc.z, cur_loc.w - prev_loc.w};
                     const V4 normed_motion = safe_normal4(motion);
@@ -830,14 +827,6 @@ class Simulator {
                     pc.lsq_rows += rows;
                     if (pc.error_flags) return ResolveResult{previous_configuration, collided, false, true};
                     const std::vector<double> raw_correction_step = colpiv_qr_solve(J, rows, D, b);
-                    if (std::getenv("FKS_ORACLE_TRACE")) {
-                        double bn = 0, xn = 0;
-                        for (double v : b) bn += v * v;
-                        for (double v : raw_correction_step) xn += v * v;
-                        std::fprintf(stderr, "step %u micro %u iter %u rows %zu |b| %.3e |x| %.3e self %zu scale %.4f\n", rng.step,
-                                     micro_step, resolver_iterations, rows, std::sqrt(bn), std::sqrt(xn), self_collision_map.size(),
-                                     correction_step_scaling);
-                    }
                     const double correction_step_motion_estimate = EstimateMaxControlInputWorkspaceMotion(robot, raw_correction_step);
                     const double allowed_resolve_distance = allowed_microstep_distance;
                     const double step_fraction = fks_math::dmax(correction_step_motion_estimate / allowed_resolve_distance, 1.0);
