@@ -241,6 +241,14 @@ def main():
             cpu = cpu_baseline(cwl, sample, threads)
             log(f"cpu baseline {cpu['value']:.0f} {UNIT} in {time.perf_counter() - t0:.1f}s")
         value = all_micro / elapsed
+        # the host-buffer entry (fks_forward_simulate: starts/targets over PCIe, outcomes
+        # back) on the same batch: reported beside `value`, never as it
+        sim.set_call_index(0)
+        t0 = time.perf_counter()
+        hr = sim.forward_simulate_arrays(wl.robot, wl.starts[lo:lo + n_local], wl.targets, True)
+        host_s = time.perf_counter() - t0
+        pcie = {"value": float(np.sum(hr["microsteps"], dtype=np.int64)) / host_s, "unit": UNIT, "ms": host_s * 1e3,
+                "note": "one fks_forward_simulate call with host buffers (H2D starts/targets, kernel, D2H outcomes), rank 0"}
         cc = None
         if not args.no_config_check and args.workload == "cfg3":
             cc = config_check_bench(sim, wl, dev, with_cpu=not args.no_cpu_baseline)
@@ -284,6 +292,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "config_check": cc,
+            "pcie_inclusive": pcie,
             # share of wave time per phase of the hot path (s_memtime cycle sums, rank 0)
             # (only in profiling builds of the library: -DFKS_PHASE_TIMERS=1, see tools/variant_bench.py)
             "kernel_phases": ({k: (v if k in PHASE_COUNTS else round(v / max(1, phases["particle"]), 4))
