@@ -1,0 +1,37 @@
+"""bench.py keeps the driver's contract: one JSON line with the BASELINE.json metric,
+whole-job value, roofline and cpu_baseline objects (GPU: a small run end to end)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_cli_parses():
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=120)
+    assert p.returncode == 0 and "--workload" in p.stdout and "--gpus" in p.stdout
+
+
+@pytest.mark.gpu
+def test_bench_json_line():
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        metric = json.load(f)["metric"]
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--particles", "2048", "--steps", "1", "--warmup", "1",
+                        "--cpu-sample", "16", "--no-config-check"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True, timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["metric"] == metric and d["n_gpus"] == 1 and d["steps"] == 1 and d["warmup"] == 1
+    assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak" and d["vs_baseline"] is None
+    assert d["dtype"] == "f64" and "workload" in d["config"]
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    c = d["cpu_baseline"]
+    assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+    assert d["pcie_inclusive"]["value"] > 0
