@@ -5,7 +5,8 @@ ResolveForwardSimulation, reference simple_particle_contact_simulator.hpp) runs
 as hand-written HIP kernels for gfx950 behind the C-ABI in include/fks_capi.h.
 """
 from ._capi import FksError, lib
-from .environment import ObstacleConfig, SimulatorEnvironment, build_complete_environment
+from .environment import (DeviceEnvironment, ObstacleConfig, SimulatorEnvironment, build_complete_environment,
+                          build_device_environment)
 from .robots import (ControllerConfig, Joint, RobotDescription, SampledActuatorModel, make_linked_robot,
                      make_sampled_actuator_model, make_se2_robot, make_se3_robot, se3_pose, transform34)
 from .simulator import (HipParticleContactSimulator, SimulationResult, SimulatorSolverParameters, get_default_solver_parameters,

@@ -249,6 +249,12 @@ PROTOTYPES = [
     ("fks_env_build", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), POINTER(c_void_p)]),
     ("fks_env_build_gpu", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), c_int32,
                                     POINTER(c_void_p), POINTER(EnvBuildStats)]),
+    ("fks_env_build_device", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), c_int32,
+                                       POINTER(c_void_p), POINTER(EnvBuildStats)]),
+    ("fks_device_env_download", c_int32, [c_void_p, POINTER(c_void_p)]),
+    ("fks_device_env_geometry", c_int32, [c_void_p, POINTER(GridGeometry)]),
+    ("fks_device_env_free", None, [c_void_p]),
+    ("fks_create_from_device_env", c_int32, [c_void_p, POINTER(SolverParams), c_double, c_uint64, c_int32, POINTER(c_void_p)]),
     ("fks_env_view", c_int32, [c_void_p, POINTER(Environment)]),
     ("fks_env_occupancy", c_int32, [c_void_p, POINTER(c_uint8), c_uint64]),
     ("fks_env_free", None, [c_void_p]),

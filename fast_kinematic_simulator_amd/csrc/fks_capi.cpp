@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "fks_capi.h"
+#include "fks_env_internal.h"
 #include "fks_device.h"
 #include "fks_portable_math.h"
 
@@ -303,12 +304,20 @@ fks_status fks_default_solver_params(fks_solver_params* out) {
     return FKS_OK;
 }
 
-fks_status fks_create(const fks_environment* env, const fks_solver_params* params, double simulation_controller_frequency,
-                      uint64_t prng_seed, int32_t debug_level, int32_t device, fks_context** out_ctx) {
+/* fks_create / fks_create_from_device_env: the environment comes either from host
+ * arrays (henv) or from a device-resident GPU build (denv) */
+static fks_status create_impl(const fks_environment* henv, const fks_device_env* denv, const fks_solver_params* params,
+                              double simulation_controller_frequency, uint64_t prng_seed, int32_t debug_level, int32_t device,
+                              fks_context** out_ctx) {
     if (!out_ctx) return FKS_ERR_INVALID_ARGUMENT;
     *out_ctx = nullptr;
-    if (!env || !params || !env->sdf_values) return FKS_ERR_INVALID_ARGUMENT;
-    if (!valid_grid(env->sdf) || !valid_grid(env->collision_map) || !valid_grid(env->normals)) return FKS_ERR_INVALID_ARGUMENT;
+    if (!params || (!henv && !denv)) return FKS_ERR_INVALID_ARGUMENT;
+    if (henv) {
+        if (!henv->sdf_values) return FKS_ERR_INVALID_ARGUMENT;
+        if (!valid_grid(henv->sdf) || !valid_grid(henv->collision_map) || !valid_grid(henv->normals)) return FKS_ERR_INVALID_ARGUMENT;
+    } else if (!valid_grid(denv->geometry) || !denv->sdf || !denv->offsets) {
+        return FKS_ERR_INVALID_ARGUMENT;
+    }
     if (!(simulation_controller_frequency != 0.0) || !std::isfinite(simulation_controller_frequency)) return FKS_ERR_INVALID_ARGUMENT;
     if (params->resolve_correction_step_scaling_decay_iterations == 0) return FKS_ERR_INVALID_ARGUMENT;
     int count = 0;
@@ -332,28 +341,54 @@ fks_status fks_create(const fks_environment* env, const fks_solver_params* param
     };
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return bail(e, "hipSetDevice");
-    ctx->sdf_g = make_grid(env->sdf);
-    ctx->nrm_g = make_grid(env->normals);
-    ctx->env_g = make_grid(env->collision_map);
-    ctx->oob = env->sdf_oob_value;
-    const size_t cells = (size_t)env->sdf.num_cells[0] * (size_t)env->sdf.num_cells[1] * (size_t)env->sdf.num_cells[2];
-    if ((e = dev_upload(&ctx->d_sdf, env->sdf_values, cells)) != hipSuccess) return bail(e, "sdf upload");
-    {
-        double lp = 0.0, cm = 0.0;
-        if (analyze_sdf(env->sdf_values, env->sdf.num_cells[0], env->sdf.num_cells[1], env->sdf.num_cells[2],
-                        env->sdf.resolution, &lp, &cm)) {
-            ctx->skip_enabled = 1;
-            ctx->skip_lplus = lp * (1.0 + 1e-6) + 1e-6;
-            ctx->skip_cmax = cm * (1.0 + 1e-6) + 1e-6;
+    double lp = 0.0, cm = 0.0;
+    bool analyzed = false;
+    if (henv) {
+        ctx->sdf_g = make_grid(henv->sdf);
+        ctx->nrm_g = make_grid(henv->normals);
+        ctx->env_g = make_grid(henv->collision_map);
+        ctx->oob = henv->sdf_oob_value;
+        const size_t cells = (size_t)henv->sdf.num_cells[0] * (size_t)henv->sdf.num_cells[1] * (size_t)henv->sdf.num_cells[2];
+        if ((e = dev_upload(&ctx->d_sdf, henv->sdf_values, cells)) != hipSuccess) return bail(e, "sdf upload");
+        analyzed = analyze_sdf(henv->sdf_values, henv->sdf.num_cells[0], henv->sdf.num_cells[1], henv->sdf.num_cells[2],
+                               henv->sdf.resolution, &lp, &cm);
+        if (henv->normal_offsets && henv->normal_entries) {
+            const size_t ncells =
+                (size_t)henv->normals.num_cells[0] * (size_t)henv->normals.num_cells[1] * (size_t)henv->normals.num_cells[2];
+            const size_t entries = henv->normal_offsets[ncells];
+            if ((e = dev_upload(&ctx->d_noff, henv->normal_offsets, ncells + 1)) != hipSuccess)
+                return bail(e, "normal offsets upload");
+            if (entries > 0 && (e = dev_upload(&ctx->d_nent, henv->normal_entries, 6 * entries)) != hipSuccess)
+                return bail(e, "normal entries upload");
+            ctx->has_normals = 1;
         }
-    }
-    if (env->normal_offsets && env->normal_entries) {
-        const size_t ncells = (size_t)env->normals.num_cells[0] * (size_t)env->normals.num_cells[1] * (size_t)env->normals.num_cells[2];
-        const size_t entries = env->normal_offsets[ncells];
-        if ((e = dev_upload(&ctx->d_noff, env->normal_offsets, ncells + 1)) != hipSuccess) return bail(e, "normal offsets upload");
-        if (entries > 0 && (e = dev_upload(&ctx->d_nent, env->normal_entries, 6 * entries)) != hipSuccess)
-            return bail(e, "normal entries upload");
+    } else {
+        /* the GPU build's grids coincide (SEB.cpp builds all three on one grid); +inf out of bounds */
+        ctx->sdf_g = make_grid(denv->geometry);
+        ctx->nrm_g = ctx->sdf_g;
+        ctx->env_g = ctx->sdf_g;
+        ctx->oob = std::numeric_limits<float>::infinity();
+        const size_t cells = (size_t)denv->cells;
+        if ((e = hipMalloc((void**)&ctx->d_sdf, cells * sizeof(float))) != hipSuccess) return bail(e, "sdf");
+        if ((e = hipMemcpy(ctx->d_sdf, denv->sdf, cells * sizeof(float), hipMemcpyDeviceToDevice)) != hipSuccess)
+            return bail(e, "sdf copy");
+        analyzed = fks_env::analyze_sdf_device(ctx->d_sdf, denv->geometry.num_cells[0], denv->geometry.num_cells[1],
+                                               denv->geometry.num_cells[2], denv->geometry.resolution, &lp, &cm);
+        if ((e = hipMalloc((void**)&ctx->d_noff, (cells + 1) * sizeof(uint32_t))) != hipSuccess) return bail(e, "offsets");
+        if ((e = hipMemcpy(ctx->d_noff, denv->offsets, (cells + 1) * sizeof(uint32_t), hipMemcpyDeviceToDevice)) != hipSuccess)
+            return bail(e, "offsets copy");
+        if (denv->num_entries > 0) {
+            const size_t bytes = 6 * (size_t)denv->num_entries * sizeof(double);
+            if ((e = hipMalloc((void**)&ctx->d_nent, bytes)) != hipSuccess) return bail(e, "entries");
+            if ((e = hipMemcpy(ctx->d_nent, denv->entries, bytes, hipMemcpyDeviceToDevice)) != hipSuccess)
+                return bail(e, "entries copy");
+        }
         ctx->has_normals = 1;
+    }
+    if (analyzed) {
+        ctx->skip_enabled = 1;
+        ctx->skip_lplus = lp * (1.0 + 1e-6) + 1e-6;
+        ctx->skip_cmax = cm * (1.0 + 1e-6) + 1e-6;
     }
     if ((e = hipMalloc((void**)&ctx->d_counters, fksd::kCounterWords * sizeof(unsigned long long))) != hipSuccess)
         return bail(e, "counters");
@@ -366,6 +401,19 @@ fks_status fks_create(const fks_environment* env, const fks_solver_params* param
     (void)same_geometry;
     *out_ctx = ctx;
     return FKS_OK;
+}
+
+fks_status fks_create(const fks_environment* env, const fks_solver_params* params, double simulation_controller_frequency,
+                      uint64_t prng_seed, int32_t debug_level, int32_t device, fks_context** out_ctx) {
+    if (!env) return FKS_ERR_INVALID_ARGUMENT;
+    return create_impl(env, nullptr, params, simulation_controller_frequency, prng_seed, debug_level, device, out_ctx);
+}
+
+fks_status fks_create_from_device_env(const fks_device_env* env, const fks_solver_params* params,
+                                      double simulation_controller_frequency, uint64_t prng_seed, int32_t debug_level,
+                                      fks_context** out_ctx) {
+    if (!env) return FKS_ERR_INVALID_ARGUMENT;
+    return create_impl(nullptr, env, params, simulation_controller_frequency, prng_seed, debug_level, env->device, out_ctx);
 }
 
 void fks_destroy(fks_context* ctx) {

@@ -368,6 +368,11 @@ struct DeviceBuffers {
     ~DeviceBuffers() {
         for (void* p : ptrs) (void)hipFree(p);
     }
+    /* hand a buffer over to the caller: it is no longer freed here */
+    void keep(void* p) {
+        for (void*& q : ptrs)
+            if (q == p) q = nullptr;
+    }
     template <typename T>
     hipError_t alloc(T** p, uint64_t count) {
         *p = nullptr;
@@ -388,7 +393,77 @@ fks_status to_status(hipError_t e) {
     return FKS_ERR_HIP;
 }
 
+/* the host's analyze_sdf (fks_capi.cpp) per cell: lplus = max |a - b| / res over axis
+ * neighbours both positive, cmax = max positive value / res next to a non-positive
+ * one; keys are the doubles' bits (all values >= 0, so bit order is value order) */
+__global__ void env_analyze(const float* __restrict__ sdf, int64_t nx, int64_t ny, int64_t nz, double inv,
+                            unsigned long long* out /* lplus bits, cmax bits, bad */) {
+    const uint64_t total = (uint64_t)nx * (uint64_t)ny * (uint64_t)nz;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    double lp = 0.0, cm = 0.0;
+    unsigned long long bad = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const double a = sdf[i];
+        if (!__builtin_isfinite(a)) {
+            bad = 1;
+            continue;
+        }
+        const int64_t z = (int64_t)(i % (uint64_t)nz), y = (int64_t)((i / (uint64_t)nz) % (uint64_t)ny),
+                      x = (int64_t)(i / ((uint64_t)ny * (uint64_t)nz));
+        const uint64_t nb[3] = {x + 1 < nx ? i + (uint64_t)ny * (uint64_t)nz : i, y + 1 < ny ? i + (uint64_t)nz : i,
+                                z + 1 < nz ? i + 1 : i};
+        for (int k = 0; k < 3; ++k) {
+            if (nb[k] == i) continue;
+            const double b = sdf[nb[k]];
+            if (!__builtin_isfinite(b)) continue;
+            if (a > 0.0 && b > 0.0) {
+                const double v = __builtin_fabs(a - b) * inv;
+                lp = v > lp ? v : lp;
+            } else if (a > 0.0) {
+                const double v = a * inv;
+                cm = v > cm ? v : cm;
+            } else if (b > 0.0) {
+                const double v = b * inv;
+                cm = v > cm ? v : cm;
+            }
+        }
+    }
+    unsigned long long klp = (unsigned long long)fks_math::bits(lp), kcm = (unsigned long long)fks_math::bits(cm);
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o1 = __shfl_xor(klp, off, 64), o2 = __shfl_xor(kcm, off, 64), o3 = __shfl_xor(bad, off, 64);
+        klp = o1 > klp ? o1 : klp;
+        kcm = o2 > kcm ? o2 : kcm;
+        bad |= o3;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(out, klp);
+        atomicMax(out + 1, kcm);
+        if (bad) atomicOr(out + 2, bad);
+    }
+}
+
 }  // namespace
+
+bool fks_env::analyze_sdf_device(const float* d_sdf, int64_t nx, int64_t ny, int64_t nz, double res, double* lplus,
+                                 double* cmax) {
+    unsigned long long* d_out = nullptr;
+    if (hipMalloc((void**)&d_out, 3 * sizeof(unsigned long long)) != hipSuccess) return false;
+    bool ok = hipMemset(d_out, 0, 3 * sizeof(unsigned long long)) == hipSuccess;
+    if (ok) {
+        const uint64_t total = (uint64_t)nx * (uint64_t)ny * (uint64_t)nz;
+        const uint64_t blocks = (total + 255) / 256;
+        hipLaunchKernelGGL(env_analyze, dim3((unsigned)(blocks < 65536 ? (blocks ? blocks : 1) : 65536)), dim3(256), 0, nullptr,
+                           d_sdf, nx, ny, nz, 1.0 / res, d_out);
+        ok = hipGetLastError() == hipSuccess;
+    }
+    unsigned long long h[3] = {0, 0, 1};
+    if (ok) ok = hipMemcpy(h, d_out, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess;
+    (void)hipFree(d_out);
+    if (!ok || h[2]) return false;
+    *lplus = fks_math::from_bits((uint64_t)h[0]);
+    *cmax = fks_math::from_bits((uint64_t)h[1]);
+    return *lplus > 0.0;
+}
 
 #define ENV_TRY(expr)                            \
     do {                                         \
@@ -396,9 +471,9 @@ fks_status to_status(hipError_t e) {
         if (_e != hipSuccess) return to_status(_e); \
     } while (0)
 
-extern "C" fks_status fks_env_build_gpu(const fks_obstacle* obstacles, int32_t num_obstacles, double resolution,
-                                        const double* grid_origin, const int64_t* num_cells, int32_t device,
-                                        fks_env_handle** out, fks_env_build_stats* stats) {
+extern "C" fks_status fks_env_build_device(const fks_obstacle* obstacles, int32_t num_obstacles, double resolution,
+                                           const double* grid_origin, const int64_t* num_cells, int32_t device,
+                                           fks_device_env** out, fks_env_build_stats* stats) {
     if (!out || !(resolution > 0.0) || num_obstacles < 0 || (num_obstacles > 0 && !obstacles)) return FKS_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     const auto t_start = std::chrono::steady_clock::now();
@@ -540,29 +615,22 @@ extern "C" fks_status fks_env_build_gpu(const fks_obstacle* obstacles, int32_t n
     float gpu_ms = 0.0f;
     ENV_TRY(hipEventElapsedTime(&gpu_ms, ev0, ev1));
 
-    fks_env_handle* env = new (std::nothrow) fks_env_handle();
+    fks_device_env* env = new (std::nothrow) fks_device_env();
     if (!env) return FKS_ERR_OUT_OF_MEMORY;
-    try {
-        env->occupancy.resize(total);
-        env->sdf.resize(total);
-        env->offsets.resize(total + 1);
-        env->entries.resize(6 * nentries);
-    } catch (const std::bad_alloc&) {
-        delete env;
-        return FKS_ERR_OUT_OF_MEMORY;
-    }
-    hipError_t e = hipMemcpy(env->occupancy.data(), d_occ, total, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(env->sdf.data(), d_sdf, total * sizeof(float), hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(env->offsets.data(), d_offsets, (total + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost);
-    if (e == hipSuccess && nentries)
-        e = hipMemcpy(env->entries.data(), d_entries, 6 * nentries * sizeof(double), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) {
-        delete env;
-        return to_status(e);
-    }
+    env->device = device;
     std::memcpy(env->geometry.origin, A.grid.origin, sizeof(A.grid.origin));
     env->geometry.resolution = resolution;
     for (int a = 0; a < 3; ++a) env->geometry.num_cells[a] = A.grid.n[a];
+    env->cells = total;
+    env->num_entries = nentries;
+    env->occupancy = d_occ;
+    env->sdf = d_sdf;
+    env->offsets = d_offsets;
+    env->entries = d_entries;
+    B.keep(d_occ);
+    B.keep(d_sdf);
+    B.keep(d_offsets);
+    B.keep(d_entries);
     if (stats) {
         stats->cells = total;
         stats->obstacle_samples = samples;
@@ -572,4 +640,65 @@ extern "C" fks_status fks_env_build_gpu(const fks_obstacle* obstacles, int32_t n
     }
     *out = env;
     return FKS_OK;
+}
+
+extern "C" fks_status fks_device_env_geometry(const fks_device_env* env, fks_grid_geometry* out) {
+    if (!env || !out) return FKS_ERR_INVALID_ARGUMENT;
+    *out = env->geometry;
+    return FKS_OK;
+}
+
+extern "C" void fks_device_env_free(fks_device_env* env) {
+    if (!env) return;
+    (void)hipSetDevice(env->device);
+    void* ptrs[] = {env->occupancy, env->sdf, env->offsets, env->entries};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    delete env;
+}
+
+extern "C" fks_status fks_device_env_download(const fks_device_env* denv, fks_env_handle** out) {
+    if (!denv || !out) return FKS_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    ENV_TRY(hipSetDevice(denv->device));
+    fks_env_handle* env = new (std::nothrow) fks_env_handle();
+    if (!env) return FKS_ERR_OUT_OF_MEMORY;
+    const uint64_t total = denv->cells, nentries = denv->num_entries;
+    try {
+        env->occupancy.resize(total);
+        env->sdf.resize(total);
+        env->offsets.resize(total + 1);
+        env->entries.resize(6 * nentries);
+    } catch (const std::bad_alloc&) {
+        delete env;
+        return FKS_ERR_OUT_OF_MEMORY;
+    }
+    hipError_t e = hipMemcpy(env->occupancy.data(), denv->occupancy, total, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(env->sdf.data(), denv->sdf, total * sizeof(float), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(env->offsets.data(), denv->offsets, (total + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && nentries)
+        e = hipMemcpy(env->entries.data(), denv->entries, 6 * nentries * sizeof(double), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        delete env;
+        return to_status(e);
+    }
+    env->geometry = denv->geometry;
+    *out = env;
+    return FKS_OK;
+}
+
+extern "C" fks_status fks_env_build_gpu(const fks_obstacle* obstacles, int32_t num_obstacles, double resolution,
+                                        const double* grid_origin, const int64_t* num_cells, int32_t device,
+                                        fks_env_handle** out, fks_env_build_stats* stats) {
+    if (!out) return FKS_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    const auto t_start = std::chrono::steady_clock::now();
+    fks_device_env* denv = nullptr;
+    fks_status st = fks_env_build_device(obstacles, num_obstacles, resolution, grid_origin, num_cells, device, &denv, stats);
+    if (st != FKS_OK) return st;
+    st = fks_device_env_download(denv, out);
+    fks_device_env_free(denv);
+    if (st == FKS_OK && stats)
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    return st;
 }

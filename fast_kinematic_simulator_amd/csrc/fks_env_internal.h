@@ -24,7 +24,23 @@ struct fks_env_handle {
     std::vector<uint8_t> occupancy;
 };
 
+/* an environment built on the GPU and kept there (fks_env_build_device) */
+struct fks_device_env {
+    int32_t device;
+    fks_grid_geometry geometry;
+    uint64_t cells;
+    uint64_t num_entries;
+    uint8_t* occupancy; /* device arrays */
+    float* sdf;
+    uint32_t* offsets;
+    double* entries;
+};
+
 namespace fks_env {
+
+/* the SDF analysis behind the kernels' skip proofs (fks_capi.cpp analyze_sdf) on a
+ * device-resident SDF; false when a value is not finite or the analysis failed */
+bool analyze_sdf_device(const float* d_sdf, int64_t nx, int64_t ny, int64_t nz, double res, double* lplus, double* cmax);
 
 FKS_HD inline double dot3(double a0, double a1, double a2, double b0, double b1, double b2) {
     return (a0 * b0 + a1 * b1) + a2 * b2;

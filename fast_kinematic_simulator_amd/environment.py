@@ -83,19 +83,113 @@ class SimulatorEnvironment:
         return out
 
 
-def build_complete_environment(obstacles: Sequence[ObstacleConfig], resolution: float, origin=None,
-                               num_cells=None, device: Optional[int] = None, stats: Optional[dict] = None) -> SimulatorEnvironment:
-    """BuildCompleteEnvironment(obstacles, resolution) (SEB.cpp:470-476).  With
-    `origin` (3x4) and `num_cells` the grid is that fixed box (e.g. 256^3).
-    device=None builds on the host (fks_env_build); device=g builds on HIP device g
-    (fks_env_build_gpu, the same bytes).  `stats`, if given, receives the GPU
-    build's sizes and timings."""
-    L = _capi.lib()
+def _obstacle_array(obstacles):
     arr = (_capi.Obstacle * max(1, len(obstacles)))()
     for i, ob in enumerate(obstacles):
         arr[i].pose[:] = [float(v) for v in np.asarray(ob.pose).reshape(12)]
         arr[i].extents[:] = [float(v) for v in ob.extents]
         arr[i].object_id = int(ob.object_id)
+    return arr
+
+
+class DeviceEnvironment:
+    """An environment built on a HIP device and kept there (fks_env_build_device):
+    a simulator made from it copies the SDF and normal CSR device to device.
+    ``download()`` gives the host copy (the same bytes as build_complete_environment)."""
+
+    def __init__(self, handle, device: int, stats: dict):
+        self._lib = _capi.lib()
+        self._handle = handle
+        self.device = int(device)
+        self.stats = stats
+        g = _capi.GridGeometry()
+        _capi.check(self._lib.fks_device_env_geometry(handle, ctypes.byref(g)), None, "fks_device_env_geometry")
+        self.geometry = GridGeometry(np.array(g.origin[:]), g.resolution, tuple(g.num_cells[:]))
+        self.frame = "world"
+        self._host = None
+
+    @property
+    def handle(self):
+        return self._handle
+
+    @property
+    def resolution(self) -> float:
+        return self.geometry.resolution
+
+    def download(self) -> SimulatorEnvironment:
+        if self._host is None:
+            L = self._lib
+            h = ctypes.c_void_p()
+            _capi.check(L.fks_device_env_download(self._handle, ctypes.byref(h)), None, "fks_device_env_download")
+            self._host = _host_environment(h)
+        return self._host
+
+    def close(self):
+        if getattr(self, "_handle", None):
+            self._lib.fks_device_env_free(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def build_device_environment(obstacles: Sequence[ObstacleConfig], resolution: float, origin=None, num_cells=None,
+                             device: int = 0) -> DeviceEnvironment:
+    """BuildCompleteEnvironment on HIP device `device`, result kept in device memory."""
+    L = _capi.lib()
+    arr = _obstacle_array(obstacles)
+    o_ptr = n_ptr = None
+    if origin is not None and num_cells is not None:
+        o_arr = np.ascontiguousarray(np.asarray(origin, dtype=np.float64).reshape(12))
+        n_arr = np.ascontiguousarray(np.asarray(num_cells, dtype=np.int64))
+        o_ptr = _capi.as_ptr(o_arr, ctypes.c_double)
+        n_ptr = _capi.as_ptr(n_arr, ctypes.c_int64)
+    handle = ctypes.c_void_p()
+    bs = _capi.EnvBuildStats()
+    st = L.fks_env_build_device(arr, len(obstacles), float(resolution), o_ptr, n_ptr, int(device), ctypes.byref(handle),
+                                ctypes.byref(bs))
+    _capi.check(st, None, "fks_env_build_device")
+    return DeviceEnvironment(handle, device, bs.as_dict())
+
+
+def _host_environment(handle) -> SimulatorEnvironment:
+    """Copy a host fks_env_handle into a SimulatorEnvironment and free the handle."""
+    L = _capi.lib()
+    try:
+        view = _capi.Environment()
+        _capi.check(L.fks_env_view(handle, ctypes.byref(view)), None, "fks_env_view")
+        geom = GridGeometry(np.array(view.sdf.origin[:]), view.sdf.resolution, tuple(view.sdf.num_cells[:]))
+        ncells = int(np.prod(geom.num_cells))
+        sdf = np.ctypeslib.as_array(view.sdf_values, shape=(ncells,)).copy()
+        offsets = np.ctypeslib.as_array(view.normal_offsets, shape=(ncells + 1,)).copy()
+        nent = int(offsets[-1])
+        entries = np.ctypeslib.as_array(view.normal_entries, shape=(6 * nent,)).copy() if nent else np.zeros(0)
+        oob = float(view.sdf_oob_value)
+        occupancy = _env_occupancy(handle, ncells)
+    finally:
+        L.fks_env_free(handle)
+    return SimulatorEnvironment(geom, sdf, offsets, entries, oob, occupancy)
+
+
+def build_complete_environment(obstacles: Sequence[ObstacleConfig], resolution: float, origin=None,
+                               num_cells=None, device: Optional[int] = None, stats: Optional[dict] = None,
+                               resident: bool = False):
+    """BuildCompleteEnvironment(obstacles, resolution) (SEB.cpp:470-476).  With
+    `origin` (3x4) and `num_cells` the grid is that fixed box (e.g. 256^3).
+    device=None builds on the host (fks_env_build); device=g builds on HIP device g
+    (fks_env_build_gpu, the same bytes).  `stats`, if given, receives the GPU
+    build's sizes and timings.  resident=True (with a device) keeps the result on the
+    device and returns a DeviceEnvironment."""
+    if resident:
+        denv = build_device_environment(obstacles, resolution, origin, num_cells, 0 if device is None else device)
+        if stats is not None:
+            stats.update(denv.stats)
+        return denv
+    L = _capi.lib()
+    arr = _obstacle_array(obstacles)
     handle = ctypes.c_void_p()
     o_ptr = None
     n_ptr = None
@@ -114,20 +208,7 @@ def build_complete_environment(obstacles: Sequence[ObstacleConfig], resolution: 
         _capi.check(st, None, "fks_env_build_gpu")
         if stats is not None:
             stats.update(bs.as_dict())
-    try:
-        view = _capi.Environment()
-        _capi.check(L.fks_env_view(handle, ctypes.byref(view)), None, "fks_env_view")
-        geom = GridGeometry(np.array(view.sdf.origin[:]), view.sdf.resolution, tuple(view.sdf.num_cells[:]))
-        ncells = int(np.prod(geom.num_cells))
-        sdf = np.ctypeslib.as_array(view.sdf_values, shape=(ncells,)).copy()
-        offsets = np.ctypeslib.as_array(view.normal_offsets, shape=(ncells + 1,)).copy()
-        nent = int(offsets[-1])
-        entries = np.ctypeslib.as_array(view.normal_entries, shape=(6 * nent,)).copy() if nent else np.zeros(0)
-        oob = float(view.sdf_oob_value)
-        occupancy = _env_occupancy(handle, ncells)
-    finally:
-        L.fks_env_free(handle)
-    return SimulatorEnvironment(geom, sdf, offsets, entries, oob, occupancy)
+    return _host_environment(handle)
 
 
 def _env_occupancy(handle, ncells):

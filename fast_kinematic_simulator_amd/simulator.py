@@ -15,7 +15,7 @@ from typing import Callable, List, Optional, Sequence
 import numpy as np
 
 from . import _capi
-from .environment import SimulatorEnvironment
+from .environment import DeviceEnvironment, SimulatorEnvironment
 from .robots import RobotDescription
 from .trace import ForwardSimulationStepTrace, TraceBuffers
 
@@ -71,13 +71,22 @@ class HipParticleContactSimulator:
         self.solver_config = solver_config
         self.simulation_controller_frequency = float(simulation_controller_frequency)
         self.prng_seed = int(prng_seed)
-        env_c, self._env_keep = environment.to_c()
         params = solver_config.to_c()
         ctx = ctypes.c_void_p()
-        st = self._lib.fks_create(ctypes.byref(env_c), ctypes.byref(params), self.simulation_controller_frequency,
-                                  ctypes.c_uint64(self.prng_seed & 0xFFFFFFFFFFFFFFFF), int(debug_level), int(device),
-                                  ctypes.byref(ctx))
-        _capi.check(st, None, "fks_create")
+        if isinstance(environment, DeviceEnvironment):
+            # device-resident GPU build: SDF + normal CSR copied device to device (fks_create_from_device_env)
+            self._env_keep = None
+            st = self._lib.fks_create_from_device_env(environment.handle, ctypes.byref(params),
+                                                      self.simulation_controller_frequency,
+                                                      ctypes.c_uint64(self.prng_seed & 0xFFFFFFFFFFFFFFFF), int(debug_level),
+                                                      ctypes.byref(ctx))
+            _capi.check(st, None, "fks_create_from_device_env")
+        else:
+            env_c, self._env_keep = environment.to_c()
+            st = self._lib.fks_create(ctypes.byref(env_c), ctypes.byref(params), self.simulation_controller_frequency,
+                                      ctypes.c_uint64(self.prng_seed & 0xFFFFFFFFFFFFFFFF), int(debug_level), int(device),
+                                      ctypes.byref(ctx))
+            _capi.check(st, None, "fks_create")
         self._ctx = ctx
         self._robot_key = None
         self._robot = None
@@ -356,7 +365,7 @@ class HipParticleContactSimulator:
         the filled cells of the collision grid ("sim_environment") and the SDF cells
         colored by sign ("sim_environment_sdf").  sdf_tools' connected-component and
         convex-segment exports have no counterpart here."""
-        env = self.environment
+        env = self.environment.download() if isinstance(self.environment, DeviceEnvironment) else self.environment
         g = env.geometry
         n = tuple(int(v) for v in g.num_cells)
         o = np.asarray(g.origin, dtype=np.float64).reshape(3, 4)

@@ -75,7 +75,7 @@ def grid_origin(lo) -> np.ndarray:
 
 
 # ---------------------------------------------------------------- cfg1: SE(2)
-def _cfg1_env(device=None, stats=None):
+def _cfg1_env(device=None, stats=None, resident=False):
     rng = np.random.default_rng(1)
     obstacles = []
     for i in range(12):
@@ -83,7 +83,7 @@ def _cfg1_env(device=None, stats=None):
         h = [rng.uniform(0.08, 0.25), rng.uniform(0.08, 0.25), 1.0]
         obstacles.append(box(i + 1, c, h, rotation_from_axis_angle([0, 0, 1], rng.uniform(0, np.pi))))
     return build_complete_environment(obstacles, 0.0625, origin=grid_origin([0.0, 0.0, -2.0]), num_cells=(64, 64, 64),
-                                      device=device, stats=stats)
+                                      device=device, stats=stats, resident=resident)
 
 
 def _se2_points(x, y, th, pts):
@@ -139,13 +139,13 @@ def serial_arm(segments, axes, radii, base_height, base_radius, limits=np.pi, na
                              allowed, _arm_controllers(n), [1.0] * n, name=name)
 
 
-def _cfg2_env(device=None, stats=None):
+def _cfg2_env(device=None, stats=None, resident=False):
     obstacles = [box(1, [0.0, 0.0, -0.05], [0.9, 0.9, 0.05]),           # table, top at z = 0
                  box(2, [0.45, 0.25, 0.25], [0.06, 0.06, 0.25]),        # post
                  box(3, [0.35, -0.35, 0.12], [0.10, 0.08, 0.12]),       # block
                  box(4, [-0.3, 0.4, 0.35], [0.05, 0.05, 0.35])]         # pillar
     return build_complete_environment(obstacles, 0.02, origin=grid_origin([-1.28, -1.28, -0.4]), num_cells=(128, 128, 128),
-                                      device=device, stats=stats)
+                                      device=device, stats=stats, resident=resident)
 
 
 def cfg2(scale: float = 1.0) -> Workload:
@@ -162,7 +162,7 @@ def cfg2(scale: float = 1.0) -> Workload:
                     solver, 100.0, 12, True, 128, 0.02)
 
 
-def _cfg3_env(device=None, stats=None):
+def _cfg3_env(device=None, stats=None, resident=False):
     rng = np.random.default_rng(4)
     obstacles = [box(1, [0.0, 0.0, -0.05], [1.1, 1.1, 0.05])]            # table, top at z = 0
     pillars = [[0.55, 0.35], [0.25, 0.62], [-0.45, 0.45], [0.6, -0.3], [-0.2, -0.6]]
@@ -170,7 +170,7 @@ def _cfg3_env(device=None, stats=None):
         h = rng.uniform(0.3, 0.5)
         obstacles.append(box(2 + i, [x, y, h / 2], [0.05, 0.05, h / 2]))
     return build_complete_environment(obstacles, 0.01, origin=grid_origin([-1.28, -1.28, -0.3]), num_cells=(256, 256, 256),
-                                      device=device, stats=stats)
+                                      device=device, stats=stats, resident=resident)
 
 
 def iiwa_style_arm() -> RobotDescription:
@@ -195,7 +195,7 @@ def cfg3(scale: float = 1.0) -> Workload:
 
 
 # ---------------------------------------------------------------- cfg4: SE(3)
-def _cfg4_env(device=None, stats=None):
+def _cfg4_env(device=None, stats=None, resident=False):
     rng = np.random.default_rng(5)
     obstacles = []
     for i in range(24):
@@ -207,7 +207,7 @@ def _cfg4_env(device=None, stats=None):
     # a block across the straight-line path to the target, so particles slide along it
     obstacles.append(box(100, [0.2, 0.14, -0.09], [0.04, 0.04, 0.04], rotation_from_axis_angle([0.0, 0.0, 1.0], 0.3)))
     return build_complete_environment(obstacles, 0.01, origin=grid_origin([-1.28, -1.28, -1.28]), num_cells=(256, 256, 256),
-                                      device=device, stats=stats)
+                                      device=device, stats=stats, resident=resident)
 
 
 def cfg4(scale: float = 1.0) -> Workload:
@@ -267,12 +267,12 @@ def dual_arm_robot() -> RobotDescription:
                              name="dual_arm_14dof")
 
 
-def _cfg5_env(device=None, stats=None):
+def _cfg5_env(device=None, stats=None, resident=False):
     obstacles = [box(1, [0.6, 0.0, 0.35], [0.35, 0.7, 0.05]),
                  box(2, [0.7, 0.35, 0.48], [0.1, 0.1, 0.08]),
                  box(3, [0.7, -0.35, 0.48], [0.1, 0.1, 0.08])]
     return build_complete_environment(obstacles, 0.005, origin=grid_origin([-0.48, -1.28, -0.2]), num_cells=(512, 512, 512),
-                                      device=device, stats=stats)
+                                      device=device, stats=stats, resident=resident)
 
 
 def cfg5(scale: float = 1.0) -> Workload:

@@ -417,6 +417,22 @@ fks_status fks_env_build_gpu(const fks_obstacle* obstacles, int32_t num_obstacle
                              double resolution, const double* grid_origin,
                              const int64_t* num_cells, int32_t device, fks_env_handle** out,
                              fks_env_build_stats* stats);
+/* The same GPU build kept in device memory, handed to a context without a trip
+ * through the host (the simulation reads exactly these bytes). */
+typedef struct fks_device_env fks_device_env;
+fks_status fks_env_build_device(const fks_obstacle* obstacles, int32_t num_obstacles,
+                                double resolution, const double* grid_origin,
+                                const int64_t* num_cells, int32_t device, fks_device_env** out,
+                                fks_env_build_stats* stats);
+/* host copy of a device environment (then fks_env_view / fks_env_occupancy / fks_env_free) */
+fks_status fks_device_env_download(const fks_device_env* env, fks_env_handle** out);
+fks_status fks_device_env_geometry(const fks_device_env* env, fks_grid_geometry* out);
+void fks_device_env_free(fks_device_env* env);
+/* fks_create on the device environment's own device: the SDF and surface-normal CSR are
+ * copied device to device; the context does not keep a reference to `env`. */
+fks_status fks_create_from_device_env(const fks_device_env* env, const fks_solver_params* params,
+                                      double simulation_controller_frequency, uint64_t prng_seed,
+                                      int32_t debug_level, fks_context** out_ctx);
 /* Fill a view whose pointers stay valid until fks_env_free. */
 fks_status fks_env_view(const fks_env_handle* env, fks_environment* out);
 /* The collision grid (1 = filled cell), z-fastest, num_cells = nx * ny * nz. */

@@ -105,3 +105,46 @@ def test_gpu_env_build_matches_host(fks_lib, name):
         assert stats["cells"] == int(np.prod(host.geometry.num_cells))
         assert stats["normal_entries"] == int(host.normal_offsets[-1])
         print(f"{name}: {stats['cells']} cells, GPU build {stats['gpu_ms']:.2f} ms (call {stats['total_ms']:.1f} ms)")
+
+
+def test_device_env_entry_points_without_device():
+    L = _capi.lib()
+    h = ctypes.c_void_p()
+    assert L.fks_env_build_device(None, 0, -1.0, None, None, 0, ctypes.byref(h), None) == _capi.ERR_INVALID_ARGUMENT
+    assert L.fks_create_from_device_env(None, None, 100.0, 0, 0, ctypes.byref(h)) == _capi.ERR_INVALID_ARGUMENT
+    assert L.fks_device_env_download(None, ctypes.byref(h)) == _capi.ERR_INVALID_ARGUMENT
+    L.fks_device_env_free(None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,scale", [("cfg3", 32 / 65536), ("cfg5", 6 / 1048576)])
+def test_device_resident_environment_feeds_the_simulator(fks_lib, name, scale):
+    """fks_env_build_device + fks_create_from_device_env: the downloaded bytes equal the
+    host build and a simulator made from the device copy gives identical results."""
+    import time
+
+    from fast_kinematic_simulator_amd import make_linked_simulator
+
+    wl = W.WORKLOADS[name](scale)
+    host = wl.environment()
+    t0 = time.perf_counter()
+    denv = W.SCENES[name](device=0, resident=True)
+    a = make_linked_simulator(denv, wl.solver, wl.controller_frequency, wl.seed)
+    setup_device = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    b = make_linked_simulator(host, wl.solver, wl.controller_frequency, wl.seed)
+    setup_host_env = time.perf_counter() - t0
+    try:
+        assert_same_environment(denv.download(), host)
+        a.set_call_index(2)
+        b.set_call_index(2)
+        ra = a.forward_simulate_arrays(wl.robot, wl.starts, wl.targets, True)
+        rb = b.forward_simulate_arrays(wl.robot, wl.starts, wl.targets, True)
+        for k in ("positions", "collided", "microsteps", "resolver_iterations", "error_flags"):
+            assert np.array_equal(ra[k], rb[k]), k
+        assert a.last_call_counters()["sdf_bytes"] == b.last_call_counters()["sdf_bytes"]
+    finally:
+        a.close()
+        b.close()
+        denv.close()
+    print(f"{name}: device build + create {setup_device:.3f}s, create from host arrays {setup_host_env:.3f}s")
