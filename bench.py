@@ -157,11 +157,12 @@ def main():
     wl = W.WORKLOADS[args.workload](scale=n_total / float(base))
     t0 = time.perf_counter()
     env_stats = {}
-    env = W.SCENES[args.workload](device=local_rank, stats=env_stats)  # fks_env_build_gpu (same bytes as the host build)
-    wl._env = env
+    # the environment is built on this rank's GPU and handed to the simulator there
+    # (fks_env_build_device + fks_create_from_device_env: the host build's bytes)
+    denv = W.SCENES[args.workload](device=local_rank, stats=env_stats, resident=True)
     log(f"[rank {rank}] environment {env_stats['cells']} cells built on the GPU in {env_stats['gpu_ms']:.1f} ms device "
-        f"time ({time.perf_counter() - t0:.2f}s call, {int(env.normal_offsets[-1])} surface-normal entries)")
-    sim = make_linked_simulator(env, wl.solver, wl.controller_frequency, wl.seed, device=local_rank)
+        f"time ({time.perf_counter() - t0:.2f}s call, {env_stats['normal_entries']} surface-normal entries)")
+    sim = make_linked_simulator(denv, wl.solver, wl.controller_frequency, wl.seed, device=local_rank)
     sim.set_robot(wl.robot)
     Wd = wl.robot.config_width
     dev = torch.device("cuda", local_rank)
@@ -237,7 +238,7 @@ def main():
             t0 = time.perf_counter()
             sample = min(args.cpu_sample, n_total)
             cwl = W.WORKLOADS[args.workload](scale=sample / float(base))
-            cwl._env = env
+            cwl._env = denv.download()
             cpu = cpu_baseline(cwl, sample, threads)
             log(f"cpu baseline {cpu['value']:.0f} {UNIT} in {time.perf_counter() - t0:.1f}s")
         value = all_micro / elapsed
@@ -251,6 +252,8 @@ def main():
                 "note": "one fks_forward_simulate call with host buffers (H2D starts/targets, kernel, D2H outcomes), rank 0"}
         cc = None
         if not args.no_config_check and args.workload == "cfg3":
+            if not args.no_cpu_baseline:
+                wl._env = denv.download()  # the oracle's CPU baseline reads the host copy
             cc = config_check_bench(sim, wl, dev, with_cpu=not args.no_cpu_baseline)
             log(f"config check {cc['value']:.3e} configs/s")
         line = {
@@ -301,6 +304,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     sim.close()
+    denv.close()
     if dist is not None:
         dist.barrier()  # rank 0 ran the CPU baseline and the config-check line after the timed region
         dist.destroy_process_group()
