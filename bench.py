@@ -139,10 +139,13 @@ def main():
 
     torch.cuda.set_device(local_rank)
     dist = None
-    if world > 1:
+    # under torchrun (RANK/MASTER_ADDR set) the RCCL process group is used even at
+    # world size 1, so the launched path is the one the multi-GPU runs take
+    if world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ):
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        log(f"[rank {rank}] joined the RCCL process group (world size {world})")
 
     from fast_kinematic_simulator_amd import make_linked_simulator
     from fast_kinematic_simulator_amd import workloads as W
@@ -174,7 +177,7 @@ def main():
     out_res = torch.empty(n_local, dtype=torch.int32, device=dev)
     out_err = torch.empty(n_local, dtype=torch.int32, device=dev)
     packed = torch.empty((n_local, Wd + 4), dtype=torch.float64, device=dev)
-    gathered = [torch.empty_like(packed) for _ in range(world)] if (dist and rank == 0) else None
+    gathered = [torch.empty_like(packed) for _ in range(world)] if (dist is not None and rank == 0) else None
     micro_total = torch.zeros((), dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
 

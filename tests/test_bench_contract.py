@@ -35,3 +35,25 @@ def test_bench_json_line():
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
     assert d["pcie_inclusive"]["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_under_torchrun():
+    """The driver's multi-GPU launch (torchrun, one rank per GPU, RCCL process group,
+    outcome gather, max-over-ranks timing) at the world size one GPU allows."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+                        "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "1",
+                        "--particles", "2048", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-config-check"],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["config"]["particles_total"] == 2048
+    assert "process group" in p.stderr  # bench.py logs the RCCL group it joined
