@@ -217,6 +217,7 @@ def main():
     kernel_ms = [a.elapsed_time(b) for a, b in events]
     tot = sim.total_counters()
     phases = sim.phase_cycles(total=True)
+    geom = sim.launch_geometry()
     local_micro = int(micro_total.item())
     assert local_micro == int(tot["microsteps"]), (local_micro, tot["microsteps"])
     if dist is not None:
@@ -296,13 +297,17 @@ def main():
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },
+            # share of the persistent grid's wave slots that held a particle during the timed
+            # launches (1.0 = no tail): wave residency in 100 MHz s_memrealtime ticks
+            "wave_slots": {"resident_waves": geom["resident_waves"],
+                           "busy_fraction": phases["wave_residency"] / 1e5 / max(1e-9, geom["resident_waves"] * sum(kernel_ms))},
             "cpu_baseline": cpu,
             "config_check": cc,
             "pcie_inclusive": pcie,
             # share of wave time per phase of the hot path (s_memtime cycle sums, rank 0)
             # (only in profiling builds of the library: -DFKS_PHASE_TIMERS=1, see tools/variant_bench.py)
             "kernel_phases": ({k: (v if k in PHASE_COUNTS else round(v / max(1, phases["particle"]), 4))
-                               for k, v in phases.items() if k not in ("particle", "reserved")}
+                               for k, v in phases.items() if k not in ("particle", "wave_residency")}
                               if phases.get("control", 0) > 0 else None),
         }
         print(json.dumps(line), flush=True)

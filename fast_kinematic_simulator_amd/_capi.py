@@ -32,8 +32,8 @@ OK, ERR_INVALID_ARGUMENT, ERR_HIP, ERR_NO_ROBOT, ERR_OUT_OF_MEMORY, ERR_UNSUPPOR
 NUM_PHASES = 16
 PHASE_NAMES = ["particle", "control", "step_setup", "micro_input", "micro_fk", "env_check", "self_check", "corrections",
                "solve", "resolve_apply", "output", "env_rounds_skipped", "env_rounds_evaluated", "corr_rounds_skipped",
-               "corr_rounds_evaluated", "reserved"]
-PHASE_COUNTS = {"env_rounds_skipped", "env_rounds_evaluated", "corr_rounds_skipped", "corr_rounds_evaluated"}
+               "corr_rounds_evaluated", "wave_residency"]
+PHASE_COUNTS = {"env_rounds_skipped", "env_rounds_evaluated", "corr_rounds_skipped", "corr_rounds_evaluated", "wave_residency"}
 
 PARTICLE_ERR_MICROSTEP_MOTION = 0x1
 PARTICLE_ERR_NORMAL_OOB = 0x2
@@ -246,6 +246,8 @@ PROTOTYPES = [
     ("fks_get_total_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
     ("fks_reset_total_counters", c_int32, [c_void_p]),
     ("fks_get_phase_cycles", c_int32, [c_void_p, c_int32, POINTER(c_uint64)]),
+    ("fks_get_launch_geometry", c_int32, [c_void_p, POINTER(c_uint32), POINTER(c_uint64)]),
+    ("fks_set_segment_steps", c_int32, [c_void_p, c_uint32]),
     ("fks_env_build", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), POINTER(c_void_p)]),
     ("fks_env_build_gpu", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), c_int32,
                                     POINTER(c_void_p), POINTER(EnvBuildStats)]),

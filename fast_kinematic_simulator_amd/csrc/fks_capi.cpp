@@ -71,6 +71,10 @@ sim_kernel_t kernel_for(int robot_type) {
 }
 
 using fksd::GridDev;
+/* controller steps per segment when a batch outnumbers the resident waves: short
+ * enough that a contact-heavy particle progresses from the start of the launch, long
+ * enough that the hand-over (resting state + one FK) costs < 1 % */
+constexpr uint32_t kDefaultSegmentSteps = 10;
 using fksd::JointDev;
 using fksd::RobotDev;
 
@@ -228,6 +232,11 @@ struct fks_context {
     uint32_t* d_res = nullptr;
     uint32_t* d_err = nullptr;
     size_t cap_particles = 0, cap_targets = 0;
+    /* controller-step segments: resting particle state between segments */
+    uint32_t segment_steps = 0; /* 0 = automatic (kDefaultSegmentSteps) */
+    double* d_seg_state = nullptr;
+    uint32_t* d_seg_done = nullptr;
+    size_t cap_seg_state = 0, cap_seg_done = 0;
     fks_statistics stats;
     fks_call_counters last;
     fks_call_counters total;
@@ -269,6 +278,11 @@ static void free_staging(fks_context* ctx) {
     ctx->d_coll = nullptr;
     ctx->d_micro = ctx->d_res = ctx->d_err = nullptr;
     ctx->cap_particles = ctx->cap_targets = 0;
+    if (ctx->d_seg_state) (void)hipFree(ctx->d_seg_state);
+    if (ctx->d_seg_done) (void)hipFree(ctx->d_seg_done);
+    ctx->d_seg_state = nullptr;
+    ctx->d_seg_done = nullptr;
+    ctx->cap_seg_state = ctx->cap_seg_done = 0;
 }
 
 extern "C" {
@@ -777,6 +791,9 @@ static fks_status settle(fks_context* ctx) {
     ctx->last.sdf_bytes = c[fksd::kCntSdfBytes];
     ctx->last.error_particles = c[fksd::kCntErrorParticles];
     ctx->last.least_squares_rows = c[fksd::kCntLsqRows];
+    if (c[fksd::kCntSegmentWaitTimeouts])
+        return fail(ctx, FKS_ERR_HIP, "segment hand-over timed out (" + std::to_string(c[fksd::kCntSegmentWaitTimeouts]) +
+                                          " particles abandoned)");
     for (int k = 0; k < FKS_NUM_PHASES; ++k) {
         ctx->phase_last[k] = c[fksd::kPhaseBase + k];
         ctx->phase_total[k] += ctx->phase_last[k];
@@ -874,6 +891,32 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.row_cap = 3u * (uint32_t)ctx->R.P;
     a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P);
+    /* controller-step segments: automatically only when the batch outnumbers the
+     * resident waves (otherwise every particle has a wave from the start), always
+     * when set explicitly (fks_set_segment_steps); traced calls run whole */
+    a.seg_steps = a.T;
+    a.nseg = 1;
+    a.seg_stride = 2u * (uint32_t)ctx->R.D + 4u;
+    if (!tr && n > 0 && (ctx->segment_steps != 0 || n > (uint64_t)ctx->grid_waves)) {
+        uint32_t k = ctx->segment_steps ? ctx->segment_steps : kDefaultSegmentSteps;
+        if (k > a.T) k = a.T;
+        a.seg_steps = k;
+        a.nseg = (a.T + k - 1u) / k;
+    }
+    if (a.nseg > 1) {
+        const size_t words = (size_t)n * a.seg_stride;
+        if (words > ctx->cap_seg_state) {
+            HIP_TRY(ctx, ensure(&ctx->d_seg_state, words));
+            ctx->cap_seg_state = words;
+        }
+        if (n > ctx->cap_seg_done) {
+            HIP_TRY(ctx, ensure(&ctx->d_seg_done, (size_t)n));
+            ctx->cap_seg_done = (size_t)n;
+        }
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_seg_done, 0, (size_t)n * sizeof(uint32_t), s));
+        a.seg_state = ctx->d_seg_state;
+        a.seg_done = ctx->d_seg_done;
+    }
     if (tr) {
         a.tr_inputs = tr->inputs;
         a.tr_micro = tr->micro;
@@ -1276,6 +1319,20 @@ fks_status fks_get_phase_cycles(const fks_context* ctx, int which, uint64_t* out
     fks_status st = settle(const_cast<fks_context*>(ctx));
     if (st != FKS_OK) return st;
     std::memcpy(out, which ? ctx->phase_total : ctx->phase_last, sizeof(ctx->phase_last));
+    return FKS_OK;
+}
+
+fks_status fks_set_segment_steps(fks_context* ctx, uint32_t controller_steps) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    ctx->segment_steps = controller_steps;
+    return FKS_OK;
+}
+
+fks_status fks_get_launch_geometry(const fks_context* ctx, uint32_t* resident_waves, uint64_t* lds_bytes_per_group) {
+    if (!ctx || !resident_waves || !lds_bytes_per_group) return FKS_ERR_INVALID_ARGUMENT;
+    if (!ctx->has_robot) return FKS_ERR_NO_ROBOT;
+    *resident_waves = ctx->grid_waves;
+    *lds_bytes_per_group = (uint64_t)ctx->lds_bytes;
     return FKS_OK;
 }
 

@@ -260,7 +260,16 @@ struct SimArgs {
     uint32_t* out_resolver;
     uint32_t* out_err;
     unsigned long long* counters; /* kCounter* */
-    unsigned long long* queue;
+    unsigned long long* queue;     /* ticket counter: ticket t = segment t / n of particle t % n */
+    /* controller-step segments (processor sharing across the persistent grid): a
+     * particle's steps [k*seg_steps, (k+1)*seg_steps) form segment k; between
+     * segments its state rests in seg_state (PID integral / last error per DOF,
+     * flags, per-particle counters; the configuration in out_q) and seg_done[p]
+     * counts its finished segments (nseg once the particle has ended) */
+    double* seg_state;
+    uint32_t* seg_done;
+    uint32_t seg_steps, nseg;
+    uint32_t seg_stride, seg_pad; /* doubles per particle in seg_state */
     double* scratch;
     uint64_t scratch_per_wave; /* doubles */
     uint32_t row_cap;          /* 3 * P */
@@ -297,6 +306,7 @@ enum {
     kCntSdfBytes,
     kCntErrorParticles,
     kCntLsqRows,
+    kCntSegmentWaitTimeouts, /* segment hand-overs abandoned after kSegmentWaitTicks (never expected) */
     kNumCounters = 16
 };
 

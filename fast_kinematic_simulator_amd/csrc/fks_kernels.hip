@@ -902,6 +902,9 @@ __device__ __forceinline__ double wave_min(double v) {
     return (b < a) ? b : a;
 }
 constexpr double kInvalidRound = -1.0e308;
+/* a segment hand-over that waits longer than this (100 MHz s_memrealtime ticks = 20 s)
+ * is abandoned and reported (kCntSegmentWaitTimeouts): every wave reaches an exit */
+constexpr uint64_t kSegmentWaitTicks = 2000000000ull;
 enum { kSkipCheck = 1, kSkipCorrections = 2 };
 
 /* (link, radius) of round r < 64 from the workgroup's LDS copy of R.rounds */
@@ -2668,12 +2671,53 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     double* res_cfg = s.lds + s.A->L.cfg_res;
     double* u = s.lds + s.A->L.u;
     unsigned long long* next_particle = reinterpret_cast<unsigned long long*>(s.lds + s.A->L.misc + 31);
+    uint32_t* seg_seen = reinterpret_cast<uint32_t*>(s.lds + s.A->L.misc + 30);
+    const uint64_t t_resident = __builtin_amdgcn_s_memrealtime();
+    const uint32_t nseg = A.nseg;
     while (true) {
+        /* ticket t: segment t / n of particle t % n, so every particle's first segment is
+         * handed out before any second one (processor sharing over the persistent grid:
+         * a contact-heavy particle no longer starts late and sets the batch's tail) */
         if (ln == 0) *next_particle = atomicAdd(A.queue, 1ull);
         wsync();
-        const uint64_t local = *next_particle;
+        const uint64_t ticket = *next_particle;
         wsync();
-        if (local >= A.n) break;
+        const uint64_t seg = (A.n > 0) ? ticket / A.n : (uint64_t)nseg;
+        if (seg >= (uint64_t)nseg) {
+            /* the queue is drained: this wave slot idles from here to the kernel's end */
+            if (ln == 0)
+                atomicAdd(A.counters + kPhaseBase + FKS_PHASE_WAVE_RESIDENCY,
+                          (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t_resident));
+            break;
+        }
+        const uint64_t local = ticket - seg * A.n;
+        if (seg > 0) {
+            /* segment seg-1 of this particle was handed out n tickets earlier; it is
+             * almost always finished (only the last rounds of a batch wait here) */
+            if (ln == 0) {
+                uint32_t v = __hip_atomic_load(A.seg_done + local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v < (uint32_t)seg) {
+                    const uint64_t t_wait = __builtin_amdgcn_s_memrealtime();
+                    while (v < (uint32_t)seg) {
+                        __builtin_amdgcn_s_sleep(16);
+                        v = __hip_atomic_load(A.seg_done + local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (v < (uint32_t)seg && __builtin_amdgcn_s_memrealtime() - t_wait > kSegmentWaitTicks) {
+                            atomicAdd(A.counters + kCntSegmentWaitTimeouts, 1ull);
+                            v = nseg;
+                        }
+                    }
+                }
+                *seg_seen = v;
+            }
+            wsync();
+            const uint32_t seen = *seg_seen;
+            wsync();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (seen >= nseg) continue; /* the particle ended in an earlier segment */
+        }
+        const uint32_t step_begin = (uint32_t)seg * A.seg_steps;
+        const uint32_t step_end = (seg + 1 == (uint64_t)nseg) ? A.T : step_begin + A.seg_steps;
+        double* st = A.seg_state + local * (uint64_t)A.seg_stride; /* nseg > 1 only */
         s.pid = A.first_pid + local;
         s.local = local;
         s.tr_steps = 0;
@@ -2687,31 +2731,47 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         if (ln < 8) s.stats[ln] = 0;
         if (ln < FKS_NUM_PHASES) s.phase[ln] = 0;
         const uint64_t t_particle = __builtin_amdgcn_s_memtime();
-        s.pid_integral = 0.0;
-        s.pid_last = 0.0;
         s.self_nonempty = false;
         s.tcur_valid = false;
         const double* start = A.starts + local * (uint64_t)W;
         const double* target = (A.num_targets == A.n) ? A.targets + local * (uint64_t)W : A.targets;
-        /* ResetPosition(start): SetPosition enforces joint limits / angle wrap */
-        if constexpr (RT == FKS_ROBOT_LINKED) {
-            if (ln < D) {
-                const JointDev& jd = s.joints[s.dofj[ln]];
-                cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(start[ln])
-                                                            : clamp(start[ln], jd.lo, jd.hi);
+        bool collided = false;
+        bool any_failed = false;
+        uint64_t micro_before = 0, resolver_before = 0;
+        if (seg == 0) {
+            s.pid_integral = 0.0;
+            s.pid_last = 0.0;
+            /* ResetPosition(start): SetPosition enforces joint limits / angle wrap */
+            if constexpr (RT == FKS_ROBOT_LINKED) {
+                if (ln < D) {
+                    const JointDev& jd = s.joints[s.dofj[ln]];
+                    cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(start[ln])
+                                                                : clamp(start[ln], jd.lo, jd.hi);
+                }
+            } else if constexpr (RT == FKS_ROBOT_SE2) {
+                if (ln < 3) cfg[ln] = (ln == 2) ? fks_math::enforce_continuous_revolute_bounds(start[2]) : start[ln];
+            } else {
+                if (ln < 12) cfg[ln] = start[ln];
             }
-        } else if constexpr (RT == FKS_ROBOT_SE2) {
-            if (ln < 3) cfg[ln] = (ln == 2) ? fks_math::enforce_continuous_revolute_bounds(start[2]) : start[ln];
         } else {
-            if (ln < 12) cfg[ln] = start[ln];
+            /* resume: configuration from out_q, controller state and per-particle totals
+             * from seg_state (bit-exact: the step loop below recomputes FK at its start) */
+            if (ln < W) cfg[ln] = A.out_q[local * (uint64_t)W + ln];
+            s.pid_integral = (ln < D) ? st[ln] : 0.0;
+            s.pid_last = (ln < D) ? st[D + ln] : 0.0;
+            const uint64_t* sw = reinterpret_cast<const uint64_t*>(st + 2 * D);
+            const uint64_t flags = sw[0];
+            collided = (flags & 1ull) != 0;
+            any_failed = (flags & 2ull) != 0;
+            micro_before = sw[1];
+            resolver_before = sw[2];
         }
         wsync();
         double* Tcur = s.lds + s.A->L.Tcur;
         double* Tprev = s.lds + s.A->L.Tprev;
-        bool collided = false;
-        bool any_failed = false;
+        bool ended = false;
         /* ForwardSimulateMutableRobot (SPCS:843-919) */
-        for (uint32_t step = 0; step < A.T; ++step) {
+        for (uint32_t step = step_begin; step < step_end; ++step) {
             s.step = step;
             s.step_count++;
             double* tgt_lds = s.lds + s.A->L.tgt;
@@ -2723,13 +2783,19 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             bool rc = false, rf = false;
             const int status = resolve_step<RT, TR>(s, cfg, res_cfg, A.allow_contacts != 0, &rc, &rf, Tcur, Tprev);
             s.err = wave_or(s.err);
-            if (status != 0 || s.err) break;
+            if (status != 0 || s.err) {
+                ended = true;
+                break;
+            }
             if (A.allow_contacts || !rc) {
                 if (ln < W) cfg[ln] = res_cfg[ln];
                 wsync();
                 if (rc) collided = true;
                 if (rf) {
-                    if (A.S.failed_resolves_end_motion) break;
+                    if (A.S.failed_resolves_end_motion) {
+                        ended = true;
+                        break;
+                    }
                     any_failed = true;
                 } else if (any_failed) {
                     if (s.lane == 0) s.stats[kCntRecovered]++;
@@ -2739,24 +2805,45 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                     wsync();
                     const double dist = config_distance<RT>(s, cfg, tgt_lds);
                     wsync();
-                    if (dist < A.S.simulation_shortcut_distance) break;
+                    if (dist < A.S.simulation_shortcut_distance) {
+                        ended = true;
+                        break;
+                    }
                 }
             } else {
+                ended = true;
                 break;
             }
         }
-        /* outputs */
+        if (step_end == A.T) ended = true;
+        /* outputs (the configuration doubles as the resting state between segments) */
         const uint64_t t_out = __builtin_amdgcn_s_memtime();
         if (ln < W) A.out_q[local * (uint64_t)W + ln] = cfg[ln];
+        const uint64_t micro_total = micro_before + s.micro_count;
+        const uint64_t resolver_total = resolver_before + s.resolver_count;
+        if (!ended) {
+            if (ln < D) {
+                st[ln] = s.pid_integral;
+                st[D + ln] = s.pid_last;
+            }
+            if (ln == 0) {
+                uint64_t* sw = reinterpret_cast<uint64_t*>(st + 2 * D);
+                sw[0] = (collided ? 1ull : 0ull) | (any_failed ? 2ull : 0ull);
+                sw[1] = micro_total;
+                sw[2] = resolver_total;
+            }
+        }
         const uint64_t bytes = wave_sum_u64(s.lane_bytes);
         if (ln == 0) {
-            if (A.out_collided) A.out_collided[local] = collided ? 1 : 0;
-            if (A.out_micro) A.out_micro[local] = (uint32_t)s.micro_count;
-            if (A.out_resolver) A.out_resolver[local] = (uint32_t)s.resolver_count;
-            if (A.out_err) A.out_err[local] = s.err;
-            if constexpr (TR) {
-                A.tr_nsteps[local] = s.tr_steps;
-                A.tr_ncfg[local] = s.tr_cfgs;
+            if (ended) {
+                if (A.out_collided) A.out_collided[local] = collided ? 1 : 0;
+                if (A.out_micro) A.out_micro[local] = (uint32_t)micro_total;
+                if (A.out_resolver) A.out_resolver[local] = (uint32_t)resolver_total;
+                if (A.out_err) A.out_err[local] = s.err;
+                if constexpr (TR) {
+                    A.tr_nsteps[local] = s.tr_steps;
+                    A.tr_ncfg[local] = s.tr_cfgs;
+                }
             }
             for (int k = 0; k < 8; ++k)
                 if (s.stats[k]) atomicAdd(A.counters + k, (unsigned long long)s.stats[k]);
@@ -2771,6 +2858,13 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             s.phase[FKS_PHASE_PARTICLE] += t_end - t_particle;
             for (int k = 0; k < FKS_NUM_PHASES; ++k)
                 if (s.phase[k]) atomicAdd(A.counters + kPhaseBase + k, (unsigned long long)s.phase[k]);
+        }
+        if (nseg > 1) {
+            /* hand the particle to whichever wave draws its next segment */
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (ln == 0)
+                __hip_atomic_store(A.seg_done + local, ended ? nseg : (uint32_t)seg + 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
         wsync();
     }

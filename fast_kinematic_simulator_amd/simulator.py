@@ -144,7 +144,20 @@ class HipParticleContactSimulator:
         """Shader-clock cycles per kernel phase (fks_get_phase_cycles), summed over waves."""
         arr = (ctypes.c_uint64 * _capi.NUM_PHASES)()
         _capi.check(self._lib.fks_get_phase_cycles(self._ctx, 1 if total else 0, arr), self._ctx, "phase cycles")
-        return {name: int(arr[i]) for i, name in enumerate(_capi.PHASE_NAMES) if name != "reserved"}
+        return {name: int(arr[i]) for i, name in enumerate(_capi.PHASE_NAMES)}
+
+    def set_segment_steps(self, controller_steps: int = 0):
+        """Controller steps per scheduling segment of a batch (fks_set_segment_steps;
+        0 = automatic).  Results do not depend on it."""
+        _capi.check(self._lib.fks_set_segment_steps(self._ctx, int(controller_steps)), self._ctx, "segment steps")
+
+    def launch_geometry(self) -> dict:
+        """Resident waves of the persistent simulation grid and LDS bytes per workgroup
+        (fks_get_launch_geometry) for the robot set last."""
+        waves, lds = ctypes.c_uint32(0), ctypes.c_uint64(0)
+        _capi.check(self._lib.fks_get_launch_geometry(self._ctx, ctypes.byref(waves), ctypes.byref(lds)), self._ctx,
+                    "launch geometry")
+        return {"resident_waves": int(waves.value), "lds_bytes_per_group": int(lds.value)}
 
     def set_robot(self, robot: RobotDescription):
         key = id(robot)

@@ -376,10 +376,27 @@ enum fks_phase {
     FKS_PHASE_ENV_ROUNDS_EVALUATED = 12, /* 64-point rounds read from the SDF */
     FKS_PHASE_CORR_ROUNDS_SKIPPED = 13,  /* correction rounds proven free */
     FKS_PHASE_CORR_ROUNDS_EVALUATED = 14,
-    FKS_PHASE_RESERVED = 15
+    /* residency of the persistent waves: 100 MHz s_memrealtime ticks from a wave's
+     * start to its exit (queue drained), summed over waves; with the kernel time it
+     * gives the share of wave slots kept busy (the batch's tail) */
+    FKS_PHASE_WAVE_RESIDENCY = 15
 };
 /* which: 0 = last call, 1 = sums since fks_create / fks_reset_total_counters */
 fks_status fks_get_phase_cycles(const fks_context* ctx, int which, uint64_t* out /* FKS_NUM_PHASES */);
+/* Launch geometry of the simulation kernel for the robot set last: resident waves of
+ * the persistent grid (CUs x workgroups per CU x waves per workgroup, one particle
+ * per wave at a time) and LDS bytes per workgroup.  Diagnostic (no reference
+ * counterpart); with FKS_PHASE_WAVE_RESIDENCY it gives the busy share of the grid. */
+fks_status fks_get_launch_geometry(const fks_context* ctx, uint32_t* resident_waves, uint64_t* lds_bytes_per_group);
+/* Scheduling granularity of fks_forward_simulate*: when a batch holds more particles
+ * than the grid has resident waves, each particle's controller steps are run in
+ * segments of `controller_steps` (0 = automatic: 10 when the batch outnumbers the
+ * resident waves, else whole; nonzero: always), handed out segment-major so
+ * that every particle progresses from the start of the launch and contact-heavy
+ * particles do not start last (the batch's tail).  Results are bit-identical for
+ * every value (the resting state between segments is exact).  No reference
+ * counterpart (SPCS:795 runs each particle whole on one OpenMP thread). */
+fks_status fks_set_segment_steps(fks_context* ctx, uint32_t controller_steps);
 
 /* sums over every call since fks_create / fks_reset_total_counters */
 fks_status fks_get_total_counters(const fks_context* ctx, fks_call_counters* out);

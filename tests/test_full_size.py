@@ -50,11 +50,19 @@ def test_full_batch_blocks_match_oracle(fks_lib, oracle_lib, name, scale, nblock
         c = sim.last_call_counters()
         sim.set_call_index(5)
         g2 = sim.forward_simulate_arrays(wl.robot, wl.starts, wl.targets, True)
+        # the batch outnumbers the resident waves, so the launches above ran in
+        # controller-step segments (fks_set_segment_steps); whole particles must agree
+        sim.set_segment_steps(wl.steps)
+        sim.set_call_index(5)
+        g3 = sim.forward_simulate_arrays(wl.robot, wl.starts, wl.targets, True)
+        c3 = sim.last_call_counters()
     finally:
         sim.close()
     n = len(wl.starts)
     for k in KEYS:
         assert np.array_equal(g[k], g2[k]), k  # deterministic across launches
+        assert np.array_equal(g[k], g3[k]), k  # segmented == whole particles
+    assert c3["microsteps"] == c["microsteps"] and c3["sdf_bytes"] == c["sdf_bytes"]
     assert c["particles"] == n and c["microsteps"] == int(np.sum(g["microsteps"], dtype=np.int64))
     assert c["resolver_iterations"] == int(np.sum(g["resolver_iterations"], dtype=np.int64))
     assert not g["error_flags"].any() and g["collided"].any()

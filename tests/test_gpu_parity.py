@@ -56,3 +56,45 @@ def test_sharded_ids_match_single_run(fks_lib, oracle_lib):
     shard = oracle.forward_simulate(wl.environment(), wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts[16:],
                                     wl.targets, True, first_particle_id=16)
     assert np.array_equal(shard["positions"], full_o["positions"][16:])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("segment_steps", [1, 7])
+@pytest.mark.parametrize("name,scale", CASES)
+def test_segmented_parity(fks_lib, oracle_lib, name, scale, segment_steps):
+    """Controller-step segments (fks_set_segment_steps): the particles are handed
+    from wave to wave between segments; every output and counter stays identical to
+    the oracle, which runs each particle whole (SPCS:795)."""
+    from fast_kinematic_simulator_amd import make_linked_simulator
+
+    wl = W.WORKLOADS[name](scale)
+    sim = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
+    try:
+        sim.set_segment_steps(segment_steps)
+        g, o = run_both(wl, sim=sim, call_index=2)
+    finally:
+        sim.close()
+    print(name, segment_steps, mismatch_report(g, o))
+    assert_identical(g, o)
+    assert g["statistics"] == o["statistics"]
+    for k in ("microsteps", "resolver_iterations", "controller_steps", "sdf_bytes", "error_particles", "least_squares_rows"):
+        assert g["counters"][k] == o["counters"][k], k
+
+
+@pytest.mark.gpu
+def test_segmented_early_stops(fks_lib, oracle_lib):
+    """allow_contacts = false ends particles mid-segment (SPCS:904-909): later
+    segments of an ended particle are skipped, its outputs stay those of the stop."""
+    from fast_kinematic_simulator_amd import make_linked_simulator
+
+    wl = W.cfg1()
+    rng = np.random.default_rng(11)
+    targets = wl.starts + rng.uniform(-0.6, 0.6, size=wl.starts.shape)
+    sim = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
+    try:
+        sim.set_segment_steps(3)
+        g, o = run_both(wl, targets=targets, allow_contacts=False, call_index=5, sim=sim)
+    finally:
+        sim.close()
+    assert_identical(g, o)
+    assert np.any(np.asarray(o["microsteps"]) < np.max(o["microsteps"]))  # some particles stopped early
