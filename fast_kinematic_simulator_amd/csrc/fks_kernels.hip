@@ -902,9 +902,26 @@ __device__ __forceinline__ double wave_min(double v) {
     return (b < a) ? b : a;
 }
 constexpr double kInvalidRound = -1.0e308;
-/* a segment hand-over that waits longer than this (100 MHz s_memrealtime ticks = 20 s)
- * is abandoned and reported (kCntSegmentWaitTimeouts): every wave reaches an exit */
-constexpr uint64_t kSegmentWaitTicks = 2000000000ull;
+constexpr uint64_t kNoTicket = ~0ull;
+/* particle hand-over between waves (possibly on different XCDs, each with its own L2):
+ * the resting state moves through device-coherent (sc1) loads and stores, ordered by
+ * waiting for the stores' completion; no L2 write-back / invalidate is needed */
+__device__ __forceinline__ void store_coherent(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_coherent(const double* p) {
+    return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void store_coherent_u64(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t load_coherent_u64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wait_memory() { __builtin_amdgcn_s_waitcnt(0); }
+constexpr uint32_t kSegClaimed = 0x80000000u; /* seg_done[p]: segment v is being run */
 enum { kSkipCheck = 1, kSkipCorrections = 2 };
 
 /* (link, radius) of round r < 64 from the workgroup's LDS copy of R.rounds */
@@ -2674,47 +2691,68 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     uint32_t* seg_seen = reinterpret_cast<uint32_t*>(s.lds + s.A->L.misc + 30);
     const uint64_t t_resident = __builtin_amdgcn_s_memrealtime();
     const uint32_t nseg = A.nseg;
+    uint64_t carry = kNoTicket; /* the next segment of the particle just run, claimed by this wave */
+    /* call counters are summed per wave and flushed once when the queue is drained
+     * (per-segment device atomics on a handful of shared addresses would serialise) */
+    if (ln < 8) s.stats[ln] = 0;
+    if (ln < FKS_NUM_PHASES) s.phase[ln] = 0;
+    s.lane_bytes = 0;
+    uint64_t w_steps = 0, w_micro = 0, w_resolver = 0, w_lsq = 0, w_errors = 0;
+    wsync();
     while (true) {
         /* ticket t: segment t / n of particle t % n, so every particle's first segment is
          * handed out before any second one (processor sharing over the persistent grid:
-         * a contact-heavy particle no longer starts late and sets the batch's tail) */
-        if (ln == 0) *next_particle = atomicAdd(A.queue, 1ull);
-        wsync();
-        const uint64_t ticket = *next_particle;
-        wsync();
-        const uint64_t seg = (A.n > 0) ? ticket / A.n : (uint64_t)nseg;
-        if (seg >= (uint64_t)nseg) {
-            /* the queue is drained: this wave slot idles from here to the kernel's end */
-            if (ln == 0)
-                atomicAdd(A.counters + kPhaseBase + FKS_PHASE_WAVE_RESIDENCY,
-                          (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t_resident));
-            break;
-        }
-        const uint64_t local = ticket - seg * A.n;
-        if (seg > 0) {
-            /* segment seg-1 of this particle was handed out n tickets earlier; it is
-             * almost always finished (only the last rounds of a batch wait here) */
+         * a contact-heavy particle no longer starts late and sets the batch's tail).
+         * Segment k >= 1 runs on whichever wave claims it first (seg_done CAS): the
+         * ticket's holder if segment k-1 has finished, else the wave finishing k-1 —
+         * no wave ever waits for another. */
+        uint64_t ticket;
+        if (carry != kNoTicket) {
+            ticket = carry;
+            carry = kNoTicket;
+        } else {
             if (ln == 0) {
-                uint32_t v = __hip_atomic_load(A.seg_done + local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (v < (uint32_t)seg) {
-                    const uint64_t t_wait = __builtin_amdgcn_s_memrealtime();
-                    while (v < (uint32_t)seg) {
-                        __builtin_amdgcn_s_sleep(16);
-                        v = __hip_atomic_load(A.seg_done + local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (v < (uint32_t)seg && __builtin_amdgcn_s_memrealtime() - t_wait > kSegmentWaitTicks) {
-                            atomicAdd(A.counters + kCntSegmentWaitTimeouts, 1ull);
-                            v = nseg;
-                        }
-                    }
+                const uint64_t t = __hip_atomic_fetch_add(A.queue, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t sg = (A.n > 0) ? t / A.n : (uint64_t)nseg;
+                uint32_t run = 1;
+                if (sg > 0 && sg < (uint64_t)nseg) {
+                    uint32_t* done = A.seg_done + (t - sg * A.n);
+                    uint32_t v = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    run = (v == (uint32_t)sg &&
+                           __hip_atomic_compare_exchange_strong(done, &v, (uint32_t)sg | kSegClaimed, __ATOMIC_RELAXED,
+                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                              ? 1u
+                              : 0u;
                 }
-                *seg_seen = v;
+                *next_particle = t;
+                *seg_seen = run;
             }
             wsync();
-            const uint32_t seen = *seg_seen;
+            ticket = *next_particle;
+            const uint32_t run = *seg_seen;
             wsync();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            if (seen >= nseg) continue; /* the particle ended in an earlier segment */
+            if ((A.n > 0 ? ticket / A.n : (uint64_t)nseg) >= (uint64_t)nseg) {
+                /* the queue is drained: this wave slot idles from here to the kernel's end */
+                const uint64_t bytes = wave_sum_u64(s.lane_bytes);
+                if (ln == 0) {
+                    s.phase[FKS_PHASE_WAVE_RESIDENCY] += __builtin_amdgcn_s_memrealtime() - t_resident;
+                    for (int k = 0; k < 8; ++k)
+                        if (s.stats[k]) atomicAdd(A.counters + k, (unsigned long long)s.stats[k]);
+                    if (w_steps) atomicAdd(A.counters + kCntSteps, (unsigned long long)w_steps);
+                    if (w_micro) atomicAdd(A.counters + kCntMicrosteps, (unsigned long long)w_micro);
+                    if (w_resolver) atomicAdd(A.counters + kCntResolver, (unsigned long long)w_resolver);
+                    if (w_lsq) atomicAdd(A.counters + kCntLsqRows, (unsigned long long)w_lsq);
+                    if (bytes) atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes);
+                    if (w_errors) atomicAdd(A.counters + kCntErrorParticles, (unsigned long long)w_errors);
+                    for (int k = 0; k < FKS_NUM_PHASES; ++k)
+                        if (s.phase[k]) atomicAdd(A.counters + kPhaseBase + k, (unsigned long long)s.phase[k]);
+                }
+                break;
+            }
+            if (!run) continue; /* segment already run, being run, or left to the wave finishing its predecessor */
         }
+        const uint64_t seg = ticket / A.n;
+        const uint64_t local = ticket - seg * A.n;
         const uint32_t step_begin = (uint32_t)seg * A.seg_steps;
         const uint32_t step_end = (seg + 1 == (uint64_t)nseg) ? A.T : step_begin + A.seg_steps;
         double* st = A.seg_state + local * (uint64_t)A.seg_stride; /* nseg > 1 only */
@@ -2723,13 +2761,10 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         s.tr_steps = 0;
         s.tr_cfgs = 0;
         s.err = 0;
-        s.lane_bytes = 0;
         s.micro_count = 0;
         s.resolver_count = 0;
         s.lsq_rows = 0;
         s.step_count = 0;
-        if (ln < 8) s.stats[ln] = 0;
-        if (ln < FKS_NUM_PHASES) s.phase[ln] = 0;
         const uint64_t t_particle = __builtin_amdgcn_s_memtime();
         s.self_nonempty = false;
         s.tcur_valid = false;
@@ -2756,15 +2791,18 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         } else {
             /* resume: configuration from out_q, controller state and per-particle totals
              * from seg_state (bit-exact: the step loop below recomputes FK at its start) */
-            if (ln < W) cfg[ln] = A.out_q[local * (uint64_t)W + ln];
-            s.pid_integral = (ln < D) ? st[ln] : 0.0;
-            s.pid_last = (ln < D) ? st[D + ln] : 0.0;
+            if (ln < W) cfg[ln] = load_coherent(A.out_q + local * (uint64_t)W + ln);
+            s.pid_integral = (ln < D) ? load_coherent(st + ln) : 0.0;
+            s.pid_last = (ln < D) ? load_coherent(st + D + ln) : 0.0;
             const uint64_t* sw = reinterpret_cast<const uint64_t*>(st + 2 * D);
-            const uint64_t flags = sw[0];
+            const uint64_t flags = load_coherent_u64(sw);
             collided = (flags & 1ull) != 0;
             any_failed = (flags & 2ull) != 0;
-            micro_before = sw[1];
-            resolver_before = sw[2];
+            micro_before = load_coherent_u64(sw + 1);
+            resolver_before = load_coherent_u64(sw + 2);
+            /* the particle's own skip-proof cache (the rounds' last full evaluations) */
+            const int nrc = kRoundState * (R.nrounds < kWave ? R.nrounds : kWave);
+            for (int e = ln; e < nrc; e += kWave) s.lds[A.L.rstate + e] = load_coherent(st + 2 * D + 4 + e);
         }
         wsync();
         double* Tcur = s.lds + s.A->L.Tcur;
@@ -2818,22 +2856,28 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         if (step_end == A.T) ended = true;
         /* outputs (the configuration doubles as the resting state between segments) */
         const uint64_t t_out = __builtin_amdgcn_s_memtime();
-        if (ln < W) A.out_q[local * (uint64_t)W + ln] = cfg[ln];
+        if (ln < W) store_coherent(A.out_q + local * (uint64_t)W + ln, cfg[ln]);
         const uint64_t micro_total = micro_before + s.micro_count;
         const uint64_t resolver_total = resolver_before + s.resolver_count;
         if (!ended) {
             if (ln < D) {
-                st[ln] = s.pid_integral;
-                st[D + ln] = s.pid_last;
+                store_coherent(st + ln, s.pid_integral);
+                store_coherent(st + D + ln, s.pid_last);
             }
             if (ln == 0) {
                 uint64_t* sw = reinterpret_cast<uint64_t*>(st + 2 * D);
-                sw[0] = (collided ? 1ull : 0ull) | (any_failed ? 2ull : 0ull);
-                sw[1] = micro_total;
-                sw[2] = resolver_total;
+                store_coherent_u64(sw, (collided ? 1ull : 0ull) | (any_failed ? 2ull : 0ull));
+                store_coherent_u64(sw + 1, micro_total);
+                store_coherent_u64(sw + 2, resolver_total);
             }
+            const int nrc = kRoundState * (R.nrounds < kWave ? R.nrounds : kWave);
+            for (int e = ln; e < nrc; e += kWave) store_coherent(st + 2 * D + 4 + e, s.lds[A.L.rstate + e]);
         }
-        const uint64_t bytes = wave_sum_u64(s.lane_bytes);
+        w_steps += s.step_count;
+        w_micro += s.micro_count;
+        w_resolver += s.resolver_count;
+        w_lsq += s.lsq_rows;
+        if (s.err) w_errors++;
         if (ln == 0) {
             if (ended) {
                 if (A.out_collided) A.out_collided[local] = collided ? 1 : 0;
@@ -2845,26 +2889,37 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                     A.tr_ncfg[local] = s.tr_cfgs;
                 }
             }
-            for (int k = 0; k < 8; ++k)
-                if (s.stats[k]) atomicAdd(A.counters + k, (unsigned long long)s.stats[k]);
-            atomicAdd(A.counters + kCntSteps, (unsigned long long)s.step_count);
-            atomicAdd(A.counters + kCntMicrosteps, (unsigned long long)s.micro_count);
-            atomicAdd(A.counters + kCntResolver, (unsigned long long)s.resolver_count);
-            atomicAdd(A.counters + kCntLsqRows, (unsigned long long)s.lsq_rows);
-            atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes);
-            if (s.err) atomicAdd(A.counters + kCntErrorParticles, 1ull);
             const uint64_t t_end = __builtin_amdgcn_s_memtime();
             s.phase[FKS_PHASE_OUTPUT] += t_end - t_out;
             s.phase[FKS_PHASE_PARTICLE] += t_end - t_particle;
-            for (int k = 0; k < FKS_NUM_PHASES; ++k)
-                if (s.phase[k]) atomicAdd(A.counters + kPhaseBase + k, (unsigned long long)s.phase[k]);
         }
         if (nseg > 1) {
-            /* hand the particle to whichever wave draws its next segment */
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            if (ln == 0)
-                __hip_atomic_store(A.seg_done + local, ended ? nseg : (uint32_t)seg + 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            /* publish the resting state; if the next segment's ticket is already out, claim
+             * the segment and run it here (its holder, if it looked earlier, skipped it) */
+            wait_memory(); /* every lane's state stores have completed */
+            wsync();
+            if (ln == 0) {
+                uint32_t nv = ended ? nseg : (uint32_t)seg + 1u;
+                __hip_atomic_store(A.seg_done + local, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                wait_memory(); /* the store is visible before the ticket counter is read (Dekker with the holder) */
+                uint32_t cont = 0;
+                if (!ended) {
+                    /* a contact-heavy segment (many resolver iterations) keeps its wave: the
+                     * particle's next segment is claimed at once instead of waiting for its
+                     * ticket, so the longest particles are not paced by the round-robin */
+                    const bool heavy = A.seg_heavy_resolver != 0 && s.resolver_count >= A.seg_heavy_resolver;
+                    const uint64_t next_ticket = (seg + 1) * A.n + local;
+                    const uint64_t issued =
+                        heavy ? ~0ull : __hip_atomic_load(A.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (issued > next_ticket &&
+                        __hip_atomic_compare_exchange_strong(A.seg_done + local, &nv, nv | kSegClaimed, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                        cont = 1;
+                }
+                *seg_seen = cont;
+            }
+            wsync();
+            if (*seg_seen) carry = (seg + 1) * A.n + local;
         }
         wsync();
     }
