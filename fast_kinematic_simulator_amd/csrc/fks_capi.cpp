@@ -905,6 +905,8 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
         a.nseg = (a.T + k - 1u) / k;
         a.seg_heavy_resolver = kHeavyResolverPerStep * k;
         if (const char* h = std::getenv("FKS_SEGMENT_HEAVY_PER_STEP")) a.seg_heavy_resolver = (uint32_t)std::atoi(h) * k;
+        a.seg_heavy_prio = 1;
+        if (const char* h = std::getenv("FKS_SEGMENT_HEAVY_PRIO")) a.seg_heavy_prio = (uint32_t)std::atoi(h);
     }
     if (a.nseg > 1) {
         const size_t words = (size_t)n * a.seg_stride;

@@ -273,6 +273,8 @@ struct SimArgs {
     uint32_t seg_steps, nseg;
     uint32_t seg_stride;          /* doubles per particle in seg_state */
     uint32_t seg_heavy_resolver;  /* resolver iterations that mark a segment contact-heavy (0: off) */
+    uint32_t seg_heavy_prio;      /* waves carrying a heavy particle raise their issue priority */
+    uint32_t seg_pad;
     double* scratch;
     uint64_t scratch_per_wave; /* doubles */
     uint32_t row_cap;          /* 3 * P */

@@ -2914,12 +2914,21 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                     if (issued > next_ticket &&
                         __hip_atomic_compare_exchange_strong(A.seg_done + local, &nv, nv | kSegClaimed, __ATOMIC_RELAXED,
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                        cont = 1;
+                        cont = heavy ? 2u : 1u;
                 }
                 *seg_seen = cont;
             }
             wsync();
-            if (*seg_seen) carry = (seg + 1) * A.n + local;
+            const uint32_t cont = *seg_seen;
+            if (cont) carry = (seg + 1) * A.n + local;
+            /* a wave carrying a contact-heavy particle issues first on its SIMD: the
+             * longest particles finish sooner, the batch's tail shrinks */
+            if (A.seg_heavy_prio) {
+                if (cont == 2u)
+                    __builtin_amdgcn_s_setprio(2);
+                else
+                    __builtin_amdgcn_s_setprio(0);
+            }
         }
         wsync();
     }

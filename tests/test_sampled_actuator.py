@@ -80,9 +80,10 @@ def test_oracle_uncovered_command_flags_error():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("segment_steps", [0, 4])
 @pytest.mark.parametrize("name,scale,narrow", [("cfg1", 0.25, False), ("cfg2", 32 / 4096, False), ("cfg3", 16 / 65536, False),
                                                ("cfg4", 16 / 1048576, False), ("cfg1", 0.125, True)])
-def test_gpu_sampled_actuator_matches_oracle(fks_lib, name, scale, narrow):
+def test_gpu_sampled_actuator_matches_oracle(fks_lib, name, scale, narrow, segment_steps):
     import oracle
     from fast_kinematic_simulator_amd import make_linked_simulator
 
@@ -95,6 +96,7 @@ def test_gpu_sampled_actuator_matches_oracle(fks_lib, name, scale, narrow):
     env = wl.environment()
     sim = make_linked_simulator(env, wl.solver, wl.controller_frequency, wl.seed)
     try:
+        sim.set_segment_steps(segment_steps)  # 4: particles handed between waves every 4 steps
         sim.set_call_index(0)
         g = sim.forward_simulate_arrays(robot, wl.starts, wl.targets, True)
     finally:

@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--segment-steps", type=int, nargs="*", default=[0])
     ap.add_argument("--heavy-per-step", type=int, nargs="*", default=[-1],
                     help="FKS_SEGMENT_HEAVY_PER_STEP values to try (-1: library default, 0: off)")
+    ap.add_argument("--prio", type=int, nargs="*", default=[-1], help="FKS_SEGMENT_HEAVY_PRIO values (-1: default)")
     ap.add_argument("--save", default="", help="write per-particle microsteps / resolver iterations (.npz)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -63,14 +64,16 @@ def main():
     ms1, ph1, m1, _ = run(sim, wl, 1, dev)
     for seg in args.segment_steps:
         for heavy in args.heavy_per_step:
-            if heavy >= 0:
-                os.environ["FKS_SEGMENT_HEAVY_PER_STEP"] = str(heavy)
-            else:
-                os.environ.pop("FKS_SEGMENT_HEAVY_PER_STEP", None)
+          for prio in args.prio:
+            for var, val in (("FKS_SEGMENT_HEAVY_PER_STEP", heavy), ("FKS_SEGMENT_HEAVY_PRIO", prio)):
+                if val >= 0:
+                    os.environ[var] = str(val)
+                else:
+                    os.environ.pop(var, None)
             sim.set_segment_steps(seg)
             ms, ph, m, r = run(sim, wl, args.particles, dev)
             ms, ph, m, r = run(sim, wl, args.particles, dev)
-            report(args, sim, f"{seg}/{heavy}", ms, ph, m, r, ms1, ph1, m1)
+            report(args, sim, f"{seg}/{heavy}/{prio}", ms, ph, m, r, ms1, ph1, m1)
 
 
 def report(args, sim, seg, ms, ph, m, r, ms1, ph1, m1):
