@@ -2926,6 +2926,8 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             if (A.seg_heavy_prio) {
                 if (cont == 2u)
                     __builtin_amdgcn_s_setprio(2);
+                else if (cont == 1u && A.seg_heavy_prio > 1u)
+                    __builtin_amdgcn_s_setprio(1); /* a particle that fell behind the round-robin */
                 else
                     __builtin_amdgcn_s_setprio(0);
             }
