@@ -64,6 +64,11 @@ def test_argument_validation(fks_lib):
     assert fks_lib.fks_default_solver_params(None) == 1
     h = ctypes.c_void_p()
     assert fks_lib.fks_env_build(None, 0, -1.0, None, None, ctypes.byref(h)) == 1
+    # scheduling knob and grid diagnostics (no reference counterpart)
+    assert fks_lib.fks_set_segment_steps(None, 10) == 1
+    waves, lds = ctypes.c_uint32(0), ctypes.c_uint64(0)
+    assert fks_lib.fks_get_launch_geometry(None, ctypes.byref(waves), ctypes.byref(lds)) == 1
+    assert _capi.PHASE_NAMES[15] == "wave_residency" and len(_capi.PHASE_NAMES) == _capi.NUM_PHASES
 
 
 def test_create_without_gpu_reports_no_device(fks_lib):
