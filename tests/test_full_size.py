@@ -2,8 +2,8 @@
 
 The oracle cannot re-simulate 65,536 particles x 200 steps in seconds, but the
 result of a particle depends only on its inputs and its global id (the RNG is keyed
-by (seed, call index, particle id, step, microstep, dof)).  So the full cfg3 batch
-(and a full per-GPU cfg5 shard) runs on the GPU, and randomly placed blocks of it
+by (seed, call index, particle id, step, microstep, dof)).  So the full cfg2 and cfg3
+batches (and full per-GPU cfg4 and cfg5 shards) run on the GPU, and randomly placed blocks of them
 are re-simulated by the oracle with first_particle_id = the block's offset: every
 output of those particles must be bit-identical.  The full batch must also be
 deterministic (two launches, identical bytes) and its per-particle counters must
@@ -39,7 +39,8 @@ def _blocks_match_oracle(wl, g, blocks, call_index):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,scale,nblocks,block", [("cfg3", 1.0, 4, 16), ("cfg5", 131072 / 1048576, 2, 6)])
+@pytest.mark.parametrize("name,scale,nblocks,block", [("cfg2", 1.0, 3, 16), ("cfg3", 1.0, 4, 16),
+                                                      ("cfg4", 131072 / 1048576, 3, 8), ("cfg5", 131072 / 1048576, 2, 6)])
 def test_full_batch_blocks_match_oracle(fks_lib, oracle_lib, name, scale, nblocks, block):
     wl = W.WORKLOADS[name](scale)
     wl._env = W.SCENES[name](device=0)  # the GPU build: same bytes as the host's (test_env_gpu.py), seconds faster at 512^3
