@@ -43,6 +43,7 @@ PARTICLE_ERR_SELF_CAPACITY = 0x10
 PARTICLE_ERR_KEY_RANGE = 0x20
 PARTICLE_ERR_MICROSTEP_CAP = 0x40
 PARTICLE_ERR_SELF_SINGULAR = 0x80
+PARTICLE_ERR_NO_NOISE_BIN = 0x100
 
 
 class SolverParams(ctypes.Structure):
@@ -162,6 +163,8 @@ class CallCounters(ctypes.Structure):
         ("call_ms", c_double),
         ("calls", c_uint64),
         ("least_squares_rows", c_uint64),
+        ("self_collision_checks", c_uint64),
+        ("self_corrected_points", c_uint64),
     ]
 
     def as_dict(self):
@@ -217,6 +220,12 @@ PROTOTYPES = [
          POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)],
     ),
     (
+        "fks_forward_simulate_mutable",
+        c_int32,
+        [c_void_p, POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_int32, POINTER(c_double), POINTER(c_double),
+         POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)],
+    ),
+    (
         "fks_forward_simulate_device",
         c_int32,
         [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -227,6 +236,12 @@ PROTOTYPES = [
         c_int32,
         [c_void_p, POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_int32, POINTER(c_double), POINTER(c_uint8),
          POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32), POINTER(Trace)],
+    ),
+    (
+        "fks_forward_simulate_traced_mutable",
+        c_int32,
+        [c_void_p, POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_int32, POINTER(c_double), POINTER(c_double),
+         POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32), POINTER(Trace)],
     ),
     ("fks_check_config_collision", c_int32,
      [c_void_p, POINTER(c_double), c_uint64, c_double, POINTER(c_uint8), POINTER(c_uint32)]),
@@ -248,6 +263,8 @@ PROTOTYPES = [
     ("fks_get_phase_cycles", c_int32, [c_void_p, c_int32, POINTER(c_uint64)]),
     ("fks_get_launch_geometry", c_int32, [c_void_p, POINTER(c_uint32), POINTER(c_uint64)]),
     ("fks_set_segment_steps", c_int32, [c_void_p, c_uint32]),
+    ("fks_set_segment_policy", c_int32, [c_void_p, c_uint32, c_uint32]),
+    ("fks_set_individual_jacobians", c_int32, [c_void_p, c_int32]),
     ("fks_env_build", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), POINTER(c_void_p)]),
     ("fks_env_build_gpu", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), c_int32,
                                     POINTER(c_void_p), POINTER(EnvBuildStats)]),

@@ -60,25 +60,38 @@ def build_variant(output: str, defines) -> str:
     return output
 
 
-def build_example(force: bool = False) -> str:
-    """Compile examples/cpp_forward_simulate.cpp (C++ host code over the C-ABI and
-    include/fast_kinematic_simulator_amd/hip_particle_contact_simulator.hpp)."""
+def build_cpp_program(src: str, name: str, force: bool = False, extra_flags=()) -> str:
+    """Compile a host C++ program over the public headers (include/) and link
+    libfks_hip.so: g++ only, no HIP toolchain, as a planner would build against the
+    drop-in.  Output: build/<name>."""
     lib = build_library()
-    src = os.path.join(ROOT, "examples", "cpp_forward_simulate.cpp")
+    src = os.path.join(ROOT, src)
     out_dir = os.path.join(ROOT, "build")
     os.makedirs(out_dir, exist_ok=True)
-    target = os.path.join(out_dir, "cpp_forward_simulate")
-    hdr = os.path.join(ROOT, "include", "fast_kinematic_simulator_amd", "hip_particle_contact_simulator.hpp")
-    capi = os.path.join(ROOT, "include", "fks_capi.h")
+    target = os.path.join(out_dir, name)
+    inc = os.path.join(ROOT, "include")
+    headers = [os.path.join(d, f) for d, _, fs in os.walk(inc) for f in fs]
     if not force and os.path.exists(target) and all(os.path.getmtime(target) >= os.path.getmtime(p)
-                                                    for p in (src, hdr, capi, lib)):
+                                                    for p in [src, lib] + headers):
         return target
-    cmd = ["g++", "-std=c++17", "-O2", "-Wall", f"-I{os.path.join(ROOT, 'include')}", src, "-o", target, f"-L{PKG}",
-           "-lfks_hip", "-Wl,-rpath,$ORIGIN/../fast_kinematic_simulator_amd", "-Wl,-rpath-link,/opt/rocm/lib"]
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-ffp-contract=off", *extra_flags, f"-I{inc}", src, "-o", target,
+           f"-L{PKG}", "-lfks_hip", "-Wl,-rpath,$ORIGIN/../fast_kinematic_simulator_amd", "-Wl,-rpath-link,/opt/rocm/lib"]
     proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if proc.returncode != 0:
         raise RuntimeError("g++ failed:\n" + proc.stdout[-6000:])
     return target
+
+
+def build_example(force: bool = False) -> str:
+    """Compile examples/cpp_forward_simulate.cpp (C++ host code over the C-ABI and
+    include/fast_kinematic_simulator_amd/hip_particle_contact_simulator.hpp)."""
+    return build_cpp_program(os.path.join("examples", "cpp_forward_simulate.cpp"), "cpp_forward_simulate", force)
+
+
+def build_planner_test(force: bool = False) -> str:
+    """Compile tests/cpp/planner_interface_test.cpp: the planner-side drop-in driven only
+    through std::shared_ptr<SimulatorInterface<...>> (fast_kinematic_simulator.hpp)."""
+    return build_cpp_program(os.path.join("tests", "cpp", "planner_interface_test.cpp"), "planner_interface_test", force)
 
 
 if __name__ == "__main__":

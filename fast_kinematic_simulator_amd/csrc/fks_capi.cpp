@@ -13,7 +13,6 @@
 #include <stdint.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -235,9 +234,13 @@ struct fks_context {
     uint32_t* d_micro = nullptr;
     uint32_t* d_res = nullptr;
     uint32_t* d_err = nullptr;
-    size_t cap_particles = 0, cap_targets = 0;
+    double* d_pid = nullptr; /* fks_forward_simulate_mutable controller state */
+    size_t cap_particles = 0, cap_targets = 0, cap_pid = 0;
     /* controller-step segments: resting particle state between segments */
     uint32_t segment_steps = 0; /* 0 = automatic (kDefaultSegmentSteps) */
+    uint32_t heavy_per_step = kHeavyResolverPerStep; /* fks_set_segment_policy */
+    uint32_t heavy_priority = 1;
+    int32_t individual_jacobians = 0; /* fks_set_individual_jacobians (SPCS:420-423) */
     double* d_seg_state = nullptr;
     uint32_t* d_seg_done = nullptr;
     size_t cap_seg_state = 0, cap_seg_done = 0;
@@ -282,6 +285,9 @@ static void free_staging(fks_context* ctx) {
     ctx->d_coll = nullptr;
     ctx->d_micro = ctx->d_res = ctx->d_err = nullptr;
     ctx->cap_particles = ctx->cap_targets = 0;
+    if (ctx->d_pid) (void)hipFree(ctx->d_pid);
+    ctx->d_pid = nullptr;
+    ctx->cap_pid = 0;
     if (ctx->d_seg_state) (void)hipFree(ctx->d_seg_state);
     if (ctx->d_seg_done) (void)hipFree(ctx->d_seg_done);
     ctx->d_seg_state = nullptr;
@@ -757,7 +763,7 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     HIP_TRY(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     ctx->grid_groups = (uint32_t)(cus * blocks_per_cu);
     ctx->grid_waves = ctx->grid_groups * (uint32_t)fksd::kWavesPerGroup;
-    ctx->scratch_per_wave = fksd::make_scratch_layout(3u * P, R.D, (int)P).total;
+    ctx->scratch_per_wave = fksd::make_scratch_layout(3u * P, R.D, (int)P, G).total;
     HIP_TRY(ctx, hipMalloc((void**)&ctx->d_scratch, (size_t)ctx->grid_waves * ctx->scratch_per_wave * sizeof(double)));
     ctx->R = R;
     ctx->has_robot = true;
@@ -795,6 +801,8 @@ static fks_status settle(fks_context* ctx) {
     ctx->last.sdf_bytes = c[fksd::kCntSdfBytes];
     ctx->last.error_particles = c[fksd::kCntErrorParticles];
     ctx->last.least_squares_rows = c[fksd::kCntLsqRows];
+    ctx->last.self_collision_checks = c[fksd::kCntSelfChecks];
+    ctx->last.self_corrected_points = c[fksd::kCntSelfPoints];
     for (int k = 0; k < FKS_NUM_PHASES; ++k) {
         ctx->phase_last[k] = c[fksd::kPhaseBase + k];
         ctx->phase_total[k] += ctx->phase_last[k];
@@ -811,6 +819,8 @@ static fks_status settle(fks_context* ctx) {
     ctx->total.sdf_bytes += ctx->last.sdf_bytes;
     ctx->total.error_particles += ctx->last.error_particles;
     ctx->total.least_squares_rows += ctx->last.least_squares_rows;
+    ctx->total.self_collision_checks += ctx->last.self_collision_checks;
+    ctx->total.self_corrected_points += ctx->last.self_corrected_points;
     ctx->total.kernel_ms += ctx->last.kernel_ms;
     ctx->total.call_ms += ctx->last.call_ms;
     ctx->total.calls += 1;
@@ -834,7 +844,7 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
                                   uint64_t num_targets, uint64_t first_particle_id, int32_t allow_contacts,
                                   double* d_out_positions, uint8_t* d_out_collided, uint32_t* d_out_microsteps,
                                   uint32_t* d_out_resolver_iterations, uint32_t* d_out_error_flags, void* stream,
-                                  int32_t synchronize, const TraceDev* tr) {
+                                  int32_t synchronize, const TraceDev* tr, double* d_pid_io = nullptr) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
     if (!ctx->has_robot) return fail(ctx, FKS_ERR_NO_ROBOT, "fks_set_robot has not been called");
     if (n > 0 && (!d_starts || !d_targets || !d_out_positions))
@@ -880,7 +890,9 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.n = n;
     a.first_pid = first_particle_id;
     a.allow_contacts = allow_contacts ? 1 : 0;
+    a.individual_jacobians = ctx->individual_jacobians;
     a.out_q = d_out_positions;
+    a.pid_io = d_pid_io;
     a.out_collided = d_out_collided;
     a.out_micro = d_out_microsteps;
     a.out_resolver = d_out_resolver_iterations;
@@ -891,7 +903,7 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
     a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds);
-    a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P);
+    a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     /* controller-step segments: automatically only when the batch outnumbers the
      * resident waves (otherwise every particle has a wave from the start), always
      * when set explicitly (fks_set_segment_steps); traced calls run whole */
@@ -902,11 +914,13 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
         uint32_t k = ctx->segment_steps ? ctx->segment_steps : kDefaultSegmentSteps;
         if (k > a.T) k = a.T;
         a.seg_steps = k;
-        a.nseg = (a.T + k - 1u) / k;
-        a.seg_heavy_resolver = kHeavyResolverPerStep * k;
-        if (const char* h = std::getenv("FKS_SEGMENT_HEAVY_PER_STEP")) a.seg_heavy_resolver = (uint32_t)std::atoi(h) * k;
-        a.seg_heavy_prio = 1;
-        if (const char* h = std::getenv("FKS_SEGMENT_HEAVY_PRIO")) a.seg_heavy_prio = (uint32_t)std::atoi(h);
+        /* T >= 1 and k >= 1: ceil(T / k) without the uint32 wrap of (T + k - 1) / k */
+        a.nseg = (uint32_t)(((uint64_t)a.T - 1u) / k + 1u);
+        /* heavy_per_step <= 65536 (fks_set_segment_policy): the product fits in 64 bits,
+         * and the kernel compares it with a per-segment count of at most 2^32 - 1 */
+        const uint64_t heavy = (uint64_t)ctx->heavy_per_step * k;
+        a.seg_heavy_resolver = (uint32_t)std::min<uint64_t>(heavy, 0xffffffffull);
+        a.seg_heavy_prio = ctx->heavy_priority;
     }
     if (a.nseg > 1) {
         const size_t words = (size_t)n * a.seg_stride;
@@ -1005,7 +1019,7 @@ fks_status fks_check_config_collision_device(fks_context* ctx, const double* d_c
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
     a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds);
-    a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P);
+    a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     *ctx->h_args = a;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice, s));
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, fksd::kCounterWords * sizeof(unsigned long long), s));
@@ -1064,7 +1078,8 @@ fks_status fks_get_last_check_counters(const fks_context* ctx, fks_call_counters
 
 static fks_status simulate_host(fks_context* ctx, const double* starts, uint64_t n, const double* targets, uint64_t num_targets,
                                 int32_t allow_contacts, double* out_positions, uint8_t* out_collided, uint32_t* out_microsteps,
-                                uint32_t* out_resolver_iterations, uint32_t* out_error_flags, const TraceDev* tr = nullptr) {
+                                uint32_t* out_resolver_iterations, uint32_t* out_error_flags, const TraceDev* tr = nullptr,
+                                double* controller_state = nullptr) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
     if (!ctx->has_robot) return fail(ctx, FKS_ERR_NO_ROBOT, "fks_set_robot has not been called");
     if (n > 0 && (!starts || !targets || !out_positions)) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "null host buffer");
@@ -1095,9 +1110,19 @@ static fks_status simulate_host(fks_context* ctx, const double* starts, uint64_t
     }
     HIP_TRY(ctx, hipMemcpy(ctx->d_starts, starts, n * W * sizeof(double), hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(ctx->d_targets, targets, nt * W * sizeof(double), hipMemcpyHostToDevice));
+    const size_t pid_words = (size_t)n * 2u * (size_t)ctx->R.D;
+    if (controller_state) {
+        if (pid_words > ctx->cap_pid) {
+            HIP_TRY(ctx, ensure(&ctx->d_pid, pid_words));
+            ctx->cap_pid = pid_words;
+        }
+        HIP_TRY(ctx, hipMemcpy(ctx->d_pid, controller_state, pid_words * sizeof(double), hipMemcpyHostToDevice));
+    }
     st = simulate_device(ctx, ctx->d_starts, n, ctx->d_targets, nt, 0, allow_contacts, ctx->d_out, ctx->d_coll, ctx->d_micro,
-                         ctx->d_res, ctx->d_err, nullptr, 1, tr);
+                         ctx->d_res, ctx->d_err, nullptr, 1, tr, controller_state ? ctx->d_pid : nullptr);
     if (st != FKS_OK) return st;
+    if (controller_state)
+        HIP_TRY(ctx, hipMemcpy(controller_state, ctx->d_pid, pid_words * sizeof(double), hipMemcpyDeviceToHost));
     HIP_TRY(ctx, hipMemcpy(out_positions, ctx->d_out, n * W * sizeof(double), hipMemcpyDeviceToHost));
     if (out_collided) HIP_TRY(ctx, hipMemcpy(out_collided, ctx->d_coll, n, hipMemcpyDeviceToHost));
     if (out_microsteps) HIP_TRY(ctx, hipMemcpy(out_microsteps, ctx->d_micro, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -1123,11 +1148,24 @@ fks_status fks_reverse_simulate(fks_context* ctx, const double* starts, uint64_t
                          out_resolver_iterations, out_error_flags);
 }
 
-/* ForwardSimulateRobot with enable_tracing = true (SPCS:824-829), batched */
-fks_status fks_forward_simulate_traced(fks_context* ctx, const double* starts, uint64_t n, const double* targets,
-                                       uint64_t num_targets, int32_t allow_contacts, double* out_positions,
-                                       uint8_t* out_collided, uint32_t* out_microsteps, uint32_t* out_resolver_iterations,
-                                       uint32_t* out_error_flags, const fks_trace* trace) {
+/* ForwardSimulateMutableRobot (SPCS:843-919) over a batch of robots that keep their controllers */
+fks_status fks_forward_simulate_mutable(fks_context* ctx, const double* starts, uint64_t n, const double* targets,
+                                        uint64_t num_targets, int32_t allow_contacts, double* controller_state,
+                                        double* out_positions, uint8_t* out_collided, uint32_t* out_microsteps,
+                                        uint32_t* out_resolver_iterations, uint32_t* out_error_flags) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    if (n > 0 && !controller_state) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "null controller state");
+    return simulate_host(ctx, starts, n, targets, num_targets, allow_contacts, out_positions, out_collided, out_microsteps,
+                         out_resolver_iterations, out_error_flags, nullptr, controller_state);
+}
+
+}  // extern "C"
+
+/* the traced calls: device trace buffers around simulate_host, copied to the caller's */
+static fks_status simulate_traced(fks_context* ctx, const double* starts, uint64_t n, const double* targets, uint64_t num_targets,
+                                  int32_t allow_contacts, double* controller_state, double* out_positions, uint8_t* out_collided,
+                                  uint32_t* out_microsteps, uint32_t* out_resolver_iterations, uint32_t* out_error_flags,
+                                  const fks_trace* trace) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
     if (!ctx->has_robot) return fail(ctx, FKS_ERR_NO_ROBOT, "fks_set_robot has not been called");
     if (!trace || !trace->num_steps || !trace->num_configs ||
@@ -1163,7 +1201,7 @@ fks_status fks_forward_simulate_traced(fks_context* ctx, const double* starts, u
         return hip_fail(ctx, e, "trace buffers");
     }
     fks_status st = simulate_host(ctx, starts, n, targets, num_targets, allow_contacts, out_positions, out_collided,
-                                  out_microsteps, out_resolver_iterations, out_error_flags, &tr);
+                                  out_microsteps, out_resolver_iterations, out_error_flags, &tr, controller_state);
     if (st == FKS_OK && n > 0) {
         struct Copy {
             void* dst;
@@ -1186,6 +1224,28 @@ fks_status fks_forward_simulate_traced(fks_context* ctx, const double* starts, u
     }
     release();
     return st;
+}
+
+extern "C" {
+
+/* ForwardSimulateRobot with enable_tracing = true (SPCS:824-829), batched */
+fks_status fks_forward_simulate_traced(fks_context* ctx, const double* starts, uint64_t n, const double* targets,
+                                       uint64_t num_targets, int32_t allow_contacts, double* out_positions,
+                                       uint8_t* out_collided, uint32_t* out_microsteps, uint32_t* out_resolver_iterations,
+                                       uint32_t* out_error_flags, const fks_trace* trace) {
+    return simulate_traced(ctx, starts, n, targets, num_targets, allow_contacts, nullptr, out_positions, out_collided,
+                           out_microsteps, out_resolver_iterations, out_error_flags, trace);
+}
+
+/* ForwardSimulateMutableRobot with enable_tracing = true (SPCS:843-919) */
+fks_status fks_forward_simulate_traced_mutable(fks_context* ctx, const double* starts, uint64_t n, const double* targets,
+                                               uint64_t num_targets, int32_t allow_contacts, double* controller_state,
+                                               double* out_positions, uint8_t* out_collided, uint32_t* out_microsteps,
+                                               uint32_t* out_resolver_iterations, uint32_t* out_error_flags,
+                                               const fks_trace* trace) {
+    if (ctx && n > 0 && !controller_state) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "null controller state");
+    return simulate_traced(ctx, starts, n, targets, num_targets, allow_contacts, controller_state, out_positions, out_collided,
+                           out_microsteps, out_resolver_iterations, out_error_flags, trace);
 }
 
 fks_status fks_robot_sizes(const fks_context* ctx, int32_t* num_links, int32_t* num_points, int32_t* num_dofs,
@@ -1242,7 +1302,7 @@ fks_status fks_kinematics(fks_context* ctx, int32_t mode, const double* configs,
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
     a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds);
-    a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P);
+    a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     a.kin_mode = mode;
     a.kin_out = d_out;
     *ctx->h_args = a;
@@ -1330,6 +1390,21 @@ fks_status fks_get_phase_cycles(const fks_context* ctx, int which, uint64_t* out
 fks_status fks_set_segment_steps(fks_context* ctx, uint32_t controller_steps) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
     ctx->segment_steps = controller_steps;
+    return FKS_OK;
+}
+
+fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_step, uint32_t heavy_priority) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    if (heavy_resolver_per_step > 65536u) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "heavy_resolver_per_step > 65536");
+    if (heavy_priority > 2u) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "heavy_priority must be 0, 1 or 2");
+    ctx->heavy_per_step = heavy_resolver_per_step;
+    ctx->heavy_priority = heavy_priority;
+    return FKS_OK;
+}
+
+fks_status fks_set_individual_jacobians(fks_context* ctx, int32_t simulate_with_individual_jacobians) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    ctx->individual_jacobians = simulate_with_individual_jacobians ? 1 : 0;
     return FKS_OK;
 }
 

@@ -193,6 +193,20 @@ inline
     return l;
 }
 
+/* dense workspace (doubles) of the self-collision impulse solve of one cell
+ * (ExtractSelfCollidingPoints SPCS:1054-1150) when a link may touch up to n = G - 1
+ * others: C, N, M, V, N^T, C^T, M^-1, two products, the Gauss-Jordan tableau (2 rows^2),
+ * A^-1, impulses and dv, rows = 3 (n + 1).  The reference's maps are unbounded; so is
+ * this (it is sized by the robot, not capped). */
+inline
+#if defined(__HIPCC__)
+    __host__ __device__
+#endif
+    uint64_t self_dense_words(int G) {
+    const uint64_t n = (uint64_t)(G > 1 ? G - 1 : 1), rows = 3 * (n + 1), cc = 3 * n;
+    return 2 * rows * cc + 2 * cc * n + 6 * rows * rows + 2 * rows + n * n + n + 64;
+}
+
 /* per-wave scratch layout (doubles) */
 struct ScratchLayout {
     uint64_t J, b, keys, corr, flag, cand, list, dense, total;
@@ -201,7 +215,7 @@ inline
 #if defined(__HIPCC__)
     __host__ __device__
 #endif
-    ScratchLayout make_scratch_layout(uint32_t row_cap, int D, int P) {
+    ScratchLayout make_scratch_layout(uint32_t row_cap, int D, int P, int G) {
     ScratchLayout l;
     uint64_t o = 0;
     l.J = o;
@@ -219,7 +233,7 @@ inline
     l.list = o;
     o += (uint64_t)P;
     l.dense = o;
-    o += 8192;
+    o += (G > 1) ? self_dense_words(G) : 8;
     l.total = (o + 7) & ~7ull;
     return l;
 }
@@ -253,8 +267,12 @@ struct SimArgs {
     uint64_t n;
     uint64_t first_pid;
     int32_t allow_contacts;
-    int32_t pad1;
+    int32_t individual_jacobians; /* ComputeResolverCorrectionStepIndividualJacobians (SPCS:1966-1988) */
     double* out_q;
+    /* ForwardSimulateMutableRobot (fks_forward_simulate_mutable): per particle 2D doubles,
+     * the PID error integrals then last errors the particle starts with, overwritten
+     * with its controllers' state when it stops; NULL = ResetPosition (zeroed PIDs) */
+    double* pid_io;
     uint8_t* out_collided;
     uint32_t* out_micro;
     uint32_t* out_resolver;
@@ -311,6 +329,8 @@ enum {
     kCntSdfBytes,
     kCntErrorParticles,
     kCntLsqRows,
+    kCntSelfChecks,
+    kCntSelfPoints,
     kNumCounters = 16
 };
 

@@ -428,6 +428,7 @@ struct Sim {
     uint32_t err;          /* per-lane error bits, OR-reduced at decision points */
     uint64_t lane_bytes;   /* per-lane algorithmic SDF bytes */
     uint64_t micro_count, resolver_count, step_count, lsq_rows;
+    uint64_t self_checks, self_points; /* non-empty self-collision maps, self-corrected points (wave totals) */
     uint32_t* stats; /* LDS, lane 0 updates */
     uint64_t* phase; /* LDS, FKS_NUM_PHASES cycle sums, lane 0 updates */
     const JointDev* joints;          /* LDS copy of R.joints */
@@ -904,8 +905,19 @@ __device__ __forceinline__ double wave_min(double v) {
 constexpr double kInvalidRound = -1.0e308;
 constexpr uint64_t kNoTicket = ~0ull;
 /* particle hand-over between waves (possibly on different XCDs, each with its own L2):
- * the resting state moves through device-coherent (sc1) loads and stores, ordered by
- * waiting for the stores' completion; no L2 write-back / invalidate is needed */
+ * the resting state moves through agent-scope atomic loads and stores, which gfx942 /
+ * gfx950 issue with sc1 (coherent across XCDs at the memory side), so no L2 write-back
+ * or invalidate is needed.  Between the state and the seg_done flag that publishes it,
+ * publish_fence() is a workgroup-scope release fence: a compiler barrier for every
+ * memory operation plus s_waitcnt vmcnt(0), i.e. the state stores have completed at the
+ * coherence point before the flag store issues; claim_fence() is the matching acquire
+ * after the claimant's CAS.  Formally the HIP model would want agent-scope
+ * release/acquire (buffer_wbl2 / buffer_inv on these targets, measured 10-20 % slower);
+ * the workgroup-scope fences are exact only because every access on both sides is an
+ * sc1 atomic, which is why other targets refuse to compile this file (below). */
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "the segment hand-over relies on the gfx942/gfx950 memory model (sc1 atomics, see above)"
+#endif
 __device__ __forceinline__ void store_coherent(double* p, double v) {
     __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -920,7 +932,8 @@ __device__ __forceinline__ void store_coherent_u64(uint64_t* p, uint64_t v) {
 __device__ __forceinline__ uint64_t load_coherent_u64(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void wait_memory() { __builtin_amdgcn_s_waitcnt(0); }
+__device__ __forceinline__ void publish_fence() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
+__device__ __forceinline__ void claim_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); }
 constexpr uint32_t kSegClaimed = 0x80000000u; /* seg_done[p]: segment v is being run */
 enum { kSkipCheck = 1, kSkipCorrections = 2 };
 
@@ -1203,11 +1216,8 @@ __device__ __noinline__ uint32_t extract_cell(const SimArgs* __restrict__ Ap, do
     }
     if (ncollide_links < 2) return 0;
     (*cells)++;
-    if (*cells > FKS_MAX_SELF_CELLS || ng > FKS_MAX_SELF_LINKS) {
-        return FKS_PARTICLE_ERR_SELF_CAPACITY;
-    }
     const double tm = A.time_multiplier;
-    D4 mom[FKS_MAX_SELF_LINKS];
+    D4 mom[kMaxGeoms];
     for (int a = 0; a < ng; ++a) {
         const uint64_t disallowed = present & ~gp(R.allowed_mask)[geo[a]] & ~(1ull << geo[a]);
         mom[a] = D4{0.0, 0.0, 0.0, 0.0};
@@ -1223,7 +1233,7 @@ __device__ __noinline__ uint32_t extract_cell(const SimArgs* __restrict__ Ap, do
     for (int a = 0; a < ng; ++a) {
         const uint64_t disallowed = present & ~gp(R.allowed_mask)[geo[a]] & ~(1ull << geo[a]);
         if (!disallowed) continue;
-        int others[FKS_MAX_SELF_LINKS];
+        int others[kMaxGeoms];
         int n = 0;
         for (int b = 0; b < ng; ++b)
             if ((disallowed >> geo[b]) & 1ull) others[n++] = b;
@@ -1491,6 +1501,7 @@ __device__ bool check_collision(Sim& s, const double* Tp, const double* Tc) {
         tock(s, FKS_PHASE_SELF_CHECK, t0);
     }
     s.self_nonempty = self;
+    if (self) s.self_checks++;
     return env || self;
 }
 
@@ -1577,6 +1588,7 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
             if (has_env) pcorr = D3{pcorr.x + ecorr.x, pcorr.y + ecorr.y, pcorr.z + ecorr.z};
         }
         const uint64_t m = __ballot(has);
+        if (s.self_nonempty) s.self_points += (uint64_t)__popcll(__ballot(has && flag[i] != 0.0));
         if (has) {
             const uint32_t row = (rows + (uint32_t)__popcll(m & ((1ull << ln) - 1ull))) * 3u;
             bv[row + 0] = pcorr.x;
@@ -1855,12 +1867,12 @@ __device__ __forceinline__ int wave_first_argmax(double val, int ln, int first, 
  * in their lanes.  Same arithmetic as qr_solve_regs / qr_solve, bit for bit. */
 template <int RM>
 __device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
-                                           uint32_t Rn, double* x) {
+                                           uint32_t Rn, double* x, uint32_t row0 = 0) {
     const SimArgs& A = *Ap;
     const int D = A.R.D;
     const uint32_t rc = A.row_cap;
-    const FKS_GLOBAL double* Jm = gp(scratch) + A.SL.J;
-    const FKS_GLOBAL double* bv = gp(scratch) + A.SL.b;
+    const FKS_GLOBAL double* Jm = gp(scratch) + A.SL.J + row0; /* rows [row0, row0 + Rn) */
+    const FKS_GLOBAL double* bv = gp(scratch) + A.SL.b + row0;
     int32_t* perm = reinterpret_cast<int32_t*>(lds + A.L.ints);
     int32_t* transp = perm + kMaxDofs;
     const bool isc = ln < D, isb = ln == D;
@@ -2018,14 +2030,16 @@ __device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double
     wsync();
 }
 
-/* ColPivHouseholderQR::solve (Eigen 3.2 / 3.3-beta1), rows lane-strided; x -> LDS */
-__device__ __noinline__ void qr_solve(const SimArgs* __restrict__ Ap, double* lds, double* scratch, int ln, uint32_t Rn, double* x) {
+/* ColPivHouseholderQR::solve (Eigen 3.2 / 3.3-beta1), rows lane-strided; x -> LDS.
+ * Works in place on rows [row0, row0 + Rn) of the stacked system in scratch. */
+__device__ __noinline__ void qr_solve(const SimArgs* __restrict__ Ap, double* lds, double* scratch, int ln, uint32_t Rn, double* x,
+                                      uint32_t row0 = 0) {
     const SimArgs& A = *Ap;
     const int D = A.R.D;
     const uint32_t rc = A.row_cap;
     const ScratchLayout& SL = A.SL;
-    double* Jm = scratch + SL.J;
-    double* c = scratch + SL.b;
+    double* Jm = scratch + SL.J + row0;
+    double* c = scratch + SL.b + row0;
     double* colsq = lds + A.L.colsq;
     double* hco = lds + A.L.hcoef;
     int32_t* perm = reinterpret_cast<int32_t*>(lds + A.L.ints);
@@ -2199,6 +2213,26 @@ __device__ __noinline__ void qr_solve(const SimArgs* __restrict__ Ap, double* ld
     wsync();
 }
 
+/* ComputeResolverCorrectionStepIndividualJacobians (SPCS:1966-1988): one
+ * ColPivHouseholderQR solve per corrected point (its 3 x D block of the stacked
+ * system), the steps summed in point order (the first assigned, then raw + step).
+ * No corrected point: the zero step (as the stacked solve of an empty system). */
+__device__ __noinline__ void individual_jacobians_solve(Sim& s, uint32_t Rn, double* x) {
+    const int ln = s.lane;
+    const int D = s.A->R.D;
+    double* acc = s.lds + s.A->L.real;
+    for (uint32_t r0 = 0; r0 < Rn; r0 += 3u) {
+        if (D < kWave)
+            qr_solve_cols<8>(s.A, s.lds, s.scratch, ln, 3u, x, r0);
+        else
+            qr_solve(s.A, s.lds, s.scratch, ln, 3u, x, r0);
+        if (ln < D) acc[ln] = (r0 == 0u) ? x[ln] : acc[ln] + x[ln];
+        wsync();
+    }
+    if (ln < D) x[ln] = (Rn == 0u) ? 0.0 : acc[ln];
+    wsync();
+}
+
 /* one controller step: ResolveForwardSimulation (SPCS:1546-1816).
  * returns 0 ok, 1 error; sets collided/failed; result config in res_cfg */
 template <int RT, bool TR>
@@ -2300,7 +2334,9 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
                 tock(s, FKS_PHASE_CORRECTIONS, t0);
                 if (s.err) return 1;
                 t0 = tick();
-                if (Rn <= 8u && R.D < kWave)
+                if (A.individual_jacobians) {
+                    individual_jacobians_solve(s, Rn, x);
+                } else if (Rn <= 8u && R.D < kWave)
                     qr_solve_cols<8>(s.A, s.lds, s.scratch, ln, Rn, x);
                 else if (Rn <= 16u && R.D < kWave)
                     qr_solve_cols<16>(s.A, s.lds, s.scratch, ln, Rn, x);
@@ -2692,12 +2728,15 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     const uint64_t t_resident = __builtin_amdgcn_s_memrealtime();
     const uint32_t nseg = A.nseg;
     uint64_t carry = kNoTicket; /* the next segment of the particle just run, claimed by this wave */
+    bool carry_heavy = false;   /* ... and whether the segment just run was contact-heavy */
     /* call counters are summed per wave and flushed once when the queue is drained
      * (per-segment device atomics on a handful of shared addresses would serialise) */
     if (ln < 8) s.stats[ln] = 0;
     if (ln < FKS_NUM_PHASES) s.phase[ln] = 0;
     s.lane_bytes = 0;
     uint64_t w_steps = 0, w_micro = 0, w_resolver = 0, w_lsq = 0, w_errors = 0;
+    s.self_checks = 0;
+    s.self_points = 0;
     wsync();
     while (true) {
         /* ticket t: segment t / n of particle t % n, so every particle's first segment is
@@ -2707,9 +2746,13 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
          * ticket's holder if segment k-1 has finished, else the wave finishing k-1 —
          * no wave ever waits for another. */
         uint64_t ticket;
+        uint32_t prio = 0;
         if (carry != kNoTicket) {
             ticket = carry;
             carry = kNoTicket;
+            /* a wave carrying a contact-heavy particle issues first on its SIMD: the
+             * longest particles finish sooner, the batch's tail shrinks */
+            prio = carry_heavy ? 2u : (A.seg_heavy_prio > 1u ? 1u : 0u);
         } else {
             if (ln == 0) {
                 const uint64_t t = __hip_atomic_fetch_add(A.queue, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2744,12 +2787,24 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                     if (w_lsq) atomicAdd(A.counters + kCntLsqRows, (unsigned long long)w_lsq);
                     if (bytes) atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes);
                     if (w_errors) atomicAdd(A.counters + kCntErrorParticles, (unsigned long long)w_errors);
+                    if (s.self_checks) atomicAdd(A.counters + kCntSelfChecks, (unsigned long long)s.self_checks);
+                    if (s.self_points) atomicAdd(A.counters + kCntSelfPoints, (unsigned long long)s.self_points);
                     for (int k = 0; k < FKS_NUM_PHASES; ++k)
                         if (s.phase[k]) atomicAdd(A.counters + kPhaseBase + k, (unsigned long long)s.phase[k]);
                 }
                 break;
             }
             if (!run) continue; /* segment already run, being run, or left to the wave finishing its predecessor */
+            claim_fence(); /* the resting state is read after the claim */
+        }
+        /* the issue priority is set afresh for every segment (0 unless carried heavy) */
+        if (A.seg_heavy_prio) {
+            if (prio == 2u)
+                __builtin_amdgcn_s_setprio(2);
+            else if (prio == 1u)
+                __builtin_amdgcn_s_setprio(1); /* a particle that fell behind the round-robin */
+            else
+                __builtin_amdgcn_s_setprio(0);
         }
         const uint64_t seg = ticket / A.n;
         const uint64_t local = ticket - seg * A.n;
@@ -2774,8 +2829,10 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         bool any_failed = false;
         uint64_t micro_before = 0, resolver_before = 0;
         if (seg == 0) {
-            s.pid_integral = 0.0;
-            s.pid_last = 0.0;
+            /* ResetPosition zeroes the controllers (TNUVA:524-536); ForwardSimulateMutableRobot
+             * continues the robot's own (SPCS:843-919, fks_forward_simulate_mutable) */
+            s.pid_integral = (A.pid_io && ln < D) ? A.pid_io[local * 2ull * (uint64_t)D + ln] : 0.0;
+            s.pid_last = (A.pid_io && ln < D) ? A.pid_io[local * 2ull * (uint64_t)D + D + ln] : 0.0;
             /* ResetPosition(start): SetPosition enforces joint limits / angle wrap */
             if constexpr (RT == FKS_ROBOT_LINKED) {
                 if (ln < D) {
@@ -2878,6 +2935,10 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         w_resolver += s.resolver_count;
         w_lsq += s.lsq_rows;
         if (s.err) w_errors++;
+        if (ended && A.pid_io && ln < D) {
+            A.pid_io[local * 2ull * (uint64_t)D + ln] = s.pid_integral;
+            A.pid_io[local * 2ull * (uint64_t)D + D + ln] = s.pid_last;
+        }
         if (ln == 0) {
             if (ended) {
                 if (A.out_collided) A.out_collided[local] = collided ? 1 : 0;
@@ -2896,12 +2957,12 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         if (nseg > 1) {
             /* publish the resting state; if the next segment's ticket is already out, claim
              * the segment and run it here (its holder, if it looked earlier, skipped it) */
-            wait_memory(); /* every lane's state stores have completed */
+            publish_fence(); /* every lane's state stores have completed */
             wsync();
             if (ln == 0) {
                 uint32_t nv = ended ? nseg : (uint32_t)seg + 1u;
                 __hip_atomic_store(A.seg_done + local, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                wait_memory(); /* the store is visible before the ticket counter is read (Dekker with the holder) */
+                publish_fence(); /* the store is visible before the ticket counter is read (Dekker with the holder) */
                 uint32_t cont = 0;
                 if (!ended) {
                     /* a contact-heavy segment (many resolver iterations) keeps its wave: the
@@ -2920,16 +2981,9 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             }
             wsync();
             const uint32_t cont = *seg_seen;
-            if (cont) carry = (seg + 1) * A.n + local;
-            /* a wave carrying a contact-heavy particle issues first on its SIMD: the
-             * longest particles finish sooner, the batch's tail shrinks */
-            if (A.seg_heavy_prio) {
-                if (cont == 2u)
-                    __builtin_amdgcn_s_setprio(2);
-                else if (cont == 1u && A.seg_heavy_prio > 1u)
-                    __builtin_amdgcn_s_setprio(1); /* a particle that fell behind the round-robin */
-                else
-                    __builtin_amdgcn_s_setprio(0);
+            if (cont) {
+                carry = (seg + 1) * A.n + local;
+                carry_heavy = cont == 2u;
             }
         }
         wsync();

@@ -151,6 +151,19 @@ class HipParticleContactSimulator:
         0 = automatic).  Results do not depend on it."""
         _capi.check(self._lib.fks_set_segment_steps(self._ctx, int(controller_steps)), self._ctx, "segment steps")
 
+    def set_segment_policy(self, heavy_resolver_per_step: int = 2, heavy_priority: int = 1):
+        """Scheduling policy of segmented batches (fks_set_segment_policy): contact-heavy
+        segments keep their wave and raise its issue priority.  Results do not depend on it."""
+        _capi.check(self._lib.fks_set_segment_policy(self._ctx, int(heavy_resolver_per_step), int(heavy_priority)), self._ctx,
+                    "segment policy")
+
+    def set_individual_jacobians(self, simulate_with_individual_jacobians: bool):
+        """The simulate_with_individual_jacobians constructor flag of the reference class
+        (SPCS:420-423, 1629): True selects ComputeResolverCorrectionStepIndividualJacobians
+        (SPCS:1966-1988) instead of the stacked solve the factories hard-wire (FKS.cpp:22)."""
+        _capi.check(self._lib.fks_set_individual_jacobians(self._ctx, 1 if simulate_with_individual_jacobians else 0), self._ctx,
+                    "individual jacobians")
+
     def launch_geometry(self) -> dict:
         """Resident waves of the persistent simulation grid and LDS bytes per workgroup
         (fks_get_launch_geometry) for the robot set last."""
@@ -190,6 +203,33 @@ class HipParticleContactSimulator:
                 _capi.as_ptr(collided, ctypes.c_uint8), _capi.as_ptr(micro, ctypes.c_uint32),
                 _capi.as_ptr(resolver, ctypes.c_uint32), _capi.as_ptr(errors, ctypes.c_uint32))
         _capi.check(st, self._ctx, "fks_forward_simulate")
+        return {"positions": out, "collided": collided.astype(bool), "microsteps": micro, "resolver_iterations": resolver,
+                "error_flags": errors}
+
+    def forward_simulate_mutable_arrays(self, robot: RobotDescription, start_positions, target_positions, allow_contacts: bool,
+                                        controller_state) -> dict:
+        """ForwardSimulateMutableRobot (SPCS:843-919) for a batch (fks_forward_simulate_mutable):
+        each particle starts with its own PID state; controller_state is an (n, 2D) float64
+        array (per dof the error integral, then per dof the last error), updated in place."""
+        self.set_robot(robot)
+        W, D = robot.config_width, robot.num_dofs
+        starts = np.ascontiguousarray(np.asarray(start_positions, dtype=np.float64).reshape(-1, W))
+        targets = np.ascontiguousarray(np.asarray(target_positions, dtype=np.float64).reshape(-1, W))
+        n = starts.shape[0]
+        if not (isinstance(controller_state, np.ndarray) and controller_state.dtype == np.float64 and
+                controller_state.flags["C_CONTIGUOUS"] and controller_state.shape == (n, 2 * D)):
+            raise ValueError("controller_state must be a C-contiguous float64 array of shape (n, 2 * num_dofs)")
+        out = np.zeros((n, W), dtype=np.float64)
+        collided = np.zeros(n, dtype=np.uint8)
+        micro = np.zeros(n, dtype=np.uint32)
+        resolver = np.zeros(n, dtype=np.uint32)
+        errors = np.zeros(n, dtype=np.uint32)
+        st = self._lib.fks_forward_simulate_mutable(
+            self._ctx, _capi.as_ptr(starts, ctypes.c_double), n, _capi.as_ptr(targets, ctypes.c_double), targets.shape[0],
+            1 if allow_contacts else 0, _capi.as_ptr(controller_state, ctypes.c_double), _capi.as_ptr(out, ctypes.c_double),
+            _capi.as_ptr(collided, ctypes.c_uint8), _capi.as_ptr(micro, ctypes.c_uint32), _capi.as_ptr(resolver, ctypes.c_uint32),
+            _capi.as_ptr(errors, ctypes.c_uint32))
+        _capi.check(st, self._ctx, "fks_forward_simulate_mutable")
         return {"positions": out, "collided": collided.astype(bool), "microsteps": micro, "resolver_iterations": resolver,
                 "error_flags": errors}
 

@@ -75,14 +75,18 @@ def grid_origin(lo) -> np.ndarray:
 
 
 # ---------------------------------------------------------------- cfg1: SE(2)
-def _cfg1_env(device=None, stats=None, resident=False):
+def cfg1_obstacles() -> List[ObstacleConfig]:
     rng = np.random.default_rng(1)
     obstacles = []
     for i in range(12):
         c = [rng.uniform(0.5, 3.5), rng.uniform(0.5, 3.5), 0.0]
         h = [rng.uniform(0.08, 0.25), rng.uniform(0.08, 0.25), 1.0]
         obstacles.append(box(i + 1, c, h, rotation_from_axis_angle([0, 0, 1], rng.uniform(0, np.pi))))
-    return build_complete_environment(obstacles, 0.0625, origin=grid_origin([0.0, 0.0, -2.0]), num_cells=(64, 64, 64),
+    return obstacles
+
+
+def _cfg1_env(device=None, stats=None, resident=False):
+    return build_complete_environment(cfg1_obstacles(), 0.0625, origin=grid_origin([0.0, 0.0, -2.0]), num_cells=(64, 64, 64),
                                       device=device, stats=stats, resident=resident)
 
 
@@ -195,7 +199,7 @@ def cfg3(scale: float = 1.0) -> Workload:
 
 
 # ---------------------------------------------------------------- cfg4: SE(3)
-def _cfg4_env(device=None, stats=None, resident=False):
+def cfg4_obstacles() -> List[ObstacleConfig]:
     rng = np.random.default_rng(5)
     obstacles = []
     for i in range(24):
@@ -206,7 +210,11 @@ def _cfg4_env(device=None, stats=None, resident=False):
         obstacles.append(box(i + 1, c, h, rotation_from_axis_angle(rng.normal(size=3), rng.uniform(0, np.pi))))
     # a block across the straight-line path to the target, so particles slide along it
     obstacles.append(box(100, [0.2, 0.14, -0.09], [0.04, 0.04, 0.04], rotation_from_axis_angle([0.0, 0.0, 1.0], 0.3)))
-    return build_complete_environment(obstacles, 0.01, origin=grid_origin([-1.28, -1.28, -1.28]), num_cells=(256, 256, 256),
+    return obstacles
+
+
+def _cfg4_env(device=None, stats=None, resident=False):
+    return build_complete_environment(cfg4_obstacles(), 0.01, origin=grid_origin([-1.28, -1.28, -1.28]), num_cells=(256, 256, 256),
                                       device=device, stats=stats, resident=resident)
 
 
@@ -292,3 +300,116 @@ SCENES: Dict[str, Callable[..., SimulatorEnvironment]] = {"cfg1": _cfg1_env, "cf
                                                           "cfg4": _cfg4_env, "cfg5": _cfg5_env}
 
 WORKLOADS: Dict[str, Callable[..., Workload]] = {"cfg1": cfg1, "cfg2": cfg2, "cfg3": cfg3, "cfg4": cfg4, "cfg5": cfg5}
+
+
+# ---------------------------------------------------------------- branch-coverage scenes (tests)
+# Small scenes that drive resolver branches the BASELINE configs rarely or never reach:
+# self-collision corrections (ExtractSelfCollidingPoints SPCS:983-1171), a cell shared by
+# many links (no capacity limit, as the reference's maps), a 32-DOF chain, continuous joints.
+def _open_space_env(device=None, stats=None, resident=False):
+    """128^3 @ 1 cm around the origin with a floor well below the robots."""
+    obstacles = [box(1, [0.0, 0.0, -0.15], [0.6, 0.6, 0.03])]
+    return build_complete_environment(obstacles, 0.01, origin=grid_origin([-0.64, -0.64, -0.2]), num_cells=(128, 128, 128),
+                                      device=device, stats=stats, resident=resident)
+
+
+def folding_arm(scale: float = 1.0, continuous: bool = False) -> Workload:
+    """3-link arm whose parallel y axes fold link 3 back onto link 1 and the base: only
+    adjacent links may touch, so the fold is a self-collision the resolver must push
+    apart (SPCS:1183-1275 -> 983-1171 -> corrections SPCS:1846-1853).  continuous=True
+    makes the joints continuous (angle wrap, TNUVA:556 / SetPosition)."""
+    segs = [0.25, 0.25, 0.25]
+    joints, geoms = [], [(0, cylinder_points(0.1, 0.05, 64, 16))]
+    for i in range(3):
+        # continuous: the first joint spins the arm about the vertical through +-pi
+        jt = _capi.JOINT_CONTINUOUS if (continuous and i == 0) else _capi.JOINT_REVOLUTE
+        joints.append(Joint(parent=i, child=i + 1, type=jt, origin=transform34([0, 0, 0.1 if i == 0 else segs[i - 1]]),
+                            axis=(0.0, 0.0, 1.0) if (continuous and i == 0) else (0.0, 1.0, 0.0), lower=-3.0, upper=3.0))
+        geoms.append((i + 1, cylinder_points(segs[i], 0.02, 64, 16)))
+    allowed = [(0, 1), (1, 2), (2, 3)]
+    robot = make_linked_robot(transform34([0, 0, 0]), 4, joints, geoms, allowed, _arm_controllers(3, vmax=1.5), [1.0] * 3,
+                              name="folding_arm_continuous" if continuous else "folding_arm")
+    rng = np.random.default_rng(8)
+    n = max(1, int(round(32 * scale)))
+    starts = np.array([2.8 if continuous else 0.0, 0.4, 0.4]) + rng.uniform(-0.05, 0.05, size=(n, 3))
+    target = np.array([[-2.8 if continuous else 0.0, 2.5, 2.6]])
+    solver = SimulatorSolverParameters(forward_simulation_time=2.0)
+    return Workload("folding_arm", "3-link arm folding onto itself (self-collision resolver)", robot, _open_space_env, starts,
+                    target, solver, 50.0, 21, True, 128, 0.01)
+
+
+def crowded_cell_robot(links: int = 10) -> RobotDescription:
+    """`links` links on revolute z joints at one point: link k carries a ring of 8 points of
+    radius 1.5 mm + 0.3 mm k, so every link has points in the same 1 cm self-collision cell
+    and no pair is allowed except along the chain.  A cell then holds `links` links (the
+    impulse solve of SPCS:1054-1150 runs with n = links - 1 others)."""
+    joints, geoms = [], []
+    geoms.append((0, np.array([[0.0015 * np.cos(a), 0.0015 * np.sin(a), 0.0, 1.0] for a in np.arange(8) * np.pi / 4])))
+    for k in range(1, links):
+        joints.append(Joint(parent=k - 1, child=k, type=_capi.JOINT_REVOLUTE, origin=transform34([0, 0, 0]),
+                            axis=(0.0, 0.0, 1.0), lower=-3.0, upper=3.0))
+        r = 0.0015 + 0.0003 * k
+        geoms.append((k, np.array([[r * np.cos(a + 0.1 * k), r * np.sin(a + 0.1 * k), 0.0005 * k, 1.0]
+                                   for a in np.arange(8) * np.pi / 4])))
+    allowed = [(k - 1, k) for k in range(1, links)]
+    return make_linked_robot(transform34([0.105, 0.105, 0.105]), links, joints, geoms, allowed,
+                             _arm_controllers(links - 1, vmax=1.0), [1.0] * (links - 1), name=f"crowded_cell_{links}")
+
+
+def crowded_cell(scale: float = 1.0, links: int = 10) -> Workload:
+    robot = crowded_cell_robot(links)
+    rng = np.random.default_rng(9)
+    n = max(1, int(round(8 * scale)))
+    starts = rng.uniform(-0.2, 0.2, size=(n, links - 1))
+    target = np.full((1, links - 1), 0.8)
+    solver = SimulatorSolverParameters(forward_simulation_time=0.1)
+    return Workload("crowded_cell", f"{links} links sharing one self-collision cell", robot, _open_space_env, starts, target,
+                    solver, 100.0, 22, True, 128, 0.01)
+
+
+def long_chain_robot(dofs: int = 32) -> RobotDescription:
+    """A `dofs`-DOF serial chain of short links (alternating y / x axes), 16 points per link."""
+    joints, geoms = [], [(0, cylinder_points(0.05, 0.03, 16, 4))]
+    for i in range(dofs):
+        joints.append(Joint(parent=i, child=i + 1, type=_capi.JOINT_REVOLUTE, origin=transform34([0, 0, 0.05 if i == 0 else 0.03]),
+                            axis=(0.0, 1.0, 0.0) if i % 2 == 0 else (1.0, 0.0, 0.0), lower=-2.5, upper=2.5))
+        geoms.append((i + 1, cylinder_points(0.03, 0.012, 16, 4)))
+    allowed = [(i, i + 1) for i in range(dofs)] + [(i, i + 2) for i in range(dofs - 1)]
+    return make_linked_robot(transform34([0, 0, 0]), dofs + 1, joints, geoms, allowed, _arm_controllers(dofs, vmax=1.0),
+                             [1.0] * dofs, name=f"chain_{dofs}dof")
+
+
+def long_chain(scale: float = 1.0, dofs: int = 32) -> Workload:
+    robot = long_chain_robot(dofs)
+    rng = np.random.default_rng(10)
+    n = max(1, int(round(16 * scale)))
+    starts = np.tile(np.linspace(0.05, 0.15, dofs), (n, 1)) + rng.uniform(-0.02, 0.02, size=(n, dofs))
+    target = np.tile(np.array([0.5, -0.4]), dofs // 2 + 1)[None, :dofs]
+    solver = SimulatorSolverParameters(forward_simulation_time=0.5)
+    return Workload("long_chain", f"{dofs}-DOF serial chain", robot, _open_space_env, starts, target, solver, 100.0, 23, True,
+                    128, 0.01)
+
+
+def pid_free_space(scale: float = 1.0) -> Workload:
+    """The folding arm's geometry moved by small targets through free space with the
+    actuator noise bounds at zero and gains that keep the PID term inside the velocity
+    clamp: every controller step's control input is the reference PID's output (PID:122-135)
+    times dt, so a trace of it can be replayed through the reference header itself
+    (tests/golden/make_pid_trace_golden.py)."""
+    wl = folding_arm(scale)
+    for c in wl.robot.controllers:
+        c.kp, c.ki, c.kd, c.integral_clamp = 2.0, 0.5, 0.01, 0.2
+        c.velocity_limit = 2.5
+        c.max_actuator_proportional_noise = 0.0
+        c.max_actuator_minimum_noise = 0.0
+    rng = np.random.default_rng(12)
+    n = max(1, int(round(4 * scale)))
+    wl.starts = np.array([0.0, 0.4, 0.4]) + rng.uniform(-0.05, 0.05, size=(n, 3))
+    wl.targets = np.array([[0.5, 0.8, 0.3]])
+    wl.solver = SimulatorSolverParameters(forward_simulation_time=1.0)
+    wl.name, wl.description = "pid_free_space", "folding-arm geometry in free space, noise bounds 0"
+    return wl
+
+
+COVERAGE: Dict[str, Callable[..., Workload]] = {"folding_arm": folding_arm, "crowded_cell": crowded_cell,
+                                                "long_chain": long_chain, "pid_free_space": pid_free_space}

@@ -1,0 +1,491 @@
+/*
+ * fast_kinematic_simulator.hpp — the planner-facing drop-in: the HIP-backed particle
+ * simulator behind simple_simulator_interface::SimulatorInterface, and the
+ * fast_kinematic_simulator factories with the reference's parameter lists.
+ *
+ *   simple_particle_contact_simulator::SimulatorSolverParameters   SPCS:345-369
+ *   simple_particle_contact_simulator::HipParticleContactSimulator
+ *       <DerivedRobotType, Configuration, RNG, ConfigAlloc>           SPCS:371-1999 (the
+ *       class the factories instantiate), every SimulatorInterface virtual overridden
+ *   fast_kinematic_simulator::SolverParameters / GetDefaultSolverParameters   FKS.hpp:11-16
+ *   fast_kinematic_simulator::Make{SE2,SE3,Linked}Simulator                    FKS.hpp:18-22,
+ *       FKS.cpp:4-71 (simulate_with_individual_jacobians = false, as there)
+ *
+ * Batch, traced, mutable-robot and validity calls all run on the GPU through the
+ * C-ABI (include/fks_capi.h); there is no CPU path.  The robot a call receives is the
+ * planner's BaseRobotType, static_cast to DerivedRobotType as the reference does
+ * (SPCS:868); DerivedRobotType is one of tnuva_robot_models::Tnuva{SE2,SE3,Linked}Robot
+ * (tnuva_robot_models.hpp), which carry the flattened description and the controller
+ * state.  Differences from the reference, by design:
+ *   - actuation noise comes from the counter RNG keyed by (seed, call, particle, step,
+ *     microstep, dof), not from GetRandomGenerator()'s stream, which is
+ *     still provided for the caller's own sampling;
+ *   - the reference's per-particle asserts (SPCS:1570-1575, 1882) become error bits,
+ *     available from LastParticleErrors() after a batch call;
+ *   - display_fn is accepted and never called (the batch path never draws, SPCS:801).
+ */
+#ifndef FAST_KINEMATIC_SIMULATOR_AMD_FAST_KINEMATIC_SIMULATOR_HPP
+#define FAST_KINEMATIC_SIMULATOR_AMD_FAST_KINEMATIC_SIMULATOR_HPP
+
+#include <cstdint>
+#include <limits>
+#include <map>
+#include <memory>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "fast_kinematic_simulator_amd/environment.hpp"
+#include "fast_kinematic_simulator_amd/simulator_interface.hpp"
+#include "fast_kinematic_simulator_amd/tnuva_robot_models.hpp"
+#include "fks_capi.h"
+
+namespace simple_particle_contact_simulator {
+
+/* SimulatorSolverParameters (SPCS:345-369) */
+struct SimulatorSolverParameters {
+    double forward_simulation_time;
+    double simulation_shortcut_distance;
+    double environment_collision_check_tolerance;
+    double resolve_correction_step_scaling_decay_rate;
+    double resolve_correction_initial_step_size;
+    double resolve_correction_min_step_scaling;
+    uint32_t max_resolver_iterations;
+    uint32_t resolve_correction_step_scaling_decay_iterations;
+    bool failed_resolves_end_motion;
+
+    SimulatorSolverParameters() {
+        forward_simulation_time = 1.0;
+        simulation_shortcut_distance = 0.0;
+        environment_collision_check_tolerance = 0.001;
+        resolve_correction_step_scaling_decay_rate = 0.5;
+        resolve_correction_initial_step_size = 1.0;
+        resolve_correction_min_step_scaling = 0.03125;
+        max_resolver_iterations = 25;
+        resolve_correction_step_scaling_decay_iterations = 5;
+        failed_resolves_end_motion = true;
+    }
+    fks_solver_params ToFks() const {
+        fks_solver_params p{};
+        p.forward_simulation_time = forward_simulation_time;
+        p.simulation_shortcut_distance = simulation_shortcut_distance;
+        p.environment_collision_check_tolerance = environment_collision_check_tolerance;
+        p.resolve_correction_step_scaling_decay_rate = resolve_correction_step_scaling_decay_rate;
+        p.resolve_correction_initial_step_size = resolve_correction_initial_step_size;
+        p.resolve_correction_min_step_scaling = resolve_correction_min_step_scaling;
+        p.max_resolver_iterations = max_resolver_iterations;
+        p.resolve_correction_step_scaling_decay_iterations = resolve_correction_step_scaling_decay_iterations;
+        p.failed_resolves_end_motion = failed_resolves_end_motion ? 1u : 0u;
+        return p;
+    }
+};
+
+template <typename DerivedRobotType, typename Configuration, typename RNG, typename ConfigAlloc = std::allocator<Configuration>>
+class HipParticleContactSimulator : public simple_simulator_interface::SimulatorInterface<Configuration, RNG, ConfigAlloc> {
+  public:
+    typedef simple_simulator_interface::SimulatorInterface<Configuration, RNG, ConfigAlloc> Base;
+    typedef typename Base::BaseRobotType BaseRobotType;
+    typedef typename Base::SimulationResult SimulationResult;
+    typedef typename Base::ForwardSimulationStepTrace ForwardSimulationStepTrace;
+    typedef typename Base::DisplayFn DisplayFn;
+    typedef fks_planner_types::MarkerArray MarkerArray;
+    typedef fks_planner_types::ColorRGBA ColorRGBA;
+
+    /* SPCS:420-444; `device` selects the MI355X (no reference counterpart) */
+    HipParticleContactSimulator(const sdf_tools::TaggedObjectCollisionMapGrid& environment,
+                                const sdf_tools::SignedDistanceField& environment_sdf,
+                                const SurfaceNormalGrid& surface_normals_grid, const SimulatorSolverParameters& solver_config,
+                                const double simulation_controller_frequency, const bool simulate_with_individual_jacobians,
+                                const uint64_t prng_seed, const int32_t debug_level, const int32_t device = 0)
+        : environment_(environment), environment_sdf_(environment_sdf), surface_normals_grid_(surface_normals_grid),
+          solver_config_(solver_config), simulation_controller_frequency_(simulation_controller_frequency) {
+        const fks_environment env =
+            simulator_environment_builder::ToFksEnvironment(environment, environment_sdf, surface_normals_grid);
+        const fks_solver_params p = solver_config.ToFks();
+        fks_context* ctx = nullptr;
+        Check(fks_create(&env, &p, simulation_controller_frequency, prng_seed, debug_level, device, &ctx), nullptr, "fks_create");
+        ctx_.reset(ctx);
+        Check(fks_set_individual_jacobians(ctx_.get(), simulate_with_individual_jacobians ? 1 : 0), ctx_.get(),
+              "fks_set_individual_jacobians");
+        ResetGenerators(prng_seed);
+    }
+
+    /* ---- SimulatorInterface (SPCS:446-1416) ---- */
+    int32_t GetDebugLevel() const override { return fks_get_debug_level(ctx_.get()); }
+    int32_t SetDebugLevel(const int32_t debug_level) override { return fks_set_debug_level(ctx_.get(), debug_level); }
+    /* SPCS:457-471: the host generator seeded as the reference seeds its thread 0 one; the
+     * simulation's own noise is the counter RNG re-keyed by the same seed */
+    void ResetGenerators(const uint64_t prng_seed) {
+        RNG prng(prng_seed);
+        std::uniform_int_distribution<uint64_t> seed_dist(0, std::numeric_limits<uint64_t>::max());
+        rng_ = RNG(seed_dist(prng));
+        Check(fks_reset_generators(ctx_.get(), prng_seed), ctx_.get(), "ResetGenerators");
+    }
+    RNG& GetRandomGenerator() override { return rng_; }
+    std::map<std::string, double> GetStatistics() const override {
+        fks_statistics s;
+        Check(fks_get_statistics(ctx_.get(), &s), ctx_.get(), "GetStatistics");
+        return {{"successful_resolves", (double)s.successful_resolves},
+                {"unsuccessful_resolves", (double)s.unsuccessful_resolves},
+                {"free_resolves", (double)s.free_resolves},
+                {"collision_resolves", (double)s.collision_resolves},
+                {"fallback_resolves", (double)s.fallback_resolves},
+                {"unsuccessful_self_collision_resolves", (double)s.unsuccessful_self_collision_resolves},
+                {"unsuccessful_env_collision_resolves", (double)s.unsuccessful_env_collision_resolves},
+                {"recovered_unsuccessful_resolves", (double)s.recovered_unsuccessful_resolves}};
+    }
+    void ResetStatistics() override { Check(fks_reset_statistics(ctx_.get()), ctx_.get(), "ResetStatistics"); }
+    std::string GetFrame() const override { return environment_.GetFrame(); }
+    double GetResolution() const { return environment_.GetResolution(); }
+
+    /* SPCS:559-586, reduced to the grids this repository holds: the filled cells of the
+     * collision map and the SDF cells colored by sign (sdf_tools' component / convex-segment
+     * exports have no counterpart) */
+    MarkerArray MakeEnvironmentDisplayRep() const override {
+        MarkerArray rep;
+        const double res = environment_.GetResolution();
+        fks_planner_types::Marker env_marker = MakeMarker("sim_environment", 1, fks_planner_types::Marker::CUBE_LIST, res,
+                                                          Base::MakeColor(1.0f, 0.0f, 0.0f, 1.0f));
+        fks_planner_types::Marker sdf_marker = MakeMarker("sim_environment_sdf", 1, fks_planner_types::Marker::CUBE_LIST, res,
+                                                          Base::MakeColor(1.0f, 1.0f, 1.0f, 1.0f));
+        const double* O = environment_.Geometry().origin;
+        for (int64_t x = 0; x < environment_.GetNumXCells(); ++x)
+            for (int64_t y = 0; y < environment_.GetNumYCells(); ++y)
+                for (int64_t z = 0; z < environment_.GetNumZCells(); ++z) {
+                    const double c[3] = {res * ((double)x + 0.5), res * ((double)y + 0.5), res * ((double)z + 0.5)};
+                    fks_planner_types::Point p;
+                    p.x = ((O[0] * c[0] + O[1] * c[1]) + O[2] * c[2]) + O[3];
+                    p.y = ((O[4] * c[0] + O[5] * c[1]) + O[6] * c[2]) + O[7];
+                    p.z = ((O[8] * c[0] + O[9] * c[1]) + O[10] * c[2]) + O[11];
+                    if (environment_.GetImmutable(x, y, z).first) env_marker.points.push_back(p);
+                    sdf_marker.points.push_back(p);
+                    sdf_marker.colors.push_back(environment_sdf_.GetImmutable(x, y, z).first < 0.0f
+                                                    ? Base::MakeColor(1.0f, 0.0f, 0.0f, 1.0f)
+                                                    : Base::MakeColor(0.0f, 0.0f, 1.0f, 1.0f));
+                }
+        rep.markers.push_back(env_marker);
+        rep.markers.push_back(sdf_marker);
+        return rep;
+    }
+    /* MakeConfigurationDisplayRep with POINTS geometries (SPCS:634-688, 695-717): every link point */
+    MarkerArray MakeConfigurationDisplayRep(const std::shared_ptr<BaseRobotType>& immutable_robot, const Configuration& configuration,
+                                            const ColorRGBA& color, const int32_t starting_index,
+                                            const std::string& config_marker_ns) const override {
+        const DerivedRobotType& robot = Derived(immutable_robot);
+        const std::vector<double> pts = Kinematics(robot, FKS_KIN_POINTS, {robot.ToFlat(configuration)});
+        const double res = GetResolution();
+        fks_planner_types::Marker m = MakeMarker(config_marker_ns, starting_index, fks_planner_types::Marker::SPHERE_LIST, res, color);
+        const std::vector<double>& local = robot.HipDescription().points;
+        for (size_t i = 0; i < pts.size() / 3; ++i) {
+            m.points.push_back(Point(pts.data() + 3 * i));
+            const double* q = local.data() + 4 * i;
+            const bool zero = (q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]) == 0.0;
+            m.colors.push_back(zero ? Base::MakeColor(0.0f, 0.0f, 0.0f, 1.0f) : color);
+        }
+        MarkerArray rep;
+        rep.markers.push_back(m);
+        return rep;
+    }
+    /* SPCS:719-774: each point before and after the clean control input */
+    MarkerArray MakeControlInputDisplayRep(const std::shared_ptr<BaseRobotType>& immutable_robot, const Configuration& configuration,
+                                           const fks_planner_types::VectorXd& control_input, const ColorRGBA& color,
+                                           const int32_t starting_index, const std::string& control_input_marker_ns) const override {
+        const DerivedRobotType& robot = Derived(immutable_robot);
+        const std::vector<double> start = robot.ToFlat(configuration);
+        const std::vector<double> after = Kinematics(robot, FKS_KIN_APPLY_CONTROL_INPUT, {start}, {control_input.values()});
+        const std::vector<double> pts = Kinematics(robot, FKS_KIN_POINTS, {start, after});
+        const size_t P = pts.size() / 6;
+        fks_planner_types::Marker m =
+            MakeMarker(control_input_marker_ns, starting_index, fks_planner_types::Marker::LINE_LIST, GetResolution() * 0.5, color);
+        for (size_t i = 0; i < P; ++i) {
+            m.points.push_back(Point(pts.data() + 3 * i));
+            m.points.push_back(Point(pts.data() + 3 * (P + i)));
+            m.colors.push_back(color);
+            m.colors.push_back(color);
+        }
+        MarkerArray rep;
+        rep.markers.push_back(m);
+        return rep;
+    }
+    /* SPCS:776-786: origin of the last geometry's link, w = 1 */
+    fks_planner_types::Vector4d Get3dPointForConfig(const std::shared_ptr<BaseRobotType>& immutable_robot,
+                                                    const Configuration& config) const override {
+        const DerivedRobotType& robot = Derived(immutable_robot);
+        const std::vector<double> T = Kinematics(robot, FKS_KIN_LINK_TRANSFORMS, {robot.ToFlat(config)});
+        const size_t l = (size_t)robot.HipDescription().geometry_link.back();
+        return fks_planner_types::Vector4d(T[12 * l + 3], T[12 * l + 7], T[12 * l + 11], 1.0);
+    }
+
+    /* SPCS:788-804 */
+    std::vector<SimulationResult> ForwardSimulateRobots(const std::shared_ptr<BaseRobotType>& immutable_robot,
+                                                        const std::vector<Configuration, ConfigAlloc>& start_positions,
+                                                        const std::vector<Configuration, ConfigAlloc>& target_positions,
+                                                        const bool allow_contacts, const DisplayFn& display_fn) override {
+        (void)display_fn;
+        return Batch(Derived(immutable_robot), start_positions, target_positions, allow_contacts, fks_forward_simulate);
+    }
+    /* SPCS:806-822: the same simulation (ReverseSimulateMutableRobot, SPCS:838-841) */
+    std::vector<SimulationResult> ReverseSimulateRobots(const std::shared_ptr<BaseRobotType>& immutable_robot,
+                                                        const std::vector<Configuration, ConfigAlloc>& start_positions,
+                                                        const std::vector<Configuration, ConfigAlloc>& target_positions,
+                                                        const bool allow_contacts, const DisplayFn& display_fn) override {
+        (void)display_fn;
+        return Batch(Derived(immutable_robot), start_positions, target_positions, allow_contacts, fks_reverse_simulate);
+    }
+    /* SPCS:824-829: a clone reset to the start (controllers zeroed) */
+    SimulationResult ForwardSimulateRobot(const std::shared_ptr<BaseRobotType>& immutable_robot, const Configuration& start_position,
+                                          const Configuration& target_position, const bool allow_contacts,
+                                          ForwardSimulationStepTrace& trace, const bool enable_tracing,
+                                          const DisplayFn& display_fn) override {
+        std::shared_ptr<BaseRobotType> robot(immutable_robot->Clone());
+        static_cast<DerivedRobotType*>(robot.get())->ResetPosition(start_position);
+        return ForwardSimulateMutableRobot(robot, target_position, allow_contacts, trace, enable_tracing, display_fn);
+    }
+    /* SPCS:831-836 */
+    SimulationResult ReverseSimulateRobot(const std::shared_ptr<BaseRobotType>& immutable_robot, const Configuration& start_position,
+                                          const Configuration& target_position, const bool allow_contacts,
+                                          ForwardSimulationStepTrace& trace, const bool enable_tracing,
+                                          const DisplayFn& display_fn) override {
+        std::shared_ptr<BaseRobotType> robot(immutable_robot->Clone());
+        static_cast<DerivedRobotType*>(robot.get())->ResetPosition(start_position);
+        return ReverseSimulateMutableRobot(robot, target_position, allow_contacts, trace, enable_tracing, display_fn);
+    }
+    /* SPCS:838-841 */
+    SimulationResult ReverseSimulateMutableRobot(const std::shared_ptr<BaseRobotType>& robot, const Configuration& target_position,
+                                                 const bool allow_contacts, ForwardSimulationStepTrace& trace,
+                                                 const bool enable_tracing, const DisplayFn& display_fn) override {
+        return ForwardSimulateMutableRobot(robot, target_position, allow_contacts, trace, enable_tracing, display_fn);
+    }
+    /* SPCS:843-919: simulates from the robot's position with its controllers as they are,
+     * then leaves the robot at the reached position with the controllers' new state */
+    SimulationResult ForwardSimulateMutableRobot(const std::shared_ptr<BaseRobotType>& robot, const Configuration& target_position,
+                                                 const bool allow_contacts, ForwardSimulationStepTrace& trace,
+                                                 const bool enable_tracing, const DisplayFn& display_fn) override {
+        (void)display_fn;
+        DerivedRobotType& r = *static_cast<DerivedRobotType*>(robot.get());
+        SetRobot(r);
+        const std::vector<double> s = r.ToFlat(r.GetPosition()), t = r.ToFlat(target_position);
+        const size_t W = s.size(), D = (size_t)r.HipDescription().NumDofs();
+        std::vector<double> q(W), pid = r.ControllerState();
+        uint8_t collided = 0;
+        uint32_t micro = 0, resolver = 0, errors = 0;
+        if (!enable_tracing) {
+            Check(fks_forward_simulate_mutable(ctx_.get(), s.data(), 1, t.data(), 1, allow_contacts ? 1 : 0, pid.data(), q.data(),
+                                               &collided, &micro, &resolver, &errors),
+                  ctx_.get(), "ForwardSimulateMutableRobot");
+        } else {
+            /* the trace holds one step record per controller step and every pushed configuration */
+            const uint32_t steps = ForwardSteps(), cap = 16384;
+            std::vector<double> inputs((size_t)steps * 2 * D), configs((size_t)cap * W);
+            std::vector<uint32_t> step_micro(steps), tags((size_t)cap * 3);
+            uint32_t num_steps = 0, num_configs = 0;
+            fks_trace tr{steps, cap, inputs.data(), step_micro.data(), configs.data(), tags.data(), &num_steps, &num_configs};
+            Check(fks_forward_simulate_traced_mutable(ctx_.get(), s.data(), 1, t.data(), 1, allow_contacts ? 1 : 0, pid.data(),
+                                                      q.data(), &collided, &micro, &resolver, &errors, &tr),
+                  ctx_.get(), "ForwardSimulateMutableRobot (traced)");
+            if (num_steps > steps || num_configs > cap) throw std::runtime_error("trace capacity exceeded");
+            AppendTrace(r, trace, inputs, num_steps, configs, tags, num_configs, D);
+        }
+        last_errors_.assign(1, errors);
+        r.SetPosition(r.FromFlat(q.data()));
+        r.SetControllerState(pid);
+        return SimulationResult(r.GetPosition(), target_position, collided != 0, true); /* SPCS:918 */
+    }
+    /* SPCS:1398-1416 */
+    bool CheckConfigCollision(const std::shared_ptr<BaseRobotType>& immutable_robot, const Configuration& config,
+                              const double inflation_ratio) const override {
+        const DerivedRobotType& robot = Derived(immutable_robot);
+        SetRobot(robot);
+        const std::vector<double> c = robot.ToFlat(config);
+        uint8_t collided = 0;
+        Check(fks_check_config_collision(ctx_.get(), c.data(), 1, inflation_ratio, &collided, nullptr), ctx_.get(),
+              "CheckConfigCollision");
+        return collided != 0;
+    }
+
+    /* ---- beyond the interface ---- */
+    /* per-particle FKS_PARTICLE_ERR_* bits of the last batch (the reference asserts instead) */
+    const std::vector<uint32_t>& LastParticleErrors() const { return last_errors_; }
+    const std::vector<uint32_t>& LastMicrosteps() const { return last_micro_; }
+    const std::vector<uint32_t>& LastResolverIterations() const { return last_resolver_; }
+    fks_context* Context() const { return ctx_.get(); }
+
+  private:
+    struct Destroy {
+        void operator()(fks_context* c) const { fks_destroy(c); }
+    };
+    typedef fks_status (*BatchFn)(fks_context*, const double*, uint64_t, const double*, uint64_t, int32_t, double*, uint8_t*,
+                                  uint32_t*, uint32_t*, uint32_t*);
+
+    static void Check(fks_status st, const fks_context* ctx, const char* what) {
+        if (st == FKS_OK) return;
+        std::string msg = std::string(what) + ": " + fks_status_string(st);
+        if (ctx) {
+            const char* detail = fks_get_last_error(ctx);
+            if (detail && detail[0]) msg += std::string(" (") + detail + ")";
+        }
+        throw fks::SimulatorError(st, msg);
+    }
+    static const DerivedRobotType& Derived(const std::shared_ptr<BaseRobotType>& robot) {
+        if (!robot) throw std::invalid_argument("null robot");
+        return *static_cast<const DerivedRobotType*>(robot.get()); /* SPCS:868 */
+    }
+    static fks_planner_types::Point Point(const double* p) {
+        fks_planner_types::Point o;
+        o.x = p[0];
+        o.y = p[1];
+        o.z = p[2];
+        return o;
+    }
+    fks_planner_types::Marker MakeMarker(const std::string& ns, int32_t id, int32_t type, double scale, const ColorRGBA& color) const {
+        fks_planner_types::Marker m;
+        m.ns = ns;
+        m.id = id;
+        m.type = type;
+        m.frame_id = GetFrame();
+        m.scale.x = m.scale.y = m.scale.z = scale;
+        m.color = color;
+        return m;
+    }
+    uint32_t ForwardSteps() const {
+        const double raw = solver_config_.forward_simulation_time * std::fabs(simulation_controller_frequency_);
+        return raw >= 1.0 && raw < 4294967295.0 ? (uint32_t)raw : 1u; /* SPCS:856 */
+    }
+    /* the robot every particle clones: flattened once per description (clones share it) */
+    void SetRobot(const DerivedRobotType& robot) const {
+        const fks::RobotDescription* d = &robot.HipDescription();
+        if (d == robot_key_) return;
+        const fks_robot_desc v = d->View();
+        Check(fks_set_robot(ctx_.get(), &v), ctx_.get(), "fks_set_robot");
+        robot_key_ = d;
+    }
+    std::vector<double> Kinematics(const DerivedRobotType& robot, int32_t mode, const std::vector<std::vector<double>>& configs,
+                                   const std::vector<std::vector<double>>& inputs = {}) const {
+        SetRobot(robot);
+        int32_t links = 0, points = 0, dofs = 0, width = 0;
+        Check(fks_robot_sizes(ctx_.get(), &links, &points, &dofs, &width), ctx_.get(), "fks_robot_sizes");
+        std::vector<double> c, u;
+        for (const auto& q : configs) c.insert(c.end(), q.begin(), q.end());
+        for (const auto& q : inputs) u.insert(u.end(), q.begin(), q.end());
+        if (mode == FKS_KIN_APPLY_CONTROL_INPUT && u.size() != configs.size() * (size_t)dofs)
+            throw std::invalid_argument("control input has the wrong width");
+        const size_t per = mode == FKS_KIN_LINK_TRANSFORMS ? 12u * (size_t)links : (mode == FKS_KIN_POINTS ? 3u * (size_t)points : (size_t)width);
+        std::vector<double> out(configs.size() * per);
+        Check(fks_kinematics(ctx_.get(), mode, c.data(), configs.size(), u.empty() ? nullptr : u.data(), out.data()), ctx_.get(),
+              "fks_kinematics");
+        return out;
+    }
+    std::vector<SimulationResult> Batch(const DerivedRobotType& robot, const std::vector<Configuration, ConfigAlloc>& starts,
+                                        const std::vector<Configuration, ConfigAlloc>& targets, bool allow_contacts, BatchFn fn) {
+        if (!starts.empty() && targets.size() != 1 && targets.size() != starts.size())
+            throw std::invalid_argument("target_positions must hold 1 or start_positions.size() configurations (SPCS:792)");
+        SetRobot(robot);
+        std::vector<double> s, t;
+        for (const auto& c : starts) {
+            const std::vector<double> f = robot.ToFlat(c);
+            s.insert(s.end(), f.begin(), f.end());
+        }
+        for (const auto& c : targets) {
+            const std::vector<double> f = robot.ToFlat(c);
+            t.insert(t.end(), f.begin(), f.end());
+        }
+        const size_t n = starts.size(), W = n ? s.size() / n : 0;
+        std::vector<double> q(n * W);
+        std::vector<uint8_t> collided(n);
+        last_micro_.assign(n, 0);
+        last_resolver_.assign(n, 0);
+        last_errors_.assign(n, 0);
+        Check(fn(ctx_.get(), s.data(), n, t.data(), targets.size(), allow_contacts ? 1 : 0, q.data(), collided.data(),
+                 last_micro_.data(), last_resolver_.data(), last_errors_.data()),
+              ctx_.get(), "ForwardSimulateRobots");
+        std::vector<SimulationResult> out;
+        out.reserve(n);
+        for (size_t i = 0; i < n; ++i) /* SimulationResult(reached, target, collided, true), SPCS:918 */
+            out.emplace_back(robot.FromFlat(q.data() + i * W), targets.size() == n ? targets[i] : targets[0], collided[i] != 0, true);
+        return out;
+    }
+    /* regroup the flat records into the reference's nesting: one resolver step per
+     * controller step (SPCS:1583-1588), one contact-resolver step per (step, microstep)
+     * (SPCS:1594), configurations in push order (SPCS:1617, 1703, 1714, 1778) */
+    void AppendTrace(const DerivedRobotType& robot, ForwardSimulationStepTrace& trace, const std::vector<double>& inputs,
+                     uint32_t num_steps, const std::vector<double>& configs, const std::vector<uint32_t>& tags, uint32_t num_configs,
+                     size_t D) const {
+        const size_t base = trace.resolver_steps.size(), W = configs.size() / (tags.size() / 3);
+        for (uint32_t k = 0; k < num_steps; ++k) {
+            typename decltype(trace.resolver_steps)::value_type rs;
+            rs.control_input = fks_planner_types::VectorXd(
+                std::vector<double>(inputs.begin() + (long)(k * 2 * D), inputs.begin() + (long)(k * 2 * D + D)));
+            rs.control_input_step = fks_planner_types::VectorXd(
+                std::vector<double>(inputs.begin() + (long)(k * 2 * D + D), inputs.begin() + (long)((k + 1) * 2 * D)));
+            trace.resolver_steps.push_back(rs);
+        }
+        int64_t last_step = -1, last_micro = -1;
+        for (uint32_t k = 0; k < num_configs; ++k) {
+            const uint32_t st = tags[3 * k], mi = tags[3 * k + 1];
+            auto& rs = trace.resolver_steps.at(base + st);
+            if ((int64_t)st != last_step || (int64_t)mi != last_micro) rs.contact_resolver_steps.emplace_back();
+            last_step = st;
+            last_micro = mi;
+            rs.contact_resolver_steps.back().contact_resolution_steps.push_back(robot.FromFlat(configs.data() + (size_t)k * W));
+        }
+    }
+
+    sdf_tools::TaggedObjectCollisionMapGrid environment_;
+    sdf_tools::SignedDistanceField environment_sdf_;
+    SurfaceNormalGrid surface_normals_grid_;
+    SimulatorSolverParameters solver_config_;
+    double simulation_controller_frequency_;
+    std::unique_ptr<fks_context, Destroy> ctx_;
+    mutable const fks::RobotDescription* robot_key_ = nullptr;
+    RNG rng_;
+    std::vector<uint32_t> last_errors_, last_micro_, last_resolver_;
+};
+
+}  // namespace simple_particle_contact_simulator
+
+namespace fast_kinematic_simulator {
+
+typedef simple_particle_contact_simulator::SimulatorSolverParameters SolverParameters;
+
+/* FKS.hpp:13-16 */
+inline SolverParameters GetDefaultSolverParameters() { return SolverParameters(); }
+
+/* FKS.hpp:18-22 / FKS.cpp:4-71: simulate_with_individual_jacobians = false.  `device`
+ * (default 0) selects the MI355X; the reference's parameter list is otherwise unchanged. */
+inline uncertainty_planning_core::SE2SimulatorPtr MakeSE2Simulator(
+    const sdf_tools::TaggedObjectCollisionMapGrid& environment, const sdf_tools::SignedDistanceField& environment_sdf,
+    const simple_particle_contact_simulator::SurfaceNormalGrid& surface_normals_grid, const SolverParameters& solver_config,
+    const double simulation_controller_frequency, const uint64_t prng_seed, const int32_t debug_level, const int32_t device = 0) {
+    using namespace uncertainty_planning_core;
+    return SE2SimulatorPtr(new simple_particle_contact_simulator::HipParticleContactSimulator<
+                           tnuva_robot_models::TnuvaSE2Robot<PRNG>, SE2Config, PRNG, SE2ConfigAlloc>(
+        environment, environment_sdf, surface_normals_grid, solver_config, simulation_controller_frequency, false, prng_seed,
+        debug_level, device));
+}
+
+inline uncertainty_planning_core::SE3SimulatorPtr MakeSE3Simulator(
+    const sdf_tools::TaggedObjectCollisionMapGrid& environment, const sdf_tools::SignedDistanceField& environment_sdf,
+    const simple_particle_contact_simulator::SurfaceNormalGrid& surface_normals_grid, const SolverParameters& solver_config,
+    const double simulation_controller_frequency, const uint64_t prng_seed, const int32_t debug_level, const int32_t device = 0) {
+    using namespace uncertainty_planning_core;
+    return SE3SimulatorPtr(new simple_particle_contact_simulator::HipParticleContactSimulator<
+                           tnuva_robot_models::TnuvaSE3Robot<PRNG>, SE3Config, PRNG, SE3ConfigAlloc>(
+        environment, environment_sdf, surface_normals_grid, solver_config, simulation_controller_frequency, false, prng_seed,
+        debug_level, device));
+}
+
+inline uncertainty_planning_core::LinkedSimulatorPtr MakeLinkedSimulator(
+    const sdf_tools::TaggedObjectCollisionMapGrid& environment, const sdf_tools::SignedDistanceField& environment_sdf,
+    const simple_particle_contact_simulator::SurfaceNormalGrid& surface_normals_grid, const SolverParameters& solver_config,
+    const double simulation_controller_frequency, const uint64_t prng_seed, const int32_t debug_level, const int32_t device = 0) {
+    using namespace uncertainty_planning_core;
+    return LinkedSimulatorPtr(new simple_particle_contact_simulator::HipParticleContactSimulator<
+                              tnuva_robot_models::TnuvaLinkedRobot<PRNG>, LinkedConfig, PRNG, LinkedConfigAlloc>(
+        environment, environment_sdf, surface_normals_grid, solver_config, simulation_controller_frequency, false, prng_seed,
+        debug_level, device));
+}
+
+}  // namespace fast_kinematic_simulator
+
+#endif

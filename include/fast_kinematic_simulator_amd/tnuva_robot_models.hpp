@@ -1,0 +1,359 @@
+/*
+ * tnuva_robot_models.hpp — the robot models the planner hands the simulator,
+ * re-declared over the flattened description the GPU uses.
+ *
+ * Reference: tnuva_robot_models::TnuvaSE2Robot / TnuvaSE3Robot / TnuvaLinkedRobot
+ * (TNUVA:26-615): arc_utilities PointSphereBasic*Robot models plus per-DOF
+ * SimplePIDController + TruncatedNormalUncertainVelocityActuator groups.  Here each
+ * class keeps the same constructor arguments (TNUVA:109-132, 293-325, 486-517), the
+ * same configuration type, position semantics (SetPosition enforces joint limits /
+ * wraps angles; ResetPosition also zeroes the controllers, TNUVA:524-536), the
+ * robot-model interface the simulator receives (SimpleRobotModelInterface: Clone,
+ * GetPosition, SetPosition, ComputeConfigurationDistanceTo), and the controller state a
+ * mutable robot carries between simulator calls.  Kinematics, noise and control run on
+ * the GPU from the flattened fks::RobotDescription each model builds once
+ * (HipDescription()); the planner never needs host FK from these classes.
+ */
+#ifndef FAST_KINEMATIC_SIMULATOR_AMD_TNUVA_ROBOT_MODELS_HPP
+#define FAST_KINEMATIC_SIMULATOR_AMD_TNUVA_ROBOT_MODELS_HPP
+
+#include <cmath>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "fast_kinematic_simulator_amd/hip_particle_contact_simulator.hpp"
+#include "fast_kinematic_simulator_amd/simulator_interface.hpp"
+#include "fks_portable_math.h"
+
+namespace simple_robot_models {
+
+/* PointSphereGeometry: link-frame points (x, y, z, w); POINTS use w = 1 (SPCS:930-932) */
+class PointSphereGeometry {
+  public:
+    enum MODEL_GEOMETRY_TYPE { POINTS, SPHERES };
+    PointSphereGeometry() : type_(POINTS), points_(std::make_shared<std::vector<fks_planner_types::Vector4d>>()) {}
+    PointSphereGeometry(const MODEL_GEOMETRY_TYPE type, const std::shared_ptr<const std::vector<fks_planner_types::Vector4d>>& points)
+        : type_(type), points_(points) {}
+    MODEL_GEOMETRY_TYPE GeometryType() const { return type_; }
+    const std::shared_ptr<const std::vector<fks_planner_types::Vector4d>>& Geometry() const { return points_; }
+
+  private:
+    MODEL_GEOMETRY_TYPE type_;
+    std::shared_ptr<const std::vector<fks_planner_types::Vector4d>> points_;
+};
+
+}  // namespace simple_robot_models
+
+namespace tnuva_robot_models {
+
+namespace detail {
+inline std::vector<double> flatten_points(const simple_robot_models::PointSphereGeometry& g) {
+    std::vector<double> xyzw;
+    for (const auto& p : *g.Geometry()) xyzw.insert(xyzw.end(), {p(0), p(1), p(2), p(3)});
+    return xyzw;
+}
+/* the per-axis gains of an SE2/SE3_ROBOT_CONFIG (TNUVA:43-107, 227-291) */
+template <typename C>
+fks_dof_controller translation(const C& c) {
+    return fks_dof_controller{c.kp, c.ki, c.kd, c.integral_clamp, c.velocity_limit, c.acceleration_limit,
+                              c.max_sensor_noise, c.max_actuator_proportional_noise, c.max_actuator_minimum_noise};
+}
+template <typename C>
+fks_dof_controller rotation(const C& c) {
+    return fks_dof_controller{c.r_kp, c.r_ki, c.r_kd, c.r_integral_clamp, c.r_velocity_limit, c.r_acceleration_limit,
+                              c.r_max_sensor_noise, c.r_max_actuator_proportional_noise, c.r_max_actuator_minimum_noise};
+}
+}  // namespace detail
+
+/* gains of the translational (kp ...) and rotational (r_kp ...) axes, TNUVA:43-107 / 227-291 */
+struct AXIS_ROBOT_CONFIG {
+    double kp = 0.0, ki = 0.0, kd = 0.0, integral_clamp = 0.0, velocity_limit = 0.0, acceleration_limit = 0.0,
+           max_sensor_noise = 0.0, max_actuator_proportional_noise = 0.0, max_actuator_minimum_noise = 0.0;
+    double r_kp = 0.0, r_ki = 0.0, r_kd = 0.0, r_integral_clamp = 0.0, r_velocity_limit = 0.0, r_acceleration_limit = 0.0,
+           r_max_sensor_noise = 0.0, r_max_actuator_proportional_noise = 0.0, r_max_actuator_minimum_noise = 0.0;
+    AXIS_ROBOT_CONFIG() {}
+    AXIS_ROBOT_CONFIG(double in_kp, double in_ki, double in_kd, double in_integral_clamp, double in_velocity_limit,
+                      double in_acceleration_limit, double in_max_sensor_noise, double in_max_actuator_proportional_noise,
+                      double in_max_actuator_minimum_noise, double in_r_kp, double in_r_ki, double in_r_kd,
+                      double in_r_integral_clamp, double in_r_velocity_limit, double in_r_acceleration_limit,
+                      double in_r_max_sensor_noise, double in_r_max_actuator_proportional_noise,
+                      double in_r_max_actuator_minimum_noise)
+        : kp(in_kp), ki(in_ki), kd(in_kd), integral_clamp(in_integral_clamp), velocity_limit(in_velocity_limit),
+          acceleration_limit(in_acceleration_limit), max_sensor_noise(in_max_sensor_noise),
+          max_actuator_proportional_noise(in_max_actuator_proportional_noise),
+          max_actuator_minimum_noise(in_max_actuator_minimum_noise), r_kp(in_r_kp), r_ki(in_r_ki), r_kd(in_r_kd),
+          r_integral_clamp(in_r_integral_clamp), r_velocity_limit(in_r_velocity_limit),
+          r_acceleration_limit(in_r_acceleration_limit), r_max_sensor_noise(in_r_max_sensor_noise),
+          r_max_actuator_proportional_noise(in_r_max_actuator_proportional_noise),
+          r_max_actuator_minimum_noise(in_r_max_actuator_minimum_noise) {}
+};
+
+/* What the HIP simulator needs from a DerivedRobotType: the flattened description, the
+ * PID state (per dof: error integral, then per dof: last error) and the conversion of
+ * configurations to and from the flat form of fks_capi.h. */
+template <typename Configuration>
+class HipRobotState {
+  public:
+    virtual ~HipRobotState() {}
+    const fks::RobotDescription& HipDescription() const { return *desc_; }
+    const std::vector<double>& ControllerState() const { return pid_; }
+    void SetControllerState(const std::vector<double>& state) {
+        if (state.size() != pid_.size()) throw std::invalid_argument("controller state has the wrong size");
+        pid_ = state;
+    }
+    virtual void ResetControllers() { std::fill(pid_.begin(), pid_.end(), 0.0); }
+    bool ControllersAreZero() const {
+        for (double v : pid_)
+            if (v != 0.0) return false;
+        return true;
+    }
+    virtual std::vector<double> ToFlat(const Configuration& config) const = 0;
+    virtual Configuration FromFlat(const double* flat) const = 0;
+
+  protected:
+    void InitState(const std::shared_ptr<const fks::RobotDescription>& desc) {
+        desc_ = desc;
+        pid_.assign(2 * (size_t)desc->NumDofs(), 0.0);
+    }
+    std::shared_ptr<const fks::RobotDescription> desc_;
+    std::vector<double> pid_;
+};
+
+/* ---------------------------------------------------------------- SE(2) (TNUVA:26-199) */
+template <typename Generator>
+class TnuvaSE2Robot
+    : public simple_robot_model_interface::SimpleRobotModelInterface<simple_se2_robot_model::SimpleSE2Configuration,
+                                                                     simple_se2_robot_model::SimpleSE2ConfigAlloc>,
+      public HipRobotState<simple_se2_robot_model::SimpleSE2Configuration> {
+  public:
+    typedef simple_se2_robot_model::SimpleSE2Configuration Configuration;
+    typedef AXIS_ROBOT_CONFIG SE2_ROBOT_CONFIG;
+
+    /* TNUVA:109-132 */
+    TnuvaSE2Robot(const Configuration& initial_position, const double position_distance_weight,
+                  const double rotation_distance_weight, const std::string& link_name,
+                  const simple_robot_models::PointSphereGeometry& geometry, const SE2_ROBOT_CONFIG& robot_config)
+        : link_name_(link_name) {
+        auto d = std::make_shared<fks::RobotDescription>();
+        d->type = FKS_ROBOT_SE2;
+        d->num_links = 1;
+        d->num_dofs = 3;
+        d->AddGeometry(0, detail::flatten_points(geometry));
+        d->controllers = {detail::translation(robot_config), detail::translation(robot_config), detail::rotation(robot_config)};
+        d->distance_weights = {position_distance_weight, rotation_distance_weight};
+        InitState(d);
+        SetPosition(initial_position);
+    }
+    simple_robot_model_interface::SimpleRobotModelInterface<Configuration, simple_se2_robot_model::SimpleSE2ConfigAlloc>* Clone()
+        const override {
+        return new TnuvaSE2Robot(*this);
+    }
+    const Configuration& GetPosition() const override { return config_; }
+    /* SetPosition: theta wrapped to [-pi, pi] */
+    const Configuration& SetPosition(const Configuration& config) override {
+        config_ = Configuration(config(0), config(1), fks_math::enforce_continuous_revolute_bounds(config(2)));
+        return config_;
+    }
+    /* TNUVA:139-150 */
+    const Configuration& ResetPosition(const Configuration& position) {
+        this->ResetControllers();
+        return SetPosition(position);
+    }
+    double ComputeConfigurationDistanceTo(const Configuration& t) const override {
+        const double dx = t(0) - config_(0), dy = t(1) - config_(1);
+        const double dr = fks_math::enforce_continuous_revolute_bounds(t(2) - config_(2));
+        const auto& w = this->HipDescription().distance_weights;
+        return w[0] * std::sqrt(dx * dx + dy * dy) + w[1] * std::fabs(dr);
+    }
+    std::vector<double> ToFlat(const Configuration& c) const override { return {c(0), c(1), c(2)}; }
+    Configuration FromFlat(const double* f) const override { return Configuration(f[0], f[1], f[2]); }
+    const std::string& GetLinkName() const { return link_name_; }
+
+  private:
+    std::string link_name_;
+    Configuration config_;
+};
+
+/* ---------------------------------------------------------------- SE(3) (TNUVA:201-413) */
+template <typename Generator>
+class TnuvaSE3Robot
+    : public simple_robot_model_interface::SimpleRobotModelInterface<simple_se3_robot_model::SimpleSE3Configuration,
+                                                                     simple_se3_robot_model::SimpleSE3ConfigAlloc>,
+      public HipRobotState<simple_se3_robot_model::SimpleSE3Configuration> {
+  public:
+    typedef simple_se3_robot_model::SimpleSE3Configuration Configuration;
+    typedef AXIS_ROBOT_CONFIG SE3_ROBOT_CONFIG;
+
+    /* TNUVA:293-325: x, y, z use the translational gains, rx, ry, rz the rotational */
+    TnuvaSE3Robot(const Configuration& initial_position, const double position_distance_weight,
+                  const double rotation_distance_weight, const std::string& link_name,
+                  const simple_robot_models::PointSphereGeometry& geometry, const SE3_ROBOT_CONFIG& robot_config)
+        : link_name_(link_name) {
+        auto d = std::make_shared<fks::RobotDescription>();
+        d->type = FKS_ROBOT_SE3;
+        d->num_links = 1;
+        d->num_dofs = 6;
+        d->AddGeometry(0, detail::flatten_points(geometry));
+        const fks_dof_controller t = detail::translation(robot_config), r = detail::rotation(robot_config);
+        d->controllers = {t, t, t, r, r, r};
+        d->distance_weights = {position_distance_weight, rotation_distance_weight};
+        InitState(d);
+        SetPosition(initial_position);
+    }
+    simple_robot_model_interface::SimpleRobotModelInterface<Configuration, simple_se3_robot_model::SimpleSE3ConfigAlloc>* Clone()
+        const override {
+        return new TnuvaSE3Robot(*this);
+    }
+    const Configuration& GetPosition() const override { return config_; }
+    const Configuration& SetPosition(const Configuration& config) override {
+        config_ = config;
+        return config_;
+    }
+    const Configuration& ResetPosition(const Configuration& position) {
+        this->ResetControllers();
+        return SetPosition(position);
+    }
+    /* weighted translation distance + rotation angle between the poses */
+    double ComputeConfigurationDistanceTo(const Configuration& t) const override {
+        const double* a = config_.data34();
+        const double* b = t.data34();
+        const double dx = b[3] - a[3], dy = b[7] - a[7], dz = b[11] - a[11];
+        double trace = 0.0; /* trace(Ra^T Rb) */
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) trace += a[4 * r + c] * b[4 * r + c];
+        const double cosang = std::max(-1.0, std::min(1.0, 0.5 * (trace - 1.0)));
+        const auto& w = this->HipDescription().distance_weights;
+        return w[0] * std::sqrt(dx * dx + dy * dy + dz * dz) + w[1] * std::acos(cosang);
+    }
+    std::vector<double> ToFlat(const Configuration& c) const override { return std::vector<double>(c.data34(), c.data34() + 12); }
+    Configuration FromFlat(const double* f) const override { return Configuration::FromRowMajor34(f); }
+    const std::string& GetLinkName() const { return link_name_; }
+
+  private:
+    std::string link_name_;
+    Configuration config_;
+};
+
+/* ---------------------------------------------------------------- linked (TNUVA:415-615) */
+template <typename Generator>
+class TnuvaLinkedRobot
+    : public simple_robot_model_interface::SimpleRobotModelInterface<simple_linked_robot_model::SimpleLinkedConfiguration,
+                                                                     simple_linked_robot_model::SimpleLinkedConfigAlloc>,
+      public HipRobotState<simple_linked_robot_model::SimpleLinkedConfiguration> {
+  public:
+    typedef simple_linked_robot_model::SimpleLinkedConfiguration Configuration;
+
+    /* TNUVA:420-457 */
+    struct LINKED_ROBOT_CONFIG {
+        double kp = 0.0, ki = 0.0, kd = 0.0, integral_clamp = 0.0, velocity_limit = 0.0, acceleration_limit = 0.0,
+               max_sensor_noise = 0.0, max_actuator_proportional_noise = 0.0, max_actuator_minimum_noise = 0.0;
+        LINKED_ROBOT_CONFIG() {}
+        LINKED_ROBOT_CONFIG(double in_kp, double in_ki, double in_kd, double in_integral_clamp, double in_velocity_limit,
+                            double in_acceleration_limit, double in_max_sensor_noise, double in_max_actuator_proportional_noise,
+                            double in_max_actuator_minimum_noise)
+            : kp(in_kp), ki(in_ki), kd(in_kd), integral_clamp(in_integral_clamp), velocity_limit(in_velocity_limit),
+              acceleration_limit(in_acceleration_limit), max_sensor_noise(in_max_sensor_noise),
+              max_actuator_proportional_noise(in_max_actuator_proportional_noise),
+              max_actuator_minimum_noise(in_max_actuator_minimum_noise) {}
+    };
+
+    /* TNUVA:486-517.  Geometries are attached to links by name; allowed self-collision
+     * pairs index link_geometries (the indices CheckIfSelfCollisionAllowed receives,
+     * SPCS:1008, 1193).  Throws std::invalid_argument when the joint-config count differs
+     * from the active-joint count (TNUVA:515). */
+    TnuvaLinkedRobot(const fks_planner_types::Isometry3d& base_transform,
+                     const std::vector<simple_linked_robot_model::RobotLink>& links,
+                     const std::vector<simple_linked_robot_model::RobotJoint>& joints, const Configuration& initial_position,
+                     const std::vector<double>& joint_distance_weights,
+                     const std::vector<std::pair<std::string, simple_robot_models::PointSphereGeometry>>& link_geometries,
+                     const std::vector<std::pair<size_t, size_t>>& allowed_self_collisions,
+                     const std::vector<LINKED_ROBOT_CONFIG>& joint_configs) {
+        auto d = std::make_shared<fks::RobotDescription>();
+        d->type = FKS_ROBOT_LINKED;
+        d->num_links = (int32_t)links.size();
+        for (int i = 0; i < 12; ++i) d->base_transform[i] = base_transform.data34()[i];
+        int32_t active = 0;
+        for (const auto& j : joints) {
+            fks_joint_desc jd{};
+            jd.parent_link = (int32_t)j.parent_link_index;
+            jd.child_link = (int32_t)j.child_link_index;
+            jd.type = (int32_t)j.joint_model.GetType();
+            for (int i = 0; i < 12; ++i) jd.origin[i] = j.joint_transform.data34()[i];
+            for (int i = 0; i < 3; ++i) jd.axis[i] = j.joint_axis(i);
+            jd.limit_lower = j.joint_model.GetLimits().first;
+            jd.limit_upper = j.joint_model.GetLimits().second;
+            d->joints.push_back(jd);
+            if (!j.joint_model.IsFixed()) {
+                active++;
+                joint_models_.push_back(j.joint_model);
+            }
+        }
+        if ((size_t)active != joint_configs.size())
+            throw std::invalid_argument("Number of joint configs must match number of active joints");
+        d->num_dofs = active;
+        for (const auto& g : link_geometries) {
+            int32_t link = -1;
+            for (size_t l = 0; l < links.size(); ++l)
+                if (links[l].link_name == g.first) link = (int32_t)l;
+            if (link < 0) throw std::invalid_argument("link geometry names an unknown link: " + g.first);
+            d->AddGeometry(link, detail::flatten_points(g.second));
+        }
+        for (const auto& p : allowed_self_collisions) d->AllowSelfCollision((int32_t)p.first, (int32_t)p.second);
+        for (const auto& c : joint_configs)
+            d->controllers.push_back(fks_dof_controller{c.kp, c.ki, c.kd, c.integral_clamp, c.velocity_limit, c.acceleration_limit,
+                                                        c.max_sensor_noise, c.max_actuator_proportional_noise,
+                                                        c.max_actuator_minimum_noise});
+        d->distance_weights = joint_distance_weights;
+        if (d->distance_weights.size() != (size_t)active) throw std::invalid_argument("one distance weight per active joint");
+        InitState(d);
+        SetPosition(initial_position);
+    }
+    simple_robot_model_interface::SimpleRobotModelInterface<Configuration, simple_linked_robot_model::SimpleLinkedConfigAlloc>* Clone()
+        const override {
+        return new TnuvaLinkedRobot(*this);
+    }
+    const Configuration& GetPosition() const override { return config_; }
+    /* SetPosition: each active joint's model with the new value (limits / wrap enforced) */
+    const Configuration& SetPosition(const Configuration& config) override {
+        if (config.size() != joint_models_.size()) throw std::invalid_argument("configuration has the wrong number of joints");
+        config_.clear();
+        for (size_t k = 0; k < config.size(); ++k) config_.push_back(joint_models_[k].CopyWithNewValue(config[k].GetValue()));
+        return config_;
+    }
+    /* TNUVA:524-536 */
+    const Configuration& ResetPosition(const Configuration& position) {
+        this->ResetControllers();
+        return SetPosition(position);
+    }
+    /* weighted joint-space distance (the simulation shortcut's metric, SPCS:898) */
+    double ComputeConfigurationDistanceTo(const Configuration& t) const override {
+        const auto& w = this->HipDescription().distance_weights;
+        double sum = 0.0;
+        for (size_t k = 0; k < config_.size(); ++k) {
+            const double d = w[k] * std::fabs(config_[k].SignedDistance(t[k].GetValue()));
+            sum += d * d;
+        }
+        return std::sqrt(sum);
+    }
+    std::vector<double> ToFlat(const Configuration& c) const override {
+        std::vector<double> f;
+        for (const auto& j : c) f.push_back(j.GetValue());
+        return f;
+    }
+    Configuration FromFlat(const double* f) const override {
+        Configuration c;
+        for (size_t k = 0; k < joint_models_.size(); ++k) c.push_back(joint_models_[k].CopyWithNewValue(f[k]));
+        return c;
+    }
+
+  private:
+    std::vector<simple_linked_robot_model::SimpleJointModel> joint_models_; /* active joints, in order */
+    Configuration config_;
+};
+
+}  // namespace tnuva_robot_models
+
+#endif

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define FKS_ABI_VERSION 2
+#define FKS_ABI_VERSION 3
 
 typedef enum {
     FKS_OK = 0,
@@ -70,17 +70,12 @@ typedef enum {
 #define FKS_PARTICLE_ERR_NORMAL_OOB 0x2u         /* SPCS:1882 surface normal lookup out of bounds        */
 #define FKS_PARTICLE_ERR_ZERO_DIRECTION 0x4u     /* SPCS:113-114 best-normal query with zero motion      */
 #define FKS_PARTICLE_ERR_RNG_EXHAUSTED 0x8u      /* truncated-normal rejection exceeded its draw budget  */
-#define FKS_PARTICLE_ERR_SELF_CAPACITY 0x10u     /* > FKS_MAX_SELF_CELLS colliding cells or
-                                                    > FKS_MAX_SELF_LINKS links in one colliding cell     */
+#define FKS_PARTICLE_ERR_SELF_CAPACITY 0x10u     /* reserved: ABI <= 2 capped the self-collision impulse
+                                                    solve; since ABI 3 it is unbounded (never raised)    */
 #define FKS_PARTICLE_ERR_KEY_RANGE 0x20u         /* non-finite point in the self-collision grid          */
 #define FKS_PARTICLE_ERR_MICROSTEP_CAP 0x40u     /* microsteps per controller step exceeded 2^20         */
 #define FKS_PARTICLE_ERR_SELF_SINGULAR 0x80u     /* NaN self-collision correction (assert SPCS:1151-1153) */
 #define FKS_PARTICLE_ERR_NO_NOISE_BIN 0x100u     /* sampled actuator: no bin holds the command (UNC:152-153) */
-
-/* capacities of the self-collision impulse solve (both the HIP path and the oracle
- * flag FKS_PARTICLE_ERR_SELF_CAPACITY beyond them) */
-#define FKS_MAX_SELF_CELLS 64
-#define FKS_MAX_SELF_LINKS 8
 
 /* SimulatorSolverParameters (SPCS:345-369); booleans widened to uint32 */
 typedef struct {
@@ -217,6 +212,11 @@ typedef struct {
     double call_ms;               /* host wall time of the whole call */
     uint64_t calls;               /* number of calls these counters cover */
     uint64_t least_squares_rows;  /* sum over resolver iterations of the stacked-Jacobian rows (3 x corrected points) */
+    /* ABI 3: the self-collision branch of the resolver (SPCS:983-1275) */
+    uint64_t self_collision_checks; /* CheckCollision calls (SPCS:1418-1436) whose self-collision map came back
+                                       non-empty, i.e. ExtractSelfCollidingPoints produced corrections (SPCS:1264-1271) */
+    uint64_t self_corrected_points; /* sum over resolver iterations of the points whose correction holds a
+                                       self-collision term (SPCS:1846-1853, 1909-1916) */
 } fks_call_counters;
 
 typedef struct fks_context fks_context;
@@ -257,6 +257,18 @@ fks_status fks_reverse_simulate(fks_context* ctx, const double* starts, uint64_t
                                 int32_t allow_contacts, double* out_positions,
                                 uint8_t* out_collided, uint32_t* out_microsteps,
                                 uint32_t* out_resolver_iterations, uint32_t* out_error_flags);
+
+/* ForwardSimulateMutableRobot (SPCS:843-919) / ReverseSimulateMutableRobot (SPCS:838-841)
+ * for a batch: particle i starts from starts[i] (SetPosition: joint limits / angle wrap)
+ * with its PID controllers as the robot holds them, not zeroed as ResetPosition does
+ * (TNUVA:524-536).  controller_state (n x 2D doubles, in/out): per dof the controller's
+ * error integral, then per dof its last error (SimplePIDController PID:53-136; D = dofs, 3 for
+ * SE(2), 6 for SE(3)); on return it holds each particle's controllers when it stopped.
+ * All zeros gives fks_forward_simulate's results. */
+fks_status fks_forward_simulate_mutable(fks_context* ctx, const double* starts, uint64_t n, const double* targets,
+                                        uint64_t num_targets, int32_t allow_contacts, double* controller_state,
+                                        double* out_positions, uint8_t* out_collided, uint32_t* out_microsteps,
+                                        uint32_t* out_resolver_iterations, uint32_t* out_error_flags);
 
 /* Same call with every buffer already in device memory of the context's GPU.
  * first_particle_id: global id of particle 0 of this shard (the RNG stream is
@@ -324,6 +336,14 @@ fks_status fks_forward_simulate_traced(fks_context* ctx, const double* starts, u
                                        uint32_t* out_resolver_iterations, uint32_t* out_error_flags,
                                        const fks_trace* trace);
 
+/* ForwardSimulateMutableRobot(..., trace, enable_tracing = true, ...) (SPCS:843-919) for a
+ * batch: fks_forward_simulate_mutable's controller state in/out plus the trace. */
+fks_status fks_forward_simulate_traced_mutable(fks_context* ctx, const double* starts, uint64_t n, const double* targets,
+                                               uint64_t num_targets, int32_t allow_contacts, double* controller_state,
+                                               double* out_positions, uint8_t* out_collided, uint32_t* out_microsteps,
+                                               uint32_t* out_resolver_iterations, uint32_t* out_error_flags,
+                                               const fks_trace* trace);
+
 /* Kinematics of a batch of configurations (host buffers), the pieces the reference's
  * host-side helpers build on, computed with the simulation kernels' own FK:
  *   FKS_KIN_LINK_TRANSFORMS     out: n x num_links x 12 (3x4 row-major link transforms
@@ -363,13 +383,13 @@ enum fks_phase {
     FKS_PHASE_PARTICLE = 0,        /* whole particle: ForwardSimulateMutableRobot SPCS:843-919 */
     FKS_PHASE_CONTROL = 1,         /* controller + sensor noise SPCS:861-876 */
     FKS_PHASE_STEP_SETUP = 2,      /* microstep count estimate SPCS:1549-1572 */
-    FKS_PHASE_MICRO_INPUT = 3,     /* ApplyControlInput incl. actuator noise SPCS:1582 */
-    FKS_PHASE_MICRO_FK = 4,        /* UpdatePosition of the microstep */
-    FKS_PHASE_ENV_CHECK = 5,       /* CheckEnvironmentCollision SPCS:1438-1459 */
-    FKS_PHASE_SELF_CHECK = 6,      /* CollectSelfCollisions SPCS:1461-1544 */
+    FKS_PHASE_MICRO_INPUT = 3,     /* ApplyControlInput incl. actuator noise SPCS:1599, TNUVA:568-596 */
+    FKS_PHASE_MICRO_FK = 4,        /* SetPosition (FK) of the post-action configuration SPCS:1600-1601 */
+    FKS_PHASE_ENV_CHECK = 5,       /* CheckEnvironmentCollision SPCS:921-981 */
+    FKS_PHASE_SELF_CHECK = 6,      /* CollectSelfCollisions SPCS:1183-1275 (+ ExtractSelfCollidingPoints 983-1171) */
     FKS_PHASE_CORRECTIONS = 7,     /* CollectPointCorrectionsAndJacobians SPCS:1818-1939 */
-    FKS_PHASE_SOLVE = 8,           /* ColPivHouseholderQR solve SPCS:1617-1619 */
-    FKS_PHASE_RESOLVE_APPLY = 9,   /* correction step sizing / application SPCS:1620-1656 */
+    FKS_PHASE_SOLVE = 8,           /* ComputeResolverCorrectionStep{StackedJacobian,IndividualJacobians} SPCS:1966-1998 */
+    FKS_PHASE_RESOLVE_APPLY = 9,   /* correction step sizing / application SPCS:1630-1690 */
     FKS_PHASE_OUTPUT = 10,         /* reached configuration + counters */
     /* event counts (not cycles) of the profiling build */
     FKS_PHASE_ENV_ROUNDS_SKIPPED = 11,   /* 64-point rounds proven free (no SDF reads) */
@@ -397,6 +417,22 @@ fks_status fks_get_launch_geometry(const fks_context* ctx, uint32_t* resident_wa
  * every value (the resting state between segments is exact).  No reference
  * counterpart (SPCS:795 runs each particle whole on one OpenMP thread). */
 fks_status fks_set_segment_steps(fks_context* ctx, uint32_t controller_steps);
+/* Scheduling policy of segmented batches (ABI 3; no reference counterpart, results are
+ * bit-identical for every value):
+ *   heavy_resolver_per_step: a segment whose particle averaged at least this many
+ *     resolver iterations per controller step is contact-heavy and its wave keeps the
+ *     particle's next segment instead of returning it to the round-robin (0 = off;
+ *     default 2; at most 65536);
+ *   heavy_priority: issue priority (s_setprio 0..2) of a wave carrying a contact-heavy
+ *     particle (default 1 = raised to 2 for heavy segments only; 0 = never raised;
+ *     2 = also 1 for particles that fell behind the round-robin).
+ * The priority is reset to 0 at the start of every segment a wave claims. */
+fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_step, uint32_t heavy_priority);
+/* SimpleParticleContactSimulator(..., simulate_with_individual_jacobians, ...) (SPCS:420-423,
+ * 1629): 0 = ComputeResolverCorrectionStepStackedJacobian (SPCS:1990-1998; what the factories
+ * FKS.cpp:22,45,68 hard-wire, the default), 1 = ComputeResolverCorrectionStepIndividualJacobians
+ * (SPCS:1966-1988: one ColPivHouseholderQR solve per corrected point, summed in point order). */
+fks_status fks_set_individual_jacobians(fks_context* ctx, int32_t simulate_with_individual_jacobians);
 
 /* sums over every call since fks_create / fks_reset_total_counters */
 fks_status fks_get_total_counters(const fks_context* ctx, fks_call_counters* out);

@@ -39,7 +39,7 @@ def lib():
             POINTER(C.Environment), POINTER(C.SolverParams), c_double, c_uint64, c_uint64, POINTER(C.RobotDesc),
             POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_uint64, c_int32, c_int32, c_int32, POINTER(c_double),
             POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32), POINTER(C.Statistics),
-            POINTER(C.CallCounters)]
+            POINTER(C.CallCounters), c_int32, POINTER(c_double)]
         L.oracle_check_config_collision.restype = c_int32
         L.oracle_check_config_collision.argtypes = [
             POINTER(C.Environment), POINTER(C.SolverParams), POINTER(C.RobotDesc), POINTER(c_double), c_uint64, c_double,
@@ -83,8 +83,12 @@ def _p(a, t):
 
 
 def forward_simulate(env, robot, solver, frequency, seed, starts, targets, allow_contacts=True, call_index=0,
-                     first_particle_id=0, rng_mode=RNG_COUNTER, threads=0):
-    """ForwardSimulateRobots on the CPU oracle.  Returns a dict like the HIP path."""
+                     first_particle_id=0, rng_mode=RNG_COUNTER, threads=0, individual_jacobians=False,
+                     controller_state=None):
+    """ForwardSimulateRobots on the CPU oracle.  Returns a dict like the HIP path.
+    individual_jacobians: the simulate_with_individual_jacobians constructor flag (SPCS:420).
+    controller_state: None (ResetPosition zeroes the PIDs) or an (n, 2D) float64 array of PID
+    states, updated in place (ForwardSimulateMutableRobot, SPCS:843-919)."""
     L = lib()
     from fast_kinematic_simulator_amd import _capi as C
 
@@ -106,7 +110,9 @@ def forward_simulate(env, robot, solver, frequency, seed, starts, targets, allow
                                    c_uint64(int(call_index)), ctypes.byref(desc), _p(starts, c_double), n,
                                    _p(targets, c_double), targets.shape[0], int(first_particle_id), 1 if allow_contacts else 0,
                                    int(rng_mode), int(threads), _p(out, c_double), _p(coll, c_uint8), _p(micro, c_uint32),
-                                   _p(res, c_uint32), _p(err, c_uint32), ctypes.byref(stats), ctypes.byref(cc))
+                                   _p(res, c_uint32), _p(err, c_uint32), ctypes.byref(stats), ctypes.byref(cc),
+                                   1 if individual_jacobians else 0,
+                                   _p(controller_state, c_double) if controller_state is not None else None)
     del keep_env, keep_robot
     if st != 0:
         raise RuntimeError(f"oracle_forward_simulate failed ({st})")

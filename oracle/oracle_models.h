@@ -60,6 +60,13 @@ class SimplePIDController {
         last_error_ = current_error;
         return (current_error * kp_) + (error_integral_ * ki_) + (error_derivative * kd_);
     }
+    /* the controller state a mutable robot carries between calls (fks_forward_simulate_mutable) */
+    double ErrorIntegral() const { return error_integral_; }
+    double LastError() const { return last_error_; }
+    void SetState(double error_integral, double last_error) {
+        error_integral_ = error_integral;
+        last_error_ = last_error;
+    }
 
   private:
     double kp_, ki_, kd_, integral_clamp_, error_integral_, last_error_;
@@ -302,6 +309,22 @@ class RobotModel {
     virtual bool CheckIfSelfCollisionAllowed(size_t a, size_t b) const = 0;
     virtual const LinkGeometries& GetLinkGeometries() const = 0;
     virtual size_t NumDofs() const = 0;
+    /* PID state per dof: out[d] = error integral, out[D + d] = last error */
+    void GetControllerState(double* out) const {
+        const size_t D = NumDofs();
+        for (size_t d = 0; d < D; ++d) {
+            out[d] = Controller(d).ErrorIntegral();
+            out[D + d] = Controller(d).LastError();
+        }
+    }
+    void SetControllerState(const double* in) {
+        const size_t D = NumDofs();
+        for (size_t d = 0; d < D; ++d) Controller(d).SetState(in[d], in[D + d]);
+    }
+
+  protected:
+    virtual SimplePIDController& Controller(size_t dof) = 0;
+    const SimplePIDController& Controller(size_t dof) const { return const_cast<RobotModel*>(this)->Controller(dof); }
 };
 
 /* ---------------- linked robot (TNUVA:415-615 over PointSphereBasicLinkedRobot) ---------------- */
@@ -348,6 +371,9 @@ class LinkedRobot : public RobotModel {
     const LinkGeometries& GetLinkGeometries() const override { return link_geometries_; }
     size_t NumDofs() const override { return num_active_joints_; }
 
+  protected:
+    SimplePIDController& Controller(size_t dof) override { return joint_controller_groups_[dof].controller; }
+
   private:
     void UpdateTransforms();
     bool IsAncestorOrSelf(int64_t maybe_ancestor, int64_t link) const;
@@ -382,6 +408,9 @@ class SE2Robot : public RobotModel {
     const LinkGeometries& GetLinkGeometries() const override { return link_geometries_; }
     size_t NumDofs() const override { return 3; }
 
+  protected:
+    SimplePIDController& Controller(size_t dof) override { return axis_[dof].controller; }
+
   private:
     LinkGeometries link_geometries_;
     JointControllerGroup axis_[3];
@@ -407,6 +436,9 @@ class SE3Robot : public RobotModel {
     bool CheckIfSelfCollisionAllowed(size_t, size_t) const override { return true; }
     const LinkGeometries& GetLinkGeometries() const override { return link_geometries_; }
     size_t NumDofs() const override { return 6; }
+
+  protected:
+    SimplePIDController& Controller(size_t dof) override { return axis_[dof].controller; }
 
   private:
     LinkGeometries link_geometries_;

@@ -46,6 +46,8 @@ struct ParticleCounters {
     uint64_t controller_steps = 0;
     uint64_t sdf_bytes = 0;
     uint64_t lsq_rows = 0;
+    uint64_t self_checks = 0; /* CheckCollision calls with a non-empty self-collision map */
+    uint64_t self_points = 0; /* corrected points holding a self-collision term */
     uint32_t error_flags = 0;
     fks_statistics stats;
     struct TraceSink* trace = nullptr; /* ForwardSimulationStepTrace of this particle (traced calls only) */
@@ -386,6 +388,21 @@ std::vector<double> colpiv_qr_solve(const std::vector<double>& Jrm, size_t R, si
     return x;
 }
 
+/* ComputeResolverCorrectionStepIndividualJacobians (SPCS:1966-1988): each corrected
+ * point's 3 x D block solved on its own, the steps summed in point order (the first
+ * assigned, later ones raw + step).  No corrected point: the zero step, as the stacked
+ * solve of an empty system returns. */
+std::vector<double> individual_jacobians_solve(const std::vector<double>& Jrm, size_t R, size_t D, const std::vector<double>& b) {
+    std::vector<double> raw(D, 0.0);
+    for (size_t r0 = 0; r0 < R; r0 += 3) {
+        const std::vector<double> Jb(Jrm.begin() + (long)(r0 * D), Jrm.begin() + (long)((r0 + 3) * D));
+        const std::vector<double> bb(b.begin() + (long)r0, b.begin() + (long)r0 + 3);
+        const std::vector<double> step = colpiv_qr_solve(Jb, 3, D, bb);
+        for (size_t i = 0; i < D; ++i) raw[i] = (r0 == 0) ? step[i] : raw[i] + step[i];
+    }
+    return raw;
+}
+
 /* ---------------- the simulator ---------------- */
 struct PairHash {
     size_t operator()(const std::pair<size_t, size_t>& p) const {
@@ -416,12 +433,14 @@ struct ResolveResult {
 
 class Simulator {
   public:
-    Simulator(const fks_environment& env, const fks_solver_params& p, double freq, int32_t debug)
+    Simulator(const fks_environment& env, const fks_solver_params& p, double freq, int32_t debug,
+              bool simulate_with_individual_jacobians = false)
         : env_geom_(env.collision_map),
           sdf_(env.sdf, env.sdf_values, env.sdf_oob_value),
           normals_(env.normals, env.normal_offsets, env.normal_entries),
           solver_(p),
-          debug_level_(debug) {
+          debug_level_(debug),
+          simulate_with_individual_jacobians_(simulate_with_individual_jacobians) {
         contact_distance_threshold_ = 0.0;
         resolution_distance_threshold_ = 0.0;
         simulation_controller_frequency_ = fks_math::dabs(freq);
@@ -470,10 +489,6 @@ class Simulator {
                     link_collisions[f->first].push_back(s->first);
         if (link_collisions.size() < 2) return result;
         (*colliding_cells)++;
-        if (*colliding_cells > FKS_MAX_SELF_CELLS || by_link.size() > FKS_MAX_SELF_LINKS) {
-            pc.error_flags |= FKS_PARTICLE_ERR_SELF_CAPACITY;
-            return result;
-        }
         const double time_multiplier = 1.0 / time_interval;
         std::map<size_t, V4> momentum;
         for (auto it = by_link.begin(); it != by_link.end(); ++it) {
@@ -624,6 +639,7 @@ class Simulator {
         const bool env_collision = CheckEnvironmentCollision(current_robot, geoms, contact_distance_threshold_, pc);
         SelfMap self = CollectSelfCollisions(previous_robot, current_robot, geoms, time_interval, pc);
         const bool collided = env_collision || (self.size() > 0);
+        if (self.size() > 0) pc.self_checks++;
         return std::make_pair(collided, self);
     }
 
@@ -747,6 +763,7 @@ class Simulator {
                     env_corr = V3{g.x * penetration, g.y * penetration, g.z * penetration};
                     has_env = true;
                 }
+                if (has_self) pc.self_points++;
                 if (has_self || has_env) {
                     /* grow the dynamic Jacobian by copy, as the reference does (SPCS:1896-1906) */
                     std::vector<double> extended(J.size() + 3 * D);
@@ -826,7 +843,10 @@ class Simulator {
                                                         self_collision_map, J, b, rows, pc);
                     pc.lsq_rows += rows;
                     if (pc.error_flags) return ResolveResult{previous_configuration, collided, false, true};
-                    const std::vector<double> raw_correction_step = colpiv_qr_solve(J, rows, D, b);
+                    /* SPCS:1629: individual (SPCS:1966-1988) or stacked (SPCS:1990-1998) solve */
+                    const std::vector<double> raw_correction_step = simulate_with_individual_jacobians_
+                                                                        ? individual_jacobians_solve(J, rows, D, b)
+                                                                        : colpiv_qr_solve(J, rows, D, b);
                     const double correction_step_motion_estimate = EstimateMaxControlInputWorkspaceMotion(robot, raw_correction_step);
                     const double allowed_resolve_distance = allowed_microstep_distance;
                     const double step_fraction = fks_math::dmax(correction_step_motion_estimate / allowed_resolve_distance, 1.0);
@@ -921,6 +941,7 @@ class Simulator {
     NormalGrid normals_;
     fks_solver_params solver_;
     int32_t debug_level_;
+    bool simulate_with_individual_jacobians_; /* SPCS:384, 423, 1629 */
     double contact_distance_threshold_, resolution_distance_threshold_;
     double simulation_controller_frequency_, simulation_controller_interval_;
 };
@@ -954,11 +975,12 @@ static int forward_simulate_impl(const fks_environment* env, const fks_solver_pa
                                  const double* targets, uint64_t num_targets, uint64_t first_particle_id, int32_t allow_contacts,
                                  int32_t rng_mode, int32_t num_threads, double* out_positions, uint8_t* out_collided,
                                  uint32_t* out_microsteps, uint32_t* out_resolver_iterations, uint32_t* out_error_flags,
-                                 fks_statistics* out_stats, fks_call_counters* out_counters, const fks_trace* trace) {
+                                 fks_statistics* out_stats, fks_call_counters* out_counters, const fks_trace* trace,
+                                 int32_t individual_jacobians, double* controller_state) {
     if (!env || !params || !robot_desc || (n > 0 && (!starts || !targets || !out_positions))) return 1;
     if (n > 0 && num_targets != 1 && num_targets != n) return 1;
     if (params->resolve_correction_step_scaling_decay_iterations == 0) return 1;
-    const Simulator sim(*env, *params, frequency, 0);
+    const Simulator sim(*env, *params, frequency, 0, individual_jacobians != 0);
     std::shared_ptr<RobotModel> immutable_robot(make_robot(*robot_desc));
     if (!immutable_robot) return 1;
     const size_t W = config_width(*robot_desc);
@@ -992,7 +1014,11 @@ static int forward_simulate_impl(const fks_environment* env, const fks_solver_pa
         /* ForwardSimulateRobot SPCS:824-829 */
         RobotPtr robot(immutable_robot->Clone());
         robot->ResetPosition(start);
+        /* ForwardSimulateMutableRobot on a robot that keeps its controllers (SPCS:843-919) */
+        const size_t D = robot->NumDofs();
+        if (controller_state) robot->SetControllerState(controller_state + (size_t)idx * 2 * D);
         const std::pair<Config, bool> result = sim.ForwardSimulateMutableRobot(robot, target, allow_contacts != 0, rng, pc);
+        if (controller_state) robot->GetControllerState(controller_state + (size_t)idx * 2 * D);
         std::memcpy(out_positions + (size_t)idx * W, result.first.data(), W * sizeof(double));
         if (out_collided) out_collided[idx] = result.second ? 1 : 0;
         if (out_microsteps) out_microsteps[idx] = (uint32_t)pc.microsteps;
@@ -1037,6 +1063,8 @@ static int forward_simulate_impl(const fks_environment* env, const fks_solver_pa
         cc.resolver_iterations += pc.resolver_iterations;
         cc.sdf_bytes += pc.sdf_bytes;
         cc.least_squares_rows += pc.lsq_rows;
+        cc.self_collision_checks += pc.self_checks;
+        cc.self_corrected_points += pc.self_points;
         cc.error_particles += pc.error_flags ? 1 : 0;
     }
     if (out_stats) *out_stats = stats;
@@ -1049,10 +1077,12 @@ int oracle_forward_simulate(const fks_environment* env, const fks_solver_params*
                             const double* targets, uint64_t num_targets, uint64_t first_particle_id, int32_t allow_contacts,
                             int32_t rng_mode, int32_t num_threads, double* out_positions, uint8_t* out_collided,
                             uint32_t* out_microsteps, uint32_t* out_resolver_iterations, uint32_t* out_error_flags,
-                            fks_statistics* out_stats, fks_call_counters* out_counters) {
+                            fks_statistics* out_stats, fks_call_counters* out_counters, int32_t individual_jacobians,
+                            double* controller_state) {
     return forward_simulate_impl(env, params, frequency, seed, call_index, robot_desc, starts, n, targets, num_targets,
                                  first_particle_id, allow_contacts, rng_mode, num_threads, out_positions, out_collided,
-                                 out_microsteps, out_resolver_iterations, out_error_flags, out_stats, out_counters, nullptr);
+                                 out_microsteps, out_resolver_iterations, out_error_flags, out_stats, out_counters, nullptr,
+                                 individual_jacobians, controller_state);
 }
 
 /* ForwardSimulateRobot(..., trace, enable_tracing = true, ...) (SPCS:824-829)
@@ -1065,7 +1095,7 @@ int oracle_forward_simulate_traced(const fks_environment* env, const fks_solver_
     if (!trace || !trace->num_steps || !trace->num_configs) return 1;
     return forward_simulate_impl(env, params, frequency, seed, call_index, robot_desc, starts, n, targets, num_targets, 0,
                                  allow_contacts, 0, num_threads, out_positions, out_collided, out_microsteps,
-                                 out_resolver_iterations, out_error_flags, nullptr, nullptr, trace);
+                                 out_resolver_iterations, out_error_flags, nullptr, nullptr, trace, 0, nullptr);
 }
 
 /* CheckConfigCollision (SPCS:1398-1416) over a batch of configurations; the

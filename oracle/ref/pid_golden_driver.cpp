@@ -5,9 +5,29 @@
 // source is compiled where it lies, never copied.
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <fast_kinematic_simulator/simple_pid_controller.hpp>
 
-int main() {
+// `pid_golden --replay`: reads "kp ki kd iclamp n" then n lines "error dt" (C99 hex
+// floats) from stdin and prints one hex-float ComputeFeedbackTerm output per line, from
+// a fresh controller (Zero() state).  Used by tests/golden/make_pid_trace_golden.py to
+// run error sequences taken from a simulation trace through the reference's PID.
+static int replay() {
+    double kp, ki, kd, iclamp;
+    long n = 0;
+    while (std::scanf("%la %la %la %la %ld", &kp, &ki, &kd, &iclamp, &n) == 5) {
+        simple_pid_controller::SimplePIDController pid(kp, ki, kd, iclamp);
+        for (long i = 0; i < n; ++i) {
+            double e, dt;
+            if (std::scanf("%la %la", &e, &dt) != 2) return 1;
+            std::printf("%a\n", pid.ComputeFeedbackTerm(e, dt));
+        }
+    }
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc > 1 && std::strcmp(argv[1], "--replay") == 0) return replay();
     // cases: kp, ki, kd, iclamp (negative gains exercise Initialize()'s abs)
     const double cases[][4] = {{1.0, 0.1, 0.01, 1.0}, {10.0, 1.0, 0.1, 0.5}, {-2.0, -0.5, -0.2, -0.25}, {4.0, 0.0, 0.0, 0.0}};
     std::printf("{\n  \"source\": \"reference simple_pid_controller.hpp via oracle/ref/pid_golden_driver.cpp\",\n  \"cases\": [\n");

@@ -1,0 +1,281 @@
+/*
+ * Planner-side drop-in test: drives the HIP simulator only through
+ * std::shared_ptr<simple_simulator_interface::SimulatorInterface<...>> as the
+ * reference's planner does (FKS.hpp:18-22 factories, SPCS:446-1416 virtuals).
+ *
+ *   planner_interface_test <scene file>
+ *
+ * The scene (written by tests/test_planner_interface.py) gives the robot's constructor
+ * arguments (TnuvaLinkedRobot TNUVA:486-517, TnuvaSE2Robot 109-132, TnuvaSE3Robot
+ * 293-325), the obstacles for BuildCompleteEnvironment (SEB.cpp:470-476), the solver
+ * parameters, starts and targets.  Every number is printed as a C99 hex float so the
+ * Python side compares with the CPU oracle bit for bit.  Exit status 3 = no GPU.
+ */
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "fast_kinematic_simulator_amd/fast_kinematic_simulator.hpp"
+
+namespace upc = uncertainty_planning_core;
+using fks_planner_types::Isometry3d;
+using fks_planner_types::Vector3d;
+using fks_planner_types::Vector4d;
+
+struct Reader {
+    std::ifstream in;
+    explicit Reader(const char* path) : in(path) {
+        if (!in) throw std::runtime_error("cannot open scene file");
+    }
+    std::string word() {
+        std::string w;
+        if (!(in >> w)) throw std::runtime_error("truncated scene file");
+        return w;
+    }
+    double num() { return std::strtod(word().c_str(), nullptr); }
+    int64_t integer() { return std::strtoll(word().c_str(), nullptr, 10); }
+    void expect(const char* tag) {
+        const std::string w = word();
+        if (w != tag) throw std::runtime_error("scene file: expected " + std::string(tag) + ", got " + w);
+    }
+    Isometry3d iso() {
+        double m[12];
+        for (double& v : m) v = num();
+        return Isometry3d::FromRowMajor34(m);
+    }
+    std::vector<double> nums(size_t n) {
+        std::vector<double> v(n);
+        for (double& x : v) x = num();
+        return v;
+    }
+};
+
+static void hex(const double v) { std::printf(" %a", v); }
+
+struct Scene {
+    std::string family;
+    double frequency = 0.0;
+    uint64_t seed = 0;
+    bool allow = true;
+    fast_kinematic_simulator::SolverParameters solver;
+    std::unique_ptr<simulator_environment_builder::EnvironmentComponents> env;
+};
+
+static Scene read_common(Reader& r) {
+    Scene s;
+    r.expect("family");
+    s.family = r.word();
+    r.expect("frequency");
+    s.frequency = r.num();
+    r.expect("seed");
+    s.seed = (uint64_t)r.integer();
+    r.expect("allow");
+    s.allow = r.integer() != 0;
+    r.expect("solver");
+    s.solver.forward_simulation_time = r.num();
+    s.solver.simulation_shortcut_distance = r.num();
+    s.solver.environment_collision_check_tolerance = r.num();
+    s.solver.resolve_correction_step_scaling_decay_rate = r.num();
+    s.solver.resolve_correction_initial_step_size = r.num();
+    s.solver.resolve_correction_min_step_scaling = r.num();
+    s.solver.max_resolver_iterations = (uint32_t)r.integer();
+    s.solver.resolve_correction_step_scaling_decay_iterations = (uint32_t)r.integer();
+    s.solver.failed_resolves_end_motion = r.integer() != 0;
+    r.expect("env");
+    const double res = r.num();
+    const std::vector<double> origin = r.nums(12);
+    const int64_t cells[3] = {r.integer(), r.integer(), r.integer()};
+    const int64_t nobs = r.integer();
+    std::vector<simulator_environment_builder::OBSTACLE_CONFIG> obstacles;
+    for (int64_t k = 0; k < nobs; ++k) {
+        const Isometry3d pose = r.iso();
+        const Vector3d ext(r.num(), r.num(), r.num());
+        obstacles.emplace_back((uint32_t)r.integer(), pose, ext);
+    }
+    s.env.reset(new simulator_environment_builder::EnvironmentComponents(
+        simulator_environment_builder::BuildCompleteEnvironment(obstacles, res, origin.data(), cells)));
+    return s;
+}
+
+static simple_robot_models::PointSphereGeometry read_points(Reader& r) {
+    const int64_t n = r.integer();
+    auto pts = std::make_shared<std::vector<Vector4d>>();
+    for (int64_t i = 0; i < n; ++i) pts->push_back(Vector4d(r.num(), r.num(), r.num(), r.num()));
+    return simple_robot_models::PointSphereGeometry(simple_robot_models::PointSphereGeometry::POINTS, pts);
+}
+
+/* the interface calls every family goes through; `to_flat` prints a configuration */
+template <typename Config, typename Alloc, typename Robot>
+static int exercise(const Scene& s, const std::shared_ptr<simple_simulator_interface::SimulatorInterface<Config, upc::PRNG, Alloc>>& sim,
+                    const std::shared_ptr<Robot>& robot, const std::vector<Config, Alloc>& starts,
+                    const std::vector<Config, Alloc>& targets) {
+    typedef simple_simulator_interface::SimulatorInterface<Config, upc::PRNG, Alloc> Interface;
+    const std::shared_ptr<typename Interface::BaseRobotType> base = robot;
+    auto print = [&](const char* tag, size_t i, const typename Interface::SimulationResult& res) {
+        std::printf("%s %zu", tag, i);
+        for (double v : robot->ToFlat(res.result_config)) hex(v);
+        std::printf(" %d %d\n", res.did_contact ? 1 : 0, res.outcome_is_valid ? 1 : 0);
+    };
+    /* call index 0: ForwardSimulateRobots (SPCS:788) */
+    const auto fwd = sim->ForwardSimulateRobots(base, starts, targets, s.allow, [](const fks_planner_types::MarkerArray&) {});
+    for (size_t i = 0; i < fwd.size(); ++i) print("fwd", i, fwd[i]);
+    for (const auto& kv : sim->GetStatistics()) std::printf("stat %s %.0f\n", kv.first.c_str(), kv.second);
+    /* call index 1: ReverseSimulateRobots (SPCS:806) */
+    const auto rev = sim->ReverseSimulateRobots(base, starts, targets, s.allow, {});
+    for (size_t i = 0; i < rev.size(); ++i) print("rev", i, rev[i]);
+    /* call index 2: ForwardSimulateRobot with tracing (SPCS:824) of particle 0 */
+    typename Interface::ForwardSimulationStepTrace trace;
+    const auto tr = sim->ForwardSimulateRobot(base, starts[0], targets[0], s.allow, trace, true, {});
+    print("traced", 0, tr);
+    size_t configs = 0;
+    for (const auto& rs : trace.resolver_steps)
+        for (const auto& c : rs.contact_resolver_steps) configs += c.contact_resolution_steps.size();
+    std::printf("trace %zu %zu", trace.resolver_steps.size(), configs);
+    for (int64_t k = 0; k < trace.resolver_steps.front().control_input.size(); ++k) hex(trace.resolver_steps.front().control_input(k));
+    std::printf("\n");
+    /* CheckConfigCollision (SPCS:1398) of every reached configuration, inflation 0.5 */
+    std::printf("check");
+    for (const auto& r : fwd) std::printf(" %d", sim->CheckConfigCollision(base, r.result_config, 0.5) ? 1 : 0);
+    std::printf("\n");
+    /* call indices 3 and 4: ForwardSimulateMutableRobot (SPCS:843) twice on one robot, the
+     * second continuing the first's controllers */
+    std::shared_ptr<typename Interface::BaseRobotType> mutable_robot(base->Clone());
+    static_cast<Robot*>(mutable_robot.get())->ResetPosition(starts[0]);
+    typename Interface::ForwardSimulationStepTrace unused;
+    const auto m1 = sim->ForwardSimulateMutableRobot(mutable_robot, targets[0], s.allow, unused, false, {});
+    print("mut1", 0, m1);
+    const auto m2 = sim->ReverseSimulateMutableRobot(mutable_robot, starts[0], s.allow, unused, false, {});
+    print("mut2", 0, m2);
+    std::printf("pid");
+    for (double v : static_cast<Robot*>(mutable_robot.get())->ControllerState()) hex(v);
+    std::printf("\n");
+    /* display helpers through the interface */
+    const Vector4d p = sim->Get3dPointForConfig(base, fwd[0].result_config);
+    std::printf("point %a %a %a %a\n", p(0), p(1), p(2), p(3));
+    const auto rep = sim->MakeConfigurationDisplayRep(base, fwd[0].result_config, Interface::MakeColor(0.f, 1.f, 0.f, 1.f), 3, "cfg");
+    std::printf("markers %zu %zu %s\n", rep.markers.size(), rep.markers[0].points.size(), sim->GetFrame().c_str());
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: %s <scene>\n", argv[0]);
+        return 2;
+    }
+    try {
+        Reader r(argv[1]);
+        const Scene s = read_common(r);
+        const auto& E = *s.env;
+        if (s.family == "linked") {
+            typedef tnuva_robot_models::TnuvaLinkedRobot<upc::PRNG> Robot;
+            r.expect("base");
+            const Isometry3d base = r.iso();
+            r.expect("links");
+            std::vector<simple_linked_robot_model::RobotLink> links((size_t)r.integer());
+            for (size_t l = 0; l < links.size(); ++l) links[l].link_name = "link_" + std::to_string(l);
+            r.expect("joints");
+            const int64_t J = r.integer();
+            std::vector<simple_linked_robot_model::RobotJoint> joints;
+            upc::LinkedConfig initial;
+            for (int64_t j = 0; j < J; ++j) {
+                simple_linked_robot_model::RobotJoint jt;
+                jt.parent_link_index = r.integer();
+                jt.child_link_index = r.integer();
+                const auto type = (simple_linked_robot_model::SimpleJointModel::JOINT_TYPE)r.integer();
+                jt.joint_transform = r.iso();
+                jt.joint_axis = Vector3d(r.num(), r.num(), r.num());
+                const double lo = r.num(), hi = r.num();
+                jt.joint_model = simple_linked_robot_model::SimpleJointModel({lo, hi}, 0.0, type);
+                if (!jt.joint_model.IsFixed()) initial.push_back(jt.joint_model);
+                joints.push_back(jt);
+            }
+            r.expect("geoms");
+            const int64_t G = r.integer();
+            std::vector<std::pair<std::string, simple_robot_models::PointSphereGeometry>> geoms;
+            for (int64_t g = 0; g < G; ++g) {
+                const int64_t link = r.integer();
+                geoms.emplace_back(links[(size_t)link].link_name, read_points(r));
+            }
+            r.expect("allowed");
+            std::vector<std::pair<size_t, size_t>> allowed((size_t)r.integer());
+            for (auto& a : allowed) a = {(size_t)r.integer(), (size_t)r.integer()};
+            r.expect("controllers");
+            std::vector<Robot::LINKED_ROBOT_CONFIG> ctrl((size_t)r.integer());
+            for (auto& c : ctrl) {
+                const std::vector<double> v = r.nums(9);
+                c = Robot::LINKED_ROBOT_CONFIG(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8]);
+            }
+            r.expect("weights");
+            const std::vector<double> weights = r.nums((size_t)r.integer());
+            auto robot = std::make_shared<Robot>(base, links, joints, initial, weights, geoms, allowed, ctrl);
+            auto read_configs = [&](const char* tag) {
+                r.expect(tag);
+                const int64_t n = r.integer();
+                std::vector<upc::LinkedConfig> v;
+                for (int64_t i = 0; i < n; ++i) {
+                    const std::vector<double> f = r.nums(initial.size());
+                    v.push_back(robot->FromFlat(f.data()));
+                }
+                return v;
+            };
+            const auto starts = read_configs("starts");
+            const auto targets = read_configs("targets");
+            upc::LinkedSimulatorPtr sim = fast_kinematic_simulator::MakeLinkedSimulator(
+                E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
+            return exercise<upc::LinkedConfig, upc::LinkedConfigAlloc>(s, sim, robot, starts, targets);
+        }
+        /* SE(2) / SE(3): pos weight, rot weight, points, the 18 gains of the config */
+        const double pw = r.num(), rw = r.num();
+        const simple_robot_models::PointSphereGeometry geometry = read_points(r);
+        const std::vector<double> c = r.nums(18);
+        const tnuva_robot_models::AXIS_ROBOT_CONFIG cfg(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[11],
+                                                        c[12], c[13], c[14], c[15], c[16], c[17]);
+        if (s.family == "se2") {
+            typedef tnuva_robot_models::TnuvaSE2Robot<upc::PRNG> Robot;
+            auto robot = std::make_shared<Robot>(upc::SE2Config(0.0, 0.0, 0.0), pw, rw, "body", geometry, cfg);
+            auto read_configs = [&](const char* tag) {
+                r.expect(tag);
+                const int64_t n = r.integer();
+                std::vector<upc::SE2Config> v;
+                for (int64_t i = 0; i < n; ++i) {
+                    const std::vector<double> f = r.nums(3);
+                    v.push_back(robot->FromFlat(f.data()));
+                }
+                return v;
+            };
+            const auto starts = read_configs("starts");
+            const auto targets = read_configs("targets");
+            upc::SE2SimulatorPtr sim = fast_kinematic_simulator::MakeSE2Simulator(
+                E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
+            return exercise<upc::SE2Config, upc::SE2ConfigAlloc>(s, sim, robot, starts, targets);
+        }
+        typedef tnuva_robot_models::TnuvaSE3Robot<upc::PRNG> Robot;
+        auto robot = std::make_shared<Robot>(upc::SE3Config::Identity(), pw, rw, "body", geometry, cfg);
+        auto read_configs = [&](const char* tag) {
+            r.expect(tag);
+            const int64_t n = r.integer();
+            std::vector<upc::SE3Config> v;
+            for (int64_t i = 0; i < n; ++i) {
+                const std::vector<double> f = r.nums(12);
+                v.push_back(robot->FromFlat(f.data()));
+            }
+            return v;
+        };
+        const auto starts = read_configs("starts");
+        const auto targets = read_configs("targets");
+        upc::SE3SimulatorPtr sim = fast_kinematic_simulator::MakeSE3Simulator(
+            E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
+        return exercise<upc::SE3Config, upc::SE3ConfigAlloc>(s, sim, robot, starts, targets);
+    } catch (const fks::SimulatorError& e) {
+        std::fprintf(stderr, "%s\n", e.what());
+        return e.status() == FKS_ERR_NO_DEVICE ? 3 : 1;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "error: %s\n", e.what());
+        return 1;
+    }
+}

@@ -3,7 +3,12 @@ same inputs and compare every output field exactly."""
 import numpy as np
 
 
-def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, first_particle_id=0, sim=None):
+COUNTER_KEYS = ("microsteps", "resolver_iterations", "controller_steps", "sdf_bytes", "error_particles", "least_squares_rows",
+                "self_collision_checks", "self_corrected_points")
+
+
+def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, first_particle_id=0, sim=None,
+             individual_jacobians=False, segment_steps=None):
     import oracle
     from fast_kinematic_simulator_amd import make_linked_simulator
 
@@ -14,6 +19,10 @@ def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, f
     own = sim is None
     if own:
         sim = make_linked_simulator(env, wl.solver, wl.controller_frequency, wl.seed)
+    if individual_jacobians:
+        sim.set_individual_jacobians(True)
+    if segment_steps is not None:
+        sim.set_segment_steps(segment_steps)
     sim.set_call_index(call_index)
     g = sim.forward_simulate_arrays(wl.robot, starts, targets, allow)
     g["statistics"] = sim.get_statistics()
@@ -21,8 +30,15 @@ def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, f
     if own:
         sim.close()
     o = oracle.forward_simulate(env, wl.robot, wl.solver, wl.controller_frequency, wl.seed, starts, targets, allow,
-                                call_index=call_index, first_particle_id=first_particle_id)
+                                call_index=call_index, first_particle_id=first_particle_id,
+                                individual_jacobians=individual_jacobians)
     return g, o
+
+
+def assert_counters_identical(g, o):
+    assert g["statistics"] == o["statistics"]
+    for k in COUNTER_KEYS:
+        assert g["counters"][k] == o["counters"][k], (k, g["counters"][k], o["counters"][k])
 
 
 def mismatch_report(g, o, limit=5):

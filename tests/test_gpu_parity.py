@@ -9,7 +9,7 @@ import pytest
 
 from fast_kinematic_simulator_amd import workloads as W
 
-from parity_util import assert_identical, mismatch_report, run_both
+from parity_util import assert_counters_identical, assert_identical, mismatch_report, run_both
 
 CASES = [("cfg1", 1.0), ("cfg2", 48 / 4096), ("cfg3", 48 / 65536), ("cfg4", 64 / 1048576)]
 
@@ -30,9 +30,7 @@ def test_forward_parity(fks_lib, oracle_lib, name, scale):
     g, o = run_both(wl)
     print(name, mismatch_report(g, o))
     assert_identical(g, o)
-    assert g["statistics"] == o["statistics"]
-    for k in ("microsteps", "resolver_iterations", "controller_steps", "sdf_bytes", "error_particles", "least_squares_rows"):
-        assert g["counters"][k] == o["counters"][k], k
+    assert_counters_identical(g, o)
 
 
 @pytest.mark.gpu
@@ -76,9 +74,7 @@ def test_segmented_parity(fks_lib, oracle_lib, name, scale, segment_steps):
         sim.close()
     print(name, segment_steps, mismatch_report(g, o))
     assert_identical(g, o)
-    assert g["statistics"] == o["statistics"]
-    for k in ("microsteps", "resolver_iterations", "controller_steps", "sdf_bytes", "error_particles", "least_squares_rows"):
-        assert g["counters"][k] == o["counters"][k], k
+    assert_counters_identical(g, o)
 
 
 @pytest.mark.gpu
@@ -98,3 +94,37 @@ def test_segmented_early_stops(fks_lib, oracle_lib):
         sim.close()
     assert_identical(g, o)
     assert np.any(np.asarray(o["microsteps"]) < np.max(o["microsteps"]))  # some particles stopped early
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,scale", [("cfg1", 0.5), ("cfg3", 24 / 65536), ("cfg4", 24 / 1048576)])
+def test_mutable_robot_controller_state(fks_lib, oracle_lib, name, scale):
+    """ForwardSimulateMutableRobot (SPCS:843-919): particles start with the controllers the
+    robot holds (fks_forward_simulate_mutable) and hand back their state; both match the
+    oracle's robots carrying the same PID state, bit for bit."""
+    import oracle
+    from fast_kinematic_simulator_amd import make_linked_simulator
+
+    wl = W.WORKLOADS[name](scale)
+    n, D = len(wl.starts), wl.robot.num_dofs
+    rng = np.random.default_rng(17)
+    state0 = np.ascontiguousarray(rng.uniform(-0.2, 0.2, size=(n, 2 * D)))
+    sim = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
+    try:
+        sim.set_call_index(6)
+        gs = state0.copy()
+        g = sim.forward_simulate_mutable_arrays(wl.robot, wl.starts, wl.targets, True, gs)
+    finally:
+        sim.close()
+    os_ = state0.copy()
+    o = oracle.forward_simulate(wl.environment(), wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts, wl.targets, True,
+                                call_index=6, controller_state=os_)
+    assert_identical(g, o)
+    assert np.array_equal(gs, os_)
+    assert not np.array_equal(gs, state0)
+    # a zero state is ResetPosition: the plain batch call's results
+    z = oracle.forward_simulate(wl.environment(), wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts, wl.targets, True,
+                                call_index=6, controller_state=np.zeros((n, 2 * D)))
+    plain = oracle.forward_simulate(wl.environment(), wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts, wl.targets,
+                                    True, call_index=6)
+    assert np.array_equal(z["positions"], plain["positions"])

@@ -1,0 +1,165 @@
+"""The planner-side drop-in (include/fast_kinematic_simulator_amd/fast_kinematic_simulator.hpp)
+driven only through std::shared_ptr<SimulatorInterface<...>> made by
+fast_kinematic_simulator::Make{Linked,SE2,SE3}Simulator with the reference's parameter
+lists (FKS.hpp:18-22), against the CPU oracle on the same scene.
+
+tests/cpp/planner_interface_test.cpp reads a scene file (robot constructor arguments,
+obstacles, solver parameters, starts, targets), builds the robot with the TNUVA
+constructors and the environment with BuildCompleteEnvironment, and calls:
+  ForwardSimulateRobots (RNG call index 0), ReverseSimulateRobots (1),
+  ForwardSimulateRobot with tracing for particle 0 (2), CheckConfigCollision of every
+  reached configuration, ForwardSimulateMutableRobot (3) then ReverseSimulateMutableRobot
+  (4) on one robot that keeps its controllers, Get3dPointForConfig and
+  MakeConfigurationDisplayRep.
+Every number comes back as a hex float and is compared with the oracle bit for bit."""
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from fast_kinematic_simulator_amd import _capi
+from fast_kinematic_simulator_amd import workloads as W
+from fast_kinematic_simulator_amd.build import build_planner_test
+from fast_kinematic_simulator_amd.environment import ObstacleConfig, build_complete_environment
+from fast_kinematic_simulator_amd.robots import rotation_from_axis_angle, transform34
+
+
+def _fmt(vals):
+    return " ".join(repr(float(v)) for v in np.asarray(vals, dtype=np.float64).reshape(-1))
+
+
+def _scene(name):
+    """(family, workload, obstacles, (resolution, origin, cells))"""
+    if name == "linked":
+        wl = W.folding_arm(0.5)
+        obstacles = [ObstacleConfig(1, transform34([0.0, 0.0, -0.15]), [0.6, 0.6, 0.03]),
+                     ObstacleConfig(2, transform34([0.2, 0.0, 0.55], rotation_from_axis_angle([0, 0, 1], 0.3)), [0.05, 0.3, 0.05])]
+        return "linked", wl, obstacles, (0.01, transform34([-0.64, -0.64, -0.2]), (128, 128, 128))
+    if name == "se2":
+        wl = W.cfg1(0.5)
+        return "se2", wl, W.cfg1_obstacles(), (0.0625, transform34([0.0, 0.0, -2.0]), (64, 64, 64))
+    if name == "se3":
+        wl = W.cfg4(16 / 1048576)
+        obstacles = [o for o in W.cfg4_obstacles() if np.linalg.norm(o.pose.reshape(3, 4)[:, 3]) < 0.7]
+        return "se3", wl, obstacles, (0.01, transform34([-0.64, -0.64, -0.64]), (128, 128, 128))
+    raise KeyError(name)
+
+
+def _write_scene(path, family, wl, obstacles, grid):
+    res, origin, cells = grid
+    s = wl.solver
+    r = wl.robot
+    lines = [f"family {family}", f"frequency {wl.controller_frequency!r}", f"seed {wl.seed}", f"allow {1 if wl.allow_contacts else 0}",
+             "solver " + _fmt([s.forward_simulation_time, s.simulation_shortcut_distance, s.environment_collision_check_tolerance,
+                               s.resolve_correction_step_scaling_decay_rate, s.resolve_correction_initial_step_size,
+                               s.resolve_correction_min_step_scaling])
+             + f" {s.max_resolver_iterations} {s.resolve_correction_step_scaling_decay_iterations} {int(s.failed_resolves_end_motion)}",
+             f"env {res!r} {_fmt(origin)} {cells[0]} {cells[1]} {cells[2]} {len(obstacles)}"]
+    for o in obstacles:
+        lines.append(f"{_fmt(o.pose)} {_fmt(o.extents)} {o.object_id}")
+    ctrl = lambda c: [c.kp, c.ki, c.kd, c.integral_clamp, c.velocity_limit, c.acceleration_limit, c.max_sensor_noise,
+                      c.max_actuator_proportional_noise, c.max_actuator_minimum_noise]
+    if family == "linked":
+        lines.append(f"base {_fmt(r.base_transform)}")
+        lines.append(f"links {r.num_links}")
+        lines.append(f"joints {len(r.joints)}")
+        for j in r.joints:
+            lines.append(f"{j.parent} {j.child} {j.type} {_fmt(j.origin)} {_fmt(j.axis)} {j.lower!r} {j.upper!r}")
+        lines.append(f"geoms {len(r.geometry_points)}")
+        for link, pts in zip(r.geometry_link, r.geometry_points):
+            lines.append(f"{link} {len(pts)} {_fmt(pts)}")
+        lines.append(f"allowed {len(r.allowed_pairs)} " + " ".join(f"{a} {b}" for a, b in r.allowed_pairs))
+        lines.append(f"controllers {len(r.controllers)} " + " ".join(_fmt(ctrl(c)) for c in r.controllers))
+        lines.append(f"weights {len(r.distance_weights)} {_fmt(r.distance_weights)}")
+    else:
+        t, rot = r.controllers[0], r.controllers[-1]
+        lines.append(f"{r.distance_weights[0]!r} {r.distance_weights[1]!r}")
+        lines.append(f"{len(r.geometry_points[0])} {_fmt(r.geometry_points[0])}")
+        lines.append(_fmt(ctrl(t) + ctrl(rot)))
+    lines.append(f"starts {len(wl.starts)} {_fmt(wl.starts)}")
+    lines.append(f"targets {len(wl.targets)} {_fmt(wl.targets)}")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def _parse(out):
+    rows = {}
+    for line in out.splitlines():
+        tag, *rest = line.split()
+        rows.setdefault(tag, []).append(rest)
+    return rows
+
+
+def _hexrow(row):
+    return np.array([float.fromhex(v) for v in row])
+
+
+def _run(name):
+    family, wl, obstacles, grid = _scene(name)
+    exe = build_planner_test()
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "scene.txt")
+        _write_scene(path, family, wl, obstacles, grid)
+        p = subprocess.run([exe, path], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600)
+    return p, family, wl, obstacles, grid
+
+
+def test_planner_program_builds_and_reads_scene():
+    """g++ over the public headers only; without a GPU the factory reports FKS_ERR_NO_DEVICE
+    (exit 3) after the scene and the environment were read and built."""
+    p, *_ = _run("linked")
+    assert p.returncode in (0, 3), p.stderr
+    if p.returncode == 3:
+        assert "no HIP device" in p.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["linked", "se2", "se3"])
+def test_planner_interface_matches_oracle(fks_lib, oracle_lib, name):
+    import oracle
+
+    p, family, wl, obstacles, (res, origin, cells) = _run(name)
+    assert p.returncode == 0, p.stderr
+    rows = _parse(p.stdout)
+    env = build_complete_environment(obstacles, res, origin=origin, num_cells=cells)
+    W_ = wl.robot.config_width
+    run = lambda starts, targets, call, **kw: oracle.forward_simulate(env, wl.robot, wl.solver, wl.controller_frequency, wl.seed,
+                                                                        starts, targets, wl.allow_contacts, call_index=call, **kw)
+    # ForwardSimulateRobots / ReverseSimulateRobots: reached configurations and did_contact
+    for tag, call in (("fwd", 0), ("rev", 1)):
+        o = run(wl.starts, wl.targets, call)
+        got = np.array([_hexrow(r[1:1 + W_]) for r in rows[tag]])
+        assert np.array_equal(got, o["positions"]), (tag, np.max(np.abs(got - o["positions"])))
+        assert [int(r[1 + W_]) for r in rows[tag]] == [int(v) for v in o["collided"]]
+        assert all(r[2 + W_] == "1" for r in rows[tag])  # outcome_is_valid (SPCS:918)
+        if tag == "fwd":
+            stats = {r[0]: float(r[1]) for r in rows["stat"]}
+            assert stats == o["statistics"]
+            assert o["counters"]["resolver_iterations"] > 0  # the scene makes contact
+    # traced ForwardSimulateRobot of particle 0
+    r0, buf = oracle.forward_simulate_traced(env, wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts[:1],
+                                             wl.targets[:1], wl.allow_contacts, call_index=2)
+    assert np.array_equal(_hexrow(rows["traced"][0][1:1 + W_]), r0["positions"][0])
+    tr = buf.particle(0)
+    nconf = sum(len(c.contact_resolution_steps) for rs in tr.resolver_steps for c in rs.contact_resolver_steps)
+    t = rows["trace"][0]
+    assert (int(t[0]), int(t[1])) == (len(tr.resolver_steps), nconf)
+    assert np.array_equal(_hexrow(t[2:]), tr.resolver_steps[0].control_input)
+    # CheckConfigCollision of the reached configurations
+    fwd = run(wl.starts, wl.targets, 0)
+    c = oracle.check_config_collision(env, wl.robot, wl.solver, fwd["positions"], 0.5)
+    assert [int(v) for v in rows["check"][0]] == [int(v) for v in c["collided"]]
+    # mutable robot: the second call continues the first call's controllers
+    D = wl.robot.num_dofs
+    state = np.zeros((1, 2 * D))
+    m1 = run(wl.starts[:1], wl.targets[:1], 3, controller_state=state)
+    assert np.array_equal(_hexrow(rows["mut1"][0][1:1 + W_]), m1["positions"][0])
+    m2 = run(m1["positions"], wl.starts[:1], 4, controller_state=state)
+    assert np.array_equal(_hexrow(rows["mut2"][0][1:1 + W_]), m2["positions"][0])
+    assert np.array_equal(_hexrow(rows["pid"][0]), state[0])
+    assert np.any(state != 0.0)
+    # display helpers
+    mk = rows["markers"][0]
+    assert int(mk[0]) == 1 and int(mk[1]) == wl.robot.num_points and mk[2] == "world"
