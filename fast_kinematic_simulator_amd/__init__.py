@@ -9,12 +9,12 @@ from .environment import (DeviceEnvironment, ObstacleConfig, SimulatorEnvironmen
                           build_device_environment)
 from .robots import (ControllerConfig, Joint, RobotDescription, SampledActuatorModel, make_linked_robot,
                      make_sampled_actuator_model, make_se2_robot, make_se3_robot, se3_pose, transform34)
-from .simulator import (HipParticleContactSimulator, SimulationResult, SimulatorSolverParameters, get_default_solver_parameters,
-                        make_linked_simulator, make_se2_simulator, make_se3_simulator)
+from .simulator import (HipParticleContactSimulator, MultiDeviceSimulator, SimulationResult, SimulatorSolverParameters,
+                        get_default_solver_parameters, make_linked_simulator, make_se2_simulator, make_se3_simulator)
 
 __all__ = [
     "FksError", "lib", "ObstacleConfig", "SimulatorEnvironment", "build_complete_environment", "ControllerConfig", "Joint",
     "RobotDescription", "make_linked_robot", "make_se2_robot", "make_se3_robot", "se3_pose", "transform34",
-    "HipParticleContactSimulator", "SimulationResult", "SimulatorSolverParameters", "get_default_solver_parameters",
+    "HipParticleContactSimulator", "MultiDeviceSimulator", "SimulationResult", "SimulatorSolverParameters", "get_default_solver_parameters",
     "make_linked_simulator", "make_se2_simulator", "make_se3_simulator",
 ]

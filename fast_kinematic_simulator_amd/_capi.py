@@ -278,6 +278,24 @@ PROTOTYPES = [
     ("fks_env_occupancy", c_int32, [c_void_p, POINTER(c_uint8), c_uint64]),
     ("fks_env_free", None, [c_void_p]),
     ("fks_selftest_math", c_int32, [c_int32, c_uint64, POINTER(c_uint64)]),
+    ("fks_shard_bounds", c_int32, [c_uint64, c_int32, c_int32, POINTER(c_uint64), POINTER(c_uint64)]),
+    ("fks_create_multi", c_int32, [POINTER(Environment), POINTER(SolverParams), c_double, c_uint64, c_int32, POINTER(c_int32), c_int32,
+                                   POINTER(c_void_p)]),
+    ("fks_destroy_multi", None, [c_void_p]),
+    ("fks_multi_get_last_error", c_char_p, [c_void_p]),
+    ("fks_multi_num_devices", c_int32, [c_void_p]),
+    ("fks_multi_device_context", c_void_p, [c_void_p, c_int32]),
+    ("fks_multi_set_robot", c_int32, [c_void_p, POINTER(RobotDesc)]),
+    (
+        "fks_multi_forward_simulate",
+        c_int32,
+        [c_void_p, POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_int32, POINTER(c_double), POINTER(c_uint8),
+         POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)],
+    ),
+    ("fks_multi_get_statistics", c_int32, [c_void_p, POINTER(Statistics)]),
+    ("fks_multi_reset_statistics", c_int32, [c_void_p]),
+    ("fks_multi_get_last_call_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
+    ("fks_multi_set_call_index", c_int32, [c_void_p, c_uint64]),
 ]
 
 _LIB = None

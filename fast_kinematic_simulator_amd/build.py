@@ -12,7 +12,7 @@ import subprocess
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-SOURCES = ["csrc/fks_kernels.hip", "csrc/fks_capi.cpp", "csrc/fks_env_builder.cpp", "csrc/fks_env_gpu.hip"]
+SOURCES = ["csrc/fks_kernels.hip", "csrc/fks_capi.cpp", "csrc/fks_multi.cpp", "csrc/fks_env_builder.cpp", "csrc/fks_env_gpu.hip"]
 HEADERS = ["csrc/fks_device.h", "csrc/fks_env_internal.h", "../include/fks_capi.h", "../include/fks_portable_math.h"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 

@@ -1,0 +1,269 @@
+/*
+ * fks_multi.cpp — one process driving several MI355X devices through the C-ABI
+ * (fks_create_multi and friends, include/fks_capi.h).
+ *
+ * Replaces the reference's `#pragma omp parallel for` over particles (SPCS:795)
+ * at device granularity: particle i of a call belongs to the device whose contiguous,
+ * balanced range holds it (fks_shard_bounds), and that device
+ * simulates it with first_particle_id = the range start, so the counter RNG stream of
+ * every particle is the one a single device would use and the results are
+ * bit-identical for any device count.  All devices share one call
+ * index per logical call.  Each device gets its inputs by its own H2D copy, runs on
+ * its own stream, and copies its outcomes straight into the caller's buffers at its
+ * offset — the gather of per-particle outcomes is per-device D2H into host memory,
+ * which is where the planner consumes them; the statistics and call counters are
+ * summed over the devices (kernel_ms is the slowest device's).  Device-resident
+ * multi-process use (one rank per GPU, RCCL gather) is bench.py / sharding.py.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "fks_capi.h"
+
+struct fks_multi_context {
+    struct Device {
+        int32_t device = 0;
+        fks_context* ctx = nullptr;
+        hipStream_t stream = nullptr;
+        double* d_starts = nullptr;
+        double* d_targets = nullptr;
+        double* d_out = nullptr;
+        uint8_t* d_coll = nullptr;
+        uint32_t* d_micro = nullptr;
+        uint32_t* d_res = nullptr;
+        uint32_t* d_err = nullptr;
+        size_t cap = 0, cap_targets = 0;
+    };
+    std::vector<Device> devices;
+    std::string last_error;
+    uint64_t call_index = 0;
+    int32_t width = 0;
+    fks_call_counters last{};
+};
+
+namespace {
+
+fks_status mfail(fks_multi_context* m, fks_status st, const std::string& msg) {
+    if (m) m->last_error = msg;
+    return st;
+}
+fks_status mhip(fks_multi_context* m, hipError_t e, const char* where) {
+    return mfail(m, FKS_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+fks_status mctx(fks_multi_context* m, fks_status st, const fks_context* ctx, const char* where) {
+    return mfail(m, st, std::string(where) + ": " + fks_status_string(st) + " (" + fks_get_last_error(ctx) + ")");
+}
+#define MHIP(m, expr)                                       \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return mhip((m), _e, #expr);  \
+    } while (0)
+
+template <typename T>
+hipError_t grow(T** p, size_t count) {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    return hipMalloc((void**)p, (count > 0 ? count : 1) * sizeof(T));
+}
+
+void free_device(fks_multi_context::Device& d) {
+    (void)hipSetDevice(d.device);
+    void* ptrs[] = {d.d_starts, d.d_targets, d.d_out, d.d_coll, d.d_micro, d.d_res, d.d_err};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+    if (d.ctx) fks_destroy(d.ctx);
+    d = fks_multi_context::Device();
+}
+
+}  // namespace
+
+extern "C" {
+
+fks_status fks_shard_bounds(uint64_t n, int32_t ndev, int32_t shard, uint64_t* begin, uint64_t* end) {
+    if (ndev < 1 || shard < 0 || shard >= ndev || !begin || !end) return FKS_ERR_INVALID_ARGUMENT;
+    /* balanced contiguous ranges, the first n % ndev shards one particle longer
+     * (fast_kinematic_simulator_amd/sharding.py shard_bounds is the same rule) */
+    const uint64_t base = n / (uint64_t)ndev, extra = n % (uint64_t)ndev, g = (uint64_t)shard;
+    *begin = g * base + (g < extra ? g : extra);
+    *end = *begin + base + (g < extra ? 1u : 0u);
+    return FKS_OK;
+}
+
+fks_status fks_create_multi(const fks_environment* env, const fks_solver_params* params, double simulation_controller_frequency,
+                            uint64_t prng_seed, int32_t debug_level, const int32_t* devices, int32_t ndev,
+                            fks_multi_context** out) {
+    if (!out) return FKS_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (!env || !params || !devices || ndev < 1 || ndev > 64) return FKS_ERR_INVALID_ARGUMENT;
+    fks_multi_context* m = new (std::nothrow) fks_multi_context();
+    if (!m) return FKS_ERR_OUT_OF_MEMORY;
+    for (int32_t g = 0; g < ndev; ++g) {
+        fks_multi_context::Device d;
+        d.device = devices[g];
+        fks_status st = fks_create(env, params, simulation_controller_frequency, prng_seed, debug_level, d.device, &d.ctx);
+        if (st == FKS_OK && hipSetDevice(d.device) != hipSuccess) st = FKS_ERR_HIP;
+        if (st == FKS_OK && hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess) st = FKS_ERR_HIP;
+        m->devices.push_back(d);
+        if (st != FKS_OK) {
+            fks_destroy_multi(m);
+            return st;
+        }
+    }
+    *out = m;
+    return FKS_OK;
+}
+
+void fks_destroy_multi(fks_multi_context* m) {
+    if (!m) return;
+    for (auto& d : m->devices) free_device(d);
+    delete m;
+}
+
+const char* fks_multi_get_last_error(const fks_multi_context* m) { return m ? m->last_error.c_str() : "null context"; }
+
+int32_t fks_multi_num_devices(const fks_multi_context* m) { return m ? (int32_t)m->devices.size() : 0; }
+
+fks_context* fks_multi_device_context(fks_multi_context* m, int32_t shard) {
+    if (!m || shard < 0 || shard >= (int32_t)m->devices.size()) return nullptr;
+    return m->devices[(size_t)shard].ctx;
+}
+
+fks_status fks_multi_set_robot(fks_multi_context* m, const fks_robot_desc* robot) {
+    if (!m) return FKS_ERR_INVALID_ARGUMENT;
+    for (auto& d : m->devices) {
+        const fks_status st = fks_set_robot(d.ctx, robot);
+        if (st != FKS_OK) return mctx(m, st, d.ctx, "fks_set_robot");
+    }
+    m->width = fks_config_width(m->devices[0].ctx);
+    return FKS_OK;
+}
+
+fks_status fks_multi_forward_simulate(fks_multi_context* m, const double* starts, uint64_t n, const double* targets,
+                                      uint64_t num_targets, int32_t allow_contacts, double* out_positions, uint8_t* out_collided,
+                                      uint32_t* out_microsteps, uint32_t* out_resolver_iterations, uint32_t* out_error_flags) {
+    if (!m) return FKS_ERR_INVALID_ARGUMENT;
+    if (m->width <= 0) return mfail(m, FKS_ERR_NO_ROBOT, "fks_multi_set_robot has not been called");
+    if (n > 0 && (!starts || !targets || !out_positions)) return mfail(m, FKS_ERR_INVALID_ARGUMENT, "null host buffer");
+    if (n > 0 && num_targets != 1 && num_targets != n) return mfail(m, FKS_ERR_INVALID_ARGUMENT, "targets must be 1 or n (SPCS:792)");
+    const auto t0 = std::chrono::steady_clock::now();
+    const size_t W = (size_t)m->width;
+    const int32_t ndev = (int32_t)m->devices.size();
+    const uint64_t call = m->call_index++;
+    /* enqueue every shard, then collect: the devices run concurrently */
+    for (int32_t g = 0; g < ndev; ++g) {
+        auto& d = m->devices[(size_t)g];
+        uint64_t lo = 0, hi = 0;
+        fks_shard_bounds(n, ndev, g, &lo, &hi);
+        const uint64_t k = hi - lo;
+        fks_status st = fks_set_call_index(d.ctx, call);
+        if (st != FKS_OK) return mctx(m, st, d.ctx, "fks_set_call_index");
+        MHIP(m, hipSetDevice(d.device));
+        if (k > d.cap) {
+            MHIP(m, grow(&d.d_starts, k * W));
+            MHIP(m, grow(&d.d_out, k * W));
+            MHIP(m, grow(&d.d_coll, k));
+            MHIP(m, grow(&d.d_micro, k));
+            MHIP(m, grow(&d.d_res, k));
+            MHIP(m, grow(&d.d_err, k));
+            d.cap = k;
+        }
+        const uint64_t nt = (num_targets == n) ? k : 1;
+        if (nt > d.cap_targets) {
+            MHIP(m, grow(&d.d_targets, nt * W));
+            d.cap_targets = nt;
+        }
+        if (k == 0) continue;
+        MHIP(m, hipMemcpyAsync(d.d_starts, starts + lo * W, k * W * sizeof(double), hipMemcpyHostToDevice, d.stream));
+        MHIP(m, hipMemcpyAsync(d.d_targets, targets + (num_targets == n ? lo * W : 0), nt * W * sizeof(double),
+                               hipMemcpyHostToDevice, d.stream));
+        st = fks_forward_simulate_device(d.ctx, d.d_starts, k, d.d_targets, nt, lo, allow_contacts, d.d_out, d.d_coll, d.d_micro,
+                                         d.d_res, d.d_err, d.stream, 0);
+        if (st != FKS_OK) return mctx(m, st, d.ctx, "fks_forward_simulate_device");
+    }
+    std::memset(&m->last, 0, sizeof(m->last));
+    for (int32_t g = 0; g < ndev; ++g) {
+        auto& d = m->devices[(size_t)g];
+        uint64_t lo = 0, hi = 0;
+        fks_shard_bounds(n, ndev, g, &lo, &hi);
+        const uint64_t k = hi - lo;
+        MHIP(m, hipSetDevice(d.device));
+        if (k > 0) {
+            MHIP(m, hipMemcpyAsync(out_positions + lo * W, d.d_out, k * W * sizeof(double), hipMemcpyDeviceToHost, d.stream));
+            if (out_collided) MHIP(m, hipMemcpyAsync(out_collided + lo, d.d_coll, k, hipMemcpyDeviceToHost, d.stream));
+            if (out_microsteps)
+                MHIP(m, hipMemcpyAsync(out_microsteps + lo, d.d_micro, k * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
+            if (out_resolver_iterations)
+                MHIP(m, hipMemcpyAsync(out_resolver_iterations + lo, d.d_res, k * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
+            if (out_error_flags)
+                MHIP(m, hipMemcpyAsync(out_error_flags + lo, d.d_err, k * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
+            MHIP(m, hipStreamSynchronize(d.stream));
+        }
+        fks_call_counters c;
+        const fks_status st = fks_get_last_call_counters(d.ctx, &c); /* settles the device's launch */
+        if (st != FKS_OK) return mctx(m, st, d.ctx, "fks_get_last_call_counters");
+        if (k == 0) continue;
+        m->last.particles += c.particles;
+        m->last.controller_steps += c.controller_steps;
+        m->last.microsteps += c.microsteps;
+        m->last.resolver_iterations += c.resolver_iterations;
+        m->last.sdf_bytes += c.sdf_bytes;
+        m->last.error_particles += c.error_particles;
+        m->last.least_squares_rows += c.least_squares_rows;
+        m->last.self_collision_checks += c.self_collision_checks;
+        m->last.self_corrected_points += c.self_corrected_points;
+        m->last.kernel_ms = std::max(m->last.kernel_ms, c.kernel_ms);
+    }
+    m->last.calls = 1;
+    m->last.call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return FKS_OK;
+}
+
+fks_status fks_multi_get_statistics(const fks_multi_context* m, fks_statistics* out) {
+    if (!m || !out) return FKS_ERR_INVALID_ARGUMENT;
+    std::memset(out, 0, sizeof(*out));
+    for (const auto& d : m->devices) {
+        fks_statistics s;
+        const fks_status st = fks_get_statistics(d.ctx, &s);
+        if (st != FKS_OK) return st;
+        out->successful_resolves += s.successful_resolves;
+        out->unsuccessful_resolves += s.unsuccessful_resolves;
+        out->free_resolves += s.free_resolves;
+        out->collision_resolves += s.collision_resolves;
+        out->fallback_resolves += s.fallback_resolves;
+        out->unsuccessful_env_collision_resolves += s.unsuccessful_env_collision_resolves;
+        out->unsuccessful_self_collision_resolves += s.unsuccessful_self_collision_resolves;
+        out->recovered_unsuccessful_resolves += s.recovered_unsuccessful_resolves;
+    }
+    return FKS_OK;
+}
+
+fks_status fks_multi_reset_statistics(fks_multi_context* m) {
+    if (!m) return FKS_ERR_INVALID_ARGUMENT;
+    for (auto& d : m->devices) {
+        const fks_status st = fks_reset_statistics(d.ctx);
+        if (st != FKS_OK) return mctx(m, st, d.ctx, "fks_reset_statistics");
+    }
+    return FKS_OK;
+}
+
+fks_status fks_multi_get_last_call_counters(const fks_multi_context* m, fks_call_counters* out) {
+    if (!m || !out) return FKS_ERR_INVALID_ARGUMENT;
+    *out = m->last;
+    return FKS_OK;
+}
+
+fks_status fks_multi_set_call_index(fks_multi_context* m, uint64_t call_index) {
+    if (!m) return FKS_ERR_INVALID_ARGUMENT;
+    m->call_index = call_index;
+    return FKS_OK;
+}
+
+}  // extern "C"

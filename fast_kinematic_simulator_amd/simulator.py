@@ -451,6 +451,86 @@ class HipParticleContactSimulator:
         _capi.check(st, self._ctx, "fks_forward_simulate_device")
 
 
+class MultiDeviceSimulator:
+    """One process, several MI355X devices (fks_create_multi): every batch is split into
+    contiguous particle shards, one per listed device, simulated concurrently with each
+    shard's first_particle_id, and gathered into one result (bit-identical to one device).
+    Statistics are summed over the devices.  Replaces the reference's OpenMP particle loop
+    (SPCS:795) at device granularity; one process per GPU under torch.distributed is the
+    other route (sharding.py, bench.py)."""
+
+    def __init__(self, environment: SimulatorEnvironment, solver_config: SimulatorSolverParameters,
+                 simulation_controller_frequency: float, prng_seed: int, devices: Sequence[int], debug_level: int = 0):
+        self._lib = _capi.lib()
+        env_c, self._env_keep = environment.to_c()
+        params = solver_config.to_c()
+        devs = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
+        ctx = ctypes.c_void_p()
+        st = self._lib.fks_create_multi(ctypes.byref(env_c), ctypes.byref(params), float(simulation_controller_frequency),
+                                        ctypes.c_uint64(int(prng_seed) & 0xFFFFFFFFFFFFFFFF), int(debug_level), devs, len(devices),
+                                        ctypes.byref(ctx))
+        _capi.check(st, None, "fks_create_multi")
+        self._ctx = ctx
+        self._robot = None
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.fks_destroy_multi(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st, what):
+        if st != _capi.FKS_OK:
+            raise _capi.FksError(st, f"{what}: {self._lib.fks_multi_get_last_error(self._ctx).decode()}")
+
+    def num_devices(self) -> int:
+        return int(self._lib.fks_multi_num_devices(self._ctx))
+
+    def set_robot(self, robot: RobotDescription):
+        if self._robot is robot:
+            return
+        desc, keep = robot.to_c()
+        self._check(self._lib.fks_multi_set_robot(self._ctx, ctypes.byref(desc)), "fks_multi_set_robot")
+        self._robot = robot
+
+    def set_call_index(self, call_index: int):
+        self._check(self._lib.fks_multi_set_call_index(self._ctx, ctypes.c_uint64(int(call_index))), "call index")
+
+    def forward_simulate_arrays(self, robot: RobotDescription, start_positions, target_positions, allow_contacts: bool) -> dict:
+        self.set_robot(robot)
+        W = robot.config_width
+        starts = np.ascontiguousarray(np.asarray(start_positions, dtype=np.float64).reshape(-1, W))
+        targets = np.ascontiguousarray(np.asarray(target_positions, dtype=np.float64).reshape(-1, W))
+        n = starts.shape[0]
+        out = np.zeros((n, W), dtype=np.float64)
+        collided = np.zeros(n, dtype=np.uint8)
+        micro = np.zeros(n, dtype=np.uint32)
+        resolver = np.zeros(n, dtype=np.uint32)
+        errors = np.zeros(n, dtype=np.uint32)
+        st = self._lib.fks_multi_forward_simulate(
+            self._ctx, _capi.as_ptr(starts, ctypes.c_double), n, _capi.as_ptr(targets, ctypes.c_double), targets.shape[0],
+            1 if allow_contacts else 0, _capi.as_ptr(out, ctypes.c_double), _capi.as_ptr(collided, ctypes.c_uint8),
+            _capi.as_ptr(micro, ctypes.c_uint32), _capi.as_ptr(resolver, ctypes.c_uint32), _capi.as_ptr(errors, ctypes.c_uint32))
+        self._check(st, "fks_multi_forward_simulate")
+        return {"positions": out, "collided": collided.astype(bool), "microsteps": micro, "resolver_iterations": resolver,
+                "error_flags": errors}
+
+    def get_statistics(self) -> dict:
+        s = _capi.Statistics()
+        self._check(self._lib.fks_multi_get_statistics(self._ctx, ctypes.byref(s)), "statistics")
+        return s.as_dict()
+
+    def last_call_counters(self) -> dict:
+        c = _capi.CallCounters()
+        self._check(self._lib.fks_multi_get_last_call_counters(self._ctx, ctypes.byref(c)), "counters")
+        return c.as_dict()
+
+
 def _marker(ns, marker_id, marker_type, frame, scale, color):
     """A visualization_msgs::Marker as a plain dict (ROS is not part of this repository)."""
     return {"ns": ns, "id": int(marker_id), "type": marker_type, "action": "ADD", "frame_id": frame,

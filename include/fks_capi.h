@@ -492,6 +492,37 @@ fks_status fks_env_view(const fks_env_handle* env, fks_environment* out);
 fks_status fks_env_occupancy(const fks_env_handle* env, uint8_t* out, uint64_t num_cells);
 void fks_env_free(fks_env_handle* env);
 
+/* ---- several devices in one process (fks_multi.cpp) ----
+ * The reference runs one simulator object over all host cores (`#pragma omp parallel for`
+ * over particles, SPCS:795); a multi context runs one fks_context per listed device and
+ * splits every batch into contiguous shards, particle i on the device whose
+ * fks_shard_bounds range holds it, simulated with first_particle_id = the range start
+ * (bit-identical results for any device list).  Inputs go to each device by its own H2D
+ * copy, the devices run concurrently on their own streams, and each copies its outcomes
+ * into the caller's buffers at its offset; statistics and call counters are summed over
+ * the devices (kernel_ms: the slowest).  The same device may be listed more than once. */
+typedef struct fks_multi_context fks_multi_context;
+/* [begin, end) of shard `shard` of n particles over ndev devices: balanced contiguous ranges,
+ * the first n % ndev shards one particle longer */
+fks_status fks_shard_bounds(uint64_t n, int32_t ndev, int32_t shard, uint64_t* begin, uint64_t* end);
+fks_status fks_create_multi(const fks_environment* env, const fks_solver_params* params, double simulation_controller_frequency,
+                            uint64_t prng_seed, int32_t debug_level, const int32_t* devices, int32_t ndev,
+                            fks_multi_context** out);
+void fks_destroy_multi(fks_multi_context* m);
+const char* fks_multi_get_last_error(const fks_multi_context* m);
+int32_t fks_multi_num_devices(const fks_multi_context* m);
+/* the per-device context of shard `shard` (for per-device settings such as fks_set_segment_steps) */
+fks_context* fks_multi_device_context(fks_multi_context* m, int32_t shard);
+fks_status fks_multi_set_robot(fks_multi_context* m, const fks_robot_desc* robot);
+/* ForwardSimulateRobots (SPCS:788-804) over all devices; arguments as fks_forward_simulate */
+fks_status fks_multi_forward_simulate(fks_multi_context* m, const double* starts, uint64_t n, const double* targets,
+                                      uint64_t num_targets, int32_t allow_contacts, double* out_positions, uint8_t* out_collided,
+                                      uint32_t* out_microsteps, uint32_t* out_resolver_iterations, uint32_t* out_error_flags);
+fks_status fks_multi_get_statistics(const fks_multi_context* m, fks_statistics* out);
+fks_status fks_multi_reset_statistics(fks_multi_context* m);
+fks_status fks_multi_get_last_call_counters(const fks_multi_context* m, fks_call_counters* out);
+fks_status fks_multi_set_call_index(fks_multi_context* m, uint64_t call_index);
+
 /* Device self-test of the portable libm against the host (bit equality). */
 fks_status fks_selftest_math(int32_t device, uint64_t n, uint64_t* out_mismatches);
 

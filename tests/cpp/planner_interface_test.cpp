@@ -48,6 +48,15 @@ struct Reader {
         for (double& v : m) v = num();
         return Isometry3d::FromRowMajor34(m);
     }
+    /* one value per call, in file order (function-argument evaluation order is unspecified) */
+    Vector3d vec3() {
+        const std::vector<double> v = nums(3);
+        return Vector3d(v[0], v[1], v[2]);
+    }
+    Vector4d vec4() {
+        const std::vector<double> v = nums(4);
+        return Vector4d(v[0], v[1], v[2], v[3]);
+    }
     std::vector<double> nums(size_t n) {
         std::vector<double> v(n);
         for (double& x : v) x = num();
@@ -94,7 +103,7 @@ static Scene read_common(Reader& r) {
     std::vector<simulator_environment_builder::OBSTACLE_CONFIG> obstacles;
     for (int64_t k = 0; k < nobs; ++k) {
         const Isometry3d pose = r.iso();
-        const Vector3d ext(r.num(), r.num(), r.num());
+        const Vector3d ext = r.vec3();
         obstacles.emplace_back((uint32_t)r.integer(), pose, ext);
     }
     s.env.reset(new simulator_environment_builder::EnvironmentComponents(
@@ -105,8 +114,48 @@ static Scene read_common(Reader& r) {
 static simple_robot_models::PointSphereGeometry read_points(Reader& r) {
     const int64_t n = r.integer();
     auto pts = std::make_shared<std::vector<Vector4d>>();
-    for (int64_t i = 0; i < n; ++i) pts->push_back(Vector4d(r.num(), r.num(), r.num(), r.num()));
+    for (int64_t i = 0; i < n; ++i) pts->push_back(r.vec4());
     return simple_robot_models::PointSphereGeometry(simple_robot_models::PointSphereGeometry::POINTS, pts);
+}
+
+/* --dump: the flattened robot the GPU receives and the flat starts / targets (no GPU needed) */
+static bool g_dump = false;
+template <typename Config, typename Robot>
+static int dump(const Robot& robot, const std::vector<Config>& starts, const std::vector<Config>& targets) {
+    const fks::RobotDescription& d = robot.HipDescription();
+    std::printf("type %d links %d dofs %d\nbase", (int)d.type, d.num_links, d.num_dofs);
+    for (double v : d.base_transform) hex(v);
+    std::printf("\njoints");
+    for (const auto& j : d.joints) {
+        std::printf(" %d %d %d", j.parent_link, j.child_link, j.type);
+        for (double v : j.origin) hex(v);
+        for (double v : j.axis) hex(v);
+        hex(j.limit_lower);
+        hex(j.limit_upper);
+    }
+    std::printf("\ngeometry_link");
+    for (int32_t v : d.geometry_link) std::printf(" %d", v);
+    std::printf("\noffsets");
+    for (uint32_t v : d.geometry_point_offset) std::printf(" %u", v);
+    std::printf("\npoints");
+    for (double v : d.points) hex(v);
+    std::printf("\nallowed");
+    for (int32_t v : d.allowed_pairs) std::printf(" %d", v);
+    std::printf("\ncontrollers");
+    for (const auto& c : d.controllers)
+        for (double v : {c.kp, c.ki, c.kd, c.integral_clamp, c.velocity_limit, c.acceleration_limit, c.max_sensor_noise,
+                         c.max_actuator_proportional_noise, c.max_actuator_minimum_noise})
+            hex(v);
+    std::printf("\nweights");
+    for (double v : d.distance_weights) hex(v);
+    std::printf("\nstarts");
+    for (const auto& c : starts)
+        for (double v : robot.ToFlat(c)) hex(v);
+    std::printf("\ntargets");
+    for (const auto& c : targets)
+        for (double v : robot.ToFlat(c)) hex(v);
+    std::printf("\n");
+    return 0;
 }
 
 /* the interface calls every family goes through; `to_flat` prints a configuration */
@@ -164,9 +213,10 @@ static int exercise(const Scene& s, const std::shared_ptr<simple_simulator_inter
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s <scene>\n", argv[0]);
+        std::fprintf(stderr, "usage: %s <scene> [--dump]\n", argv[0]);
         return 2;
     }
+    g_dump = argc > 2 && std::string(argv[2]) == "--dump";
     try {
         Reader r(argv[1]);
         const Scene s = read_common(r);
@@ -188,7 +238,7 @@ int main(int argc, char** argv) {
                 jt.child_link_index = r.integer();
                 const auto type = (simple_linked_robot_model::SimpleJointModel::JOINT_TYPE)r.integer();
                 jt.joint_transform = r.iso();
-                jt.joint_axis = Vector3d(r.num(), r.num(), r.num());
+                jt.joint_axis = r.vec3();
                 const double lo = r.num(), hi = r.num();
                 jt.joint_model = simple_linked_robot_model::SimpleJointModel({lo, hi}, 0.0, type);
                 if (!jt.joint_model.IsFixed()) initial.push_back(jt.joint_model);
@@ -225,6 +275,7 @@ int main(int argc, char** argv) {
             };
             const auto starts = read_configs("starts");
             const auto targets = read_configs("targets");
+            if (g_dump) return dump(*robot, starts, targets);
             upc::LinkedSimulatorPtr sim = fast_kinematic_simulator::MakeLinkedSimulator(
                 E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
             return exercise<upc::LinkedConfig, upc::LinkedConfigAlloc>(s, sim, robot, starts, targets);
@@ -250,6 +301,7 @@ int main(int argc, char** argv) {
             };
             const auto starts = read_configs("starts");
             const auto targets = read_configs("targets");
+            if (g_dump) return dump(*robot, starts, targets);
             upc::SE2SimulatorPtr sim = fast_kinematic_simulator::MakeSE2Simulator(
                 E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
             return exercise<upc::SE2Config, upc::SE2ConfigAlloc>(s, sim, robot, starts, targets);
@@ -268,6 +320,7 @@ int main(int argc, char** argv) {
         };
         const auto starts = read_configs("starts");
         const auto targets = read_configs("targets");
+        if (g_dump) return dump(*robot, starts, targets);
         upc::SE3SimulatorPtr sim = fast_kinematic_simulator::MakeSE3Simulator(
             E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
         return exercise<upc::SE3Config, upc::SE3ConfigAlloc>(s, sim, robot, starts, targets);

@@ -106,6 +106,42 @@ def _run(name):
     return p, family, wl, obstacles, grid
 
 
+@pytest.mark.parametrize("name", ["linked", "se2", "se3"])
+def test_planner_robot_flattens_like_python(name):
+    """The TNUVA constructors of the C++ drop-in flatten the robot exactly as the Python
+    mirror does (the description the GPU receives), and configurations convert losslessly."""
+    family, wl, obstacles, grid = _scene(name)
+    exe = build_planner_test()
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "scene.txt")
+        _write_scene(path, family, wl, obstacles, grid)
+        p = subprocess.run([exe, path, "--dump"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    rows = {line.split()[0]: line.split()[1:] for line in p.stdout.splitlines()}
+    r = wl.robot
+    hx = lambda key: _hexrow(rows[key]) if rows[key] else np.zeros(0)
+    assert int(rows["type"][0]) == r.robot_type and int(rows["type"][-1]) == r.num_dofs
+    assert np.array_equal(hx("points"), r.points.reshape(-1))
+    assert np.array_equal(hx("starts"), wl.starts.reshape(-1)) and np.array_equal(hx("targets"), wl.targets.reshape(-1))
+    assert [int(v) for v in rows["geometry_link"]] == list(r.geometry_link)
+    ctrl = np.array([[c.kp, c.ki, c.kd, c.integral_clamp, c.velocity_limit, c.acceleration_limit, c.max_sensor_noise,
+                      c.max_actuator_proportional_noise, c.max_actuator_minimum_noise] for c in r.controllers])
+    assert np.array_equal(hx("controllers"), ctrl.reshape(-1))
+    assert np.array_equal(hx("weights"), np.asarray(r.distance_weights, dtype=np.float64))
+    if family == "linked":
+        assert np.array_equal(hx("base"), np.asarray(r.base_transform, dtype=np.float64).reshape(-1))
+        assert [int(v) for v in rows["allowed"]] == [int(v) for pair in r.allowed_pairs for v in pair]
+        j = rows["joints"]
+        per = 3 + 12 + 3 + 2
+        assert len(j) == per * len(r.joints)
+        for k, jt in enumerate(r.joints):
+            f = j[per * k:per * (k + 1)]
+            assert [int(v) for v in f[:3]] == [jt.parent, jt.child, jt.type]
+            assert np.array_equal(_hexrow(f[3:15]), np.asarray(jt.origin, dtype=np.float64).reshape(-1))
+            assert np.array_equal(_hexrow(f[15:18]), np.asarray(jt.axis, dtype=np.float64))
+            assert np.array_equal(_hexrow(f[18:20]), np.array([jt.lower, jt.upper]))
+
+
 def test_planner_program_builds_and_reads_scene():
     """g++ over the public headers only; without a GPU the factory reports FKS_ERR_NO_DEVICE
     (exit 3) after the scene and the environment were read and built."""

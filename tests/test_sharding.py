@@ -55,3 +55,55 @@ def test_gloo_world2_gather_matches_single_run(oracle_lib, tmp_path):
     v = json.loads(out.read_text())
     assert v["rows"] == 13 and v["identical"], v
     assert v["collided"] > 0
+
+
+def test_c_shard_bounds_match_python(fks_lib):
+    """fks_shard_bounds (the multi-device context's split) is sharding.shard_bounds."""
+    import ctypes
+
+    from fast_kinematic_simulator_amd.sharding import shard_bounds
+
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    for n in (0, 1, 7, 64, 65536, 1048577, 2 ** 40 + 3):
+        for world in (1, 2, 3, 8, 13):
+            prev = 0
+            for r in range(world):
+                assert fks_lib.fks_shard_bounds(n, world, r, ctypes.byref(lo), ctypes.byref(hi)) == 0
+                assert (lo.value, hi.value) == shard_bounds(n, world, r)
+                assert lo.value == prev
+                prev = hi.value
+            assert prev == n
+    assert fks_lib.fks_shard_bounds(4, 0, 0, ctypes.byref(lo), ctypes.byref(hi)) == 1
+    assert fks_lib.fks_shard_bounds(4, 2, 2, ctypes.byref(lo), ctypes.byref(hi)) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_device_context_matches_single(fks_lib, oracle_lib, devices):
+    """fks_create_multi over a device list (the same MI355X listed k times runs k shards on
+    k contexts): results bit-identical to one context and to the oracle; statistics summed."""
+    import oracle
+    from fast_kinematic_simulator_amd import MultiDeviceSimulator, make_linked_simulator
+    from fast_kinematic_simulator_amd import workloads as W
+
+    wl = W.cfg3(61 / 65536)
+    multi = MultiDeviceSimulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed, devices)
+    single = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
+    try:
+        assert multi.num_devices() == len(devices)
+        multi.set_call_index(3)
+        single.set_call_index(3)
+        m = multi.forward_simulate_arrays(wl.robot, wl.starts, wl.targets, True)
+        s = single.forward_simulate_arrays(wl.robot, wl.starts, wl.targets, True)
+        for k in ("positions", "collided", "microsteps", "resolver_iterations", "error_flags"):
+            assert np.array_equal(m[k], s[k]), k
+        assert multi.get_statistics() == single.get_statistics()
+        mc, sc = multi.last_call_counters(), single.last_call_counters()
+        for k in ("particles", "microsteps", "resolver_iterations", "sdf_bytes", "least_squares_rows", "controller_steps"):
+            assert mc[k] == sc[k], k
+    finally:
+        multi.close()
+        single.close()
+    o = oracle.forward_simulate(wl.environment(), wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts, wl.targets, True,
+                                call_index=3)
+    assert np.array_equal(m["positions"], o["positions"])
