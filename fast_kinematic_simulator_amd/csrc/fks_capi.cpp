@@ -29,6 +29,9 @@
 extern "C" __global__ void fks_simulate_linked(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se2(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se3(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_linked_indiv(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_se2_indiv(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_se3_indiv(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_traced(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se2_traced(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se3_traced(const fksd::SimArgs* args);
@@ -62,11 +65,11 @@ sim_kernel_t traced_kernel_for(int robot_type) {
     }
 }
 
-sim_kernel_t kernel_for(int robot_type) {
+sim_kernel_t kernel_for(int robot_type, bool individual_jacobians = false) {
     switch (robot_type) {
-        case FKS_ROBOT_SE2: return fks_simulate_se2;
-        case FKS_ROBOT_SE3: return fks_simulate_se3;
-        default: return fks_simulate_linked;
+        case FKS_ROBOT_SE2: return individual_jacobians ? fks_simulate_se2_indiv : fks_simulate_se2;
+        case FKS_ROBOT_SE3: return individual_jacobians ? fks_simulate_se3_indiv : fks_simulate_se3;
+        default: return individual_jacobians ? fks_simulate_linked_indiv : fks_simulate_linked;
     }
 }
 
@@ -954,7 +957,7 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? (groups_needed > 0 ? groups_needed : 1)
                                                                                   : ctx->grid_groups);
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
-    hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type) : kernel_for(ctx->R.type), dim3(grid),
+    hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type) : kernel_for(ctx->R.type, ctx->individual_jacobians != 0), dim3(grid),
                        dim3(64 * fksd::kWavesPerGroup), ctx->lds_bytes, s, static_cast<const fksd::SimArgs*>(ctx->d_args));
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));

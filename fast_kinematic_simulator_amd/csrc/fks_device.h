@@ -209,7 +209,7 @@ inline
 
 /* per-wave scratch layout (doubles) */
 struct ScratchLayout {
-    uint64_t J, b, keys, corr, flag, cand, list, dense, total;
+    uint64_t J, b, keys, corr, flag, cand, list, cellw, dense, total;
 };
 inline
 #if defined(__HIPCC__)
@@ -232,6 +232,8 @@ inline
     o += (uint64_t)P;
     l.list = o;
     o += (uint64_t)P;
+    l.cellw = o; /* ExtractSelfCollidingPoints tables: 4 x kMaxGeoms int32, kMaxGeoms momenta (D4) */
+    o += 2u * kMaxGeoms + 4u * kMaxGeoms;
     l.dense = o;
     o += (G > 1) ? self_dense_words(G) : 8;
     l.total = (o + 7) & ~7ull;

@@ -428,7 +428,6 @@ struct Sim {
     uint32_t err;          /* per-lane error bits, OR-reduced at decision points */
     uint64_t lane_bytes;   /* per-lane algorithmic SDF bytes */
     uint64_t micro_count, resolver_count, step_count, lsq_rows;
-    uint64_t self_checks, self_points; /* non-empty self-collision maps, self-corrected points (wave totals) */
     uint32_t* stats; /* LDS, lane 0 updates */
     uint64_t* phase; /* LDS, FKS_NUM_PHASES cycle sums, lane 0 updates */
     const JointDev* joints;          /* LDS copy of R.joints */
@@ -441,6 +440,10 @@ struct Sim {
     uint64_t local;            /* particle index within the call (traced kernels) */
     uint32_t tr_steps, tr_cfgs; /* trace records produced so far (traced kernels) */
 };
+
+/* wave totals of the self-collision branch (kCntSelfChecks, kCntSelfPoints), kept in the
+ * wave's LDS block (misc + 28, + 29) rather than in registers: the branch is rare */
+__device__ __forceinline__ uint64_t* self_counters(const Sim& s) { return reinterpret_cast<uint64_t*>(s.lds + s.A->L.misc + 28); }
 
 /* ForwardSimulationStepTrace records (traced kernel instantiations only) */
 template <bool TR>
@@ -1191,9 +1194,14 @@ __device__ __noinline__ uint32_t extract_cell(const SimArgs* __restrict__ Ap, do
     double* flag = scratch + SL.flag;
     double* dense = scratch + SL.dense;
     if (nm <= 1) return 0;
-    /* by_link: geometries present (ascending), ranges into members */
-    int geo[kMaxGeoms];
-    int gbeg[kMaxGeoms], gend[kMaxGeoms];
+    /* by_link: geometries present (ascending), ranges into members.  The per-cell tables
+     * live in the wave's global workspace, not in private arrays: private arrays become
+     * per-lane scratch of the whole kernel, and scratch size limits the waves in flight */
+    int32_t* geo = reinterpret_cast<int32_t*>(scratch + SL.cellw);
+    int32_t* gbeg = geo + kMaxGeoms;
+    int32_t* gend = gbeg + kMaxGeoms;
+    int32_t* others = gend + kMaxGeoms;
+    D4* mom = reinterpret_cast<D4*>(scratch + SL.cellw + 2 * kMaxGeoms);
     int ng = 0;
     for (int m = 0; m < nm; ++m) {
         const int g = gp(R.point_geom)[members[m]];
@@ -1217,7 +1225,6 @@ __device__ __noinline__ uint32_t extract_cell(const SimArgs* __restrict__ Ap, do
     if (ncollide_links < 2) return 0;
     (*cells)++;
     const double tm = A.time_multiplier;
-    D4 mom[kMaxGeoms];
     for (int a = 0; a < ng; ++a) {
         const uint64_t disallowed = present & ~gp(R.allowed_mask)[geo[a]] & ~(1ull << geo[a]);
         mom[a] = D4{0.0, 0.0, 0.0, 0.0};
@@ -1233,7 +1240,6 @@ __device__ __noinline__ uint32_t extract_cell(const SimArgs* __restrict__ Ap, do
     for (int a = 0; a < ng; ++a) {
         const uint64_t disallowed = present & ~gp(R.allowed_mask)[geo[a]] & ~(1ull << geo[a]);
         if (!disallowed) continue;
-        int others[kMaxGeoms];
         int n = 0;
         for (int b = 0; b < ng; ++b)
             if ((disallowed >> geo[b]) & 1ull) others[n++] = b;
@@ -1501,7 +1507,7 @@ __device__ bool check_collision(Sim& s, const double* Tp, const double* Tc) {
         tock(s, FKS_PHASE_SELF_CHECK, t0);
     }
     s.self_nonempty = self;
-    if (self) s.self_checks++;
+    if (self && s.lane == 0) self_counters(s)[0]++;
     return env || self;
 }
 
@@ -1588,7 +1594,10 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
             if (has_env) pcorr = D3{pcorr.x + ecorr.x, pcorr.y + ecorr.y, pcorr.z + ecorr.z};
         }
         const uint64_t m = __ballot(has);
-        if (s.self_nonempty) s.self_points += (uint64_t)__popcll(__ballot(has && flag[i] != 0.0));
+        if (s.self_nonempty) {
+            const uint64_t k = (uint64_t)__popcll(__ballot(has && flag[i] != 0.0));
+            if (ln == 0) self_counters(s)[1] += k;
+        }
         if (has) {
             const uint32_t row = (rows + (uint32_t)__popcll(m & ((1ull << ln) - 1ull))) * 3u;
             bv[row + 0] = pcorr.x;
@@ -2234,8 +2243,11 @@ __device__ __noinline__ void individual_jacobians_solve(Sim& s, uint32_t Rn, dou
 }
 
 /* one controller step: ResolveForwardSimulation (SPCS:1546-1816).
- * returns 0 ok, 1 error; sets collided/failed; result config in res_cfg */
-template <int RT, bool TR>
+ * returns 0 ok, 1 error; sets collided/failed; result config in res_cfg.
+ * IND: the individual-Jacobian solve (SPCS:1966-1988) is compiled into a kernel of its
+ * own, so the default stacked-Jacobian kernel does not carry it; the traced kernels
+ * (not on the hot path) read the choice at run time. */
+template <int RT, bool TR, bool IND>
 __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg, bool allow_contacts, bool* out_collided,
                             bool* out_failed, double*& Tcur, double*& Tprev) {
     const SimArgs& A = *s.A;
@@ -2334,7 +2346,7 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
                 tock(s, FKS_PHASE_CORRECTIONS, t0);
                 if (s.err) return 1;
                 t0 = tick();
-                if (A.individual_jacobians) {
+                if (IND || (TR && A.individual_jacobians)) {
                     individual_jacobians_solve(s, Rn, x);
                 } else if (Rn <= 8u && R.D < kWave)
                     qr_solve_cols<8>(s.A, s.lds, s.scratch, ln, Rn, x);
@@ -2671,7 +2683,7 @@ __device__ __forceinline__ void kinematics(const SimArgs* __restrict__ args, dou
     }
 }
 
-template <int RT, bool TR>
+template <int RT, bool TR, bool IND = false>
 __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ args, double* lds_mem) {
     const SimArgs& A = *args;
     const RobotDev& R = A.R;
@@ -2735,8 +2747,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     if (ln < FKS_NUM_PHASES) s.phase[ln] = 0;
     s.lane_bytes = 0;
     uint64_t w_steps = 0, w_micro = 0, w_resolver = 0, w_lsq = 0, w_errors = 0;
-    s.self_checks = 0;
-    s.self_points = 0;
+    if (ln < 2) self_counters(s)[ln] = 0;
     wsync();
     while (true) {
         /* ticket t: segment t / n of particle t % n, so every particle's first segment is
@@ -2787,8 +2798,9 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                     if (w_lsq) atomicAdd(A.counters + kCntLsqRows, (unsigned long long)w_lsq);
                     if (bytes) atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes);
                     if (w_errors) atomicAdd(A.counters + kCntErrorParticles, (unsigned long long)w_errors);
-                    if (s.self_checks) atomicAdd(A.counters + kCntSelfChecks, (unsigned long long)s.self_checks);
-                    if (s.self_points) atomicAdd(A.counters + kCntSelfPoints, (unsigned long long)s.self_points);
+                    const uint64_t* sc = self_counters(s);
+                    if (sc[0]) atomicAdd(A.counters + kCntSelfChecks, (unsigned long long)sc[0]);
+                    if (sc[1]) atomicAdd(A.counters + kCntSelfPoints, (unsigned long long)sc[1]);
                     for (int k = 0; k < FKS_NUM_PHASES; ++k)
                         if (s.phase[k]) atomicAdd(A.counters + kPhaseBase + k, (unsigned long long)s.phase[k]);
                 }
@@ -2876,7 +2888,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             wsync();
             tock(s, FKS_PHASE_CONTROL, t0);
             bool rc = false, rf = false;
-            const int status = resolve_step<RT, TR>(s, cfg, res_cfg, A.allow_contacts != 0, &rc, &rf, Tcur, Tprev);
+            const int status = resolve_step<RT, TR, IND>(s, cfg, res_cfg, A.allow_contacts != 0, &rc, &rf, Tcur, Tprev);
             s.err = wave_or(s.err);
             if (status != 0 || s.err) {
                 ended = true;
@@ -3008,6 +3020,20 @@ extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se2(const SimArgs* __re
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se3(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
     simulate_particles<FKS_ROBOT_SE3, false>(args, lds_mem);
+}
+
+/* simulate_with_individual_jacobians = true (SPCS:420, 1629; fks_set_individual_jacobians) */
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked_indiv(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_LINKED, false, true>(args, lds_mem);
+}
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se2_indiv(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_SE2, false, true>(args, lds_mem);
+}
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se3_indiv(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_SE3, false, true>(args, lds_mem);
 }
 
 /* traced instantiations: ForwardSimulateRobot with enable_tracing (fks_forward_simulate_traced) */

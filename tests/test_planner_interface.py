@@ -176,9 +176,10 @@ def test_planner_interface_matches_oracle(fks_lib, oracle_lib, name):
             assert o["counters"]["resolver_iterations"] > 0  # the scene makes contact
     # traced ForwardSimulateRobot of particle 0
     r0, buf = oracle.forward_simulate_traced(env, wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts[:1],
-                                             wl.targets[:1], wl.allow_contacts, call_index=2)
+                                             wl.targets[:1], wl.allow_contacts, call_index=2, config_capacity=16384)
     assert np.array_equal(_hexrow(rows["traced"][0][1:1 + W_]), r0["positions"][0])
     tr = buf.particle(0)
+    assert not tr.truncated
     nconf = sum(len(c.contact_resolution_steps) for rs in tr.resolver_steps for c in rs.contact_resolver_steps)
     t = rows["trace"][0]
     assert (int(t[0]), int(t[1])) == (len(tr.resolver_steps), nconf)
