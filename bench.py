@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 METRIC = "particle-microsteps/sec, 7-DOF arm vs 256³ SDF, at 1/2/4/8 MI355X"
 UNIT = "particle-microsteps/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s spec)
+FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak, AMD's public spec (not in the container guide)
 PARTICLES_PER_GPU = 65536
 # the other BASELINE.json configs, runnable with --workload for side measurements
 # (the headline line is cfg3): base particle count of the config, default per GPU, description
@@ -48,11 +49,35 @@ def log(msg):
     print(msg, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(wl, sample_particles: int, threads: int):
+def host_cpu():
+    """What the CPU baseline ran on: the host's logical CPUs (nproc), the ones this process
+    may use (affinity), the OpenMP thread count and the lscpu model string."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "model": model}
+
+
+def cpu_baseline(wl, sample_particles: int):
     """The oracle in reference-RNG mode (per-OpenMP-thread mt19937_64, SPCS:431-441,
-    #pragma omp parallel for over particles, SPCS:795) on a prefix of the batch."""
+    #pragma omp parallel for over particles, SPCS:795) on a prefix of the batch, with
+    every OpenMP thread the process is given (OMP_NUM_THREADS: 16 on the GPU box, its CPU
+    share per GPU).  The particle loop is embarrassingly parallel, so the per-core rate
+    is reported too."""
     import oracle
 
+    threads = int(oracle.lib().oracle_max_threads())
     env = wl.environment()
     starts = wl.starts[:sample_particles]
     t0 = time.perf_counter()
@@ -60,9 +85,27 @@ def cpu_baseline(wl, sample_particles: int, threads: int):
                                 rng_mode=oracle.RNG_REFERENCE, threads=threads)
     dt = time.perf_counter() - t0
     micro = int(r["counters"]["microsteps"])
-    return {"value": micro / dt, "unit": UNIT, "cores": threads, "kind": "port",
+    return {"value": micro / dt, "unit": UNIT, "cores": threads, "kind": "port", "per_core": micro / dt / threads,
+            "host": host_cpu(),
             "sample": f"first {len(starts)} particles of {wl.name} x {wl.steps} controller steps ({micro} microsteps, "
-                      f"{dt:.1f} s), oracle in reference-RNG mode, OpenMP {threads} threads"}
+                      f"{dt:.1f} s), oracle in reference-RNG mode (per-check robot clones, hash-map self-collision, "
+                      f"dynamic-matrix QR as SPCS), OpenMP {threads} threads"}
+
+
+def fp64_algorithmic_flops(robot, counters):
+    """FP64 flops the reference's algorithm performs for the counted work:
+    per microstep the FK (145 per moving joint: angle-axis matrix 19 + two 3x4 compositions
+    63 each; 63 per fixed joint) and, for every point, the environment check (45: link
+    transform 21, inverse grid origin 21, scaling 3) and the self-collision key (45,
+    SPCS:1202-1236); per controller step two FKs and two workspace-motion maxima (50 per
+    point); per resolver iteration a Jacobian (12 per point and dof, SPCS:1858), the
+    distance estimate (45 per point), one FK and a motion maximum; per least-squares row
+    2 D^2 for the Householder QR (SPCS:1994)."""
+    P, D = robot.num_points, robot.num_dofs
+    J = len(robot.joints)
+    fk = 145 * D + 63 * (J - D) if robot.robot_type == 0 else 63
+    return (counters["microsteps"] * (fk + 90 * P) + counters["controller_steps"] * (2 * fk + 100 * P)
+            + counters["resolver_iterations"] * (P * (95 + 12 * D) + fk) + 2 * D * D * counters["least_squares_rows"])
 
 
 def config_check_bench(sim, wl, dev, n=1 << 20, reps=3, cpu_sample=16384, threads=16, with_cpu=True):
@@ -105,17 +148,19 @@ def config_check_bench(sim, wl, dev, n=1 << 20, reps=3, cpu_sample=16384, thread
 
 
 def load_traffic():
-    """HBM bytes per launch of the simulation kernel from the committed rocprofv3 PMC
-    summary (profiles/*_pmc.json written by tools/profile_pmc.py), or None."""
+    """HBM bytes per launch of the simulation kernel and the L2 hit rate from the committed
+    rocprofv3 PMC summary (profiles/latest_pmc.json, written by tools/profile_pmc.py from
+    separate FETCH_SIZE / WRITE_SIZE / TCC_HIT+MISS passes of this bench), or Nones.  It is
+    the builder's profile of the same command, not a measurement of this run."""
     path = os.path.join(ROOT, "profiles", "latest_pmc.json")
     if not os.path.exists(path):
-        return None
+        return None, None, None
     try:
         with open(path) as f:
             d = json.load(f)
-        return float(d["hbm_bytes_per_launch"])
+        return float(d["hbm_bytes_per_launch"]), d.get("l2_hit_rate"), d.get("source", "profiles/latest_pmc.json")
     except Exception:
-        return None
+        return None, None, None
 
 
 def main():
@@ -126,7 +171,7 @@ def main():
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS),
                     help="BASELINE.json config (the headline metric is cfg3)")
     ap.add_argument("--particles", type=int, default=0, help="particles per GPU (default: the workload's)")
-    ap.add_argument("--cpu-sample", type=int, default=2048, help="particles in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=4096, help="particles in the CPU-baseline sample (SURVEY §8d: 4096)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config-check", action="store_true", help="skip the batched CheckConfigCollision line")
     args = ap.parse_args()
@@ -220,6 +265,8 @@ def main():
     geom = sim.launch_geometry()
     local_micro = int(micro_total.item())
     assert local_micro == int(tot["microsteps"]), (local_micro, tot["microsteps"])
+    stats = sim.get_statistics()  # this rank's SimpleParticleContactSimulator counters (SPCS:488-500)
+    stat_names = sorted(stats)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -227,6 +274,10 @@ def main():
         m = torch.tensor([local_micro], dtype=torch.int64, device=dev)
         dist.all_reduce(m)
         all_micro = int(m.item())
+        # GetStatistics of the whole job: every rank's counters summed (RCCL all-reduce)
+        st = torch.tensor([stats[k] for k in stat_names], dtype=torch.float64, device=dev)
+        dist.all_reduce(st)
+        stats = {k: float(v) for k, v in zip(stat_names, st.tolist())}
     else:
         all_micro = local_micro
 
@@ -235,15 +286,16 @@ def main():
         avg_kernel_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3
         bytes_per_launch = tot["sdf_bytes"] / calls
         achieved = bytes_per_launch / avg_kernel_s / 1e9
-        traffic = load_traffic() if args.workload == "cfg3" else None  # the PMC summary is of the cfg3 kernel
+        traffic, l2_hit, traffic_src = load_traffic() if args.workload == "cfg3" else (None, None, None)  # cfg3 profile
+        per_launch = {k: tot[k] / calls for k in ("microsteps", "controller_steps", "resolver_iterations", "least_squares_rows")}
+        flops = fp64_algorithmic_flops(wl.robot, per_launch)
         cpu = None
         if not args.no_cpu_baseline:
-            threads = max(1, min(16, os.cpu_count() or 1))
             t0 = time.perf_counter()
             sample = min(args.cpu_sample, n_total)
             cwl = W.WORKLOADS[args.workload](scale=sample / float(base))
             cwl._env = denv.download()
-            cpu = cpu_baseline(cwl, sample, threads)
+            cpu = cpu_baseline(cwl, sample)
             log(f"cpu baseline {cpu['value']:.0f} {UNIT} in {time.perf_counter() - t0:.1f}s")
         value = all_micro / elapsed
         # the host-buffer entry (fks_forward_simulate: starts/targets over PCIe, outcomes
@@ -293,10 +345,17 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
+                "l2_hit_rate": l2_hit,
                 "kernel": KERNELS[wl.robot.robot_type],
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
+                # second entry: the kernel is FP64-VALU- and latency-bound, not HBM-bound
+                "fp64": {"bound": "valu", "achieved": flops / avg_kernel_s / 1e12, "peak": FP64_VECTOR_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": flops / avg_kernel_s / 1e12 / FP64_VECTOR_PEAK_TFLOPS,
+                         "algorithmic_flops_per_launch": flops},
             },
+            "statistics": stats,
             # share of the persistent grid's wave slots that held a particle during the timed
             # launches (1.0 = no tail): wave residency in 100 MHz s_memrealtime ticks
             "wave_slots": {"resident_waves": geom["resident_waves"],

@@ -216,6 +216,7 @@ struct fks_context {
     uint64_t scratch_per_wave = 0;
     uint32_t grid_waves = 0;
     uint32_t grid_groups = 0;
+    uint32_t waves_per_group = fksd::kWavesPerGroup;
     size_t lds_bytes = 0;
     unsigned long long* d_counters = nullptr; /* kNumCounters + queue + phase cycles */
     uint64_t phase_last[FKS_NUM_PHASES] = {};
@@ -756,17 +757,38 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     }
     /* launch geometry: one wave per workgroup, as many resident waves as fit */
     const fksd::LdsLayout L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds);
-    ctx->lds_bytes = ((size_t)L.shared_total + (size_t)fksd::kWavesPerGroup * L.total) * sizeof(double);
+    /* four waves share one LDS copy of the robot tables; robots whose per-wave blocks do
+     * not fit four times in the CU's 160 KiB run two or one wave per workgroup (the
+     * largest robot the descriptor admits, 64 links / dofs / geometries, fits at one) */
+    ctx->waves_per_group = fksd::kWavesPerGroup;
+    for (;;) {
+        ctx->lds_bytes = ((size_t)L.shared_total + (size_t)ctx->waves_per_group * L.total) * sizeof(double);
+        if (ctx->lds_bytes <= 160 * 1024 || ctx->waves_per_group == 1) break;
+        ctx->waves_per_group /= 2;
+    }
     if (ctx->lds_bytes > 160 * 1024) return fail(ctx, FKS_ERR_UNSUPPORTED, "robot too large for the LDS layout");
     int blocks_per_cu = 0;
     HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, reinterpret_cast<const void*>(kernel_for(R.type)),
-                                                              64 * fksd::kWavesPerGroup, ctx->lds_bytes));
+                                                              64 * ctx->waves_per_group, ctx->lds_bytes));
     if (blocks_per_cu < 1) return fail(ctx, FKS_ERR_UNSUPPORTED, "kernel does not fit on a CU");
     int cus = 0;
     HIP_TRY(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     ctx->grid_groups = (uint32_t)(cus * blocks_per_cu);
-    ctx->grid_waves = ctx->grid_groups * (uint32_t)fksd::kWavesPerGroup;
+    ctx->grid_waves = ctx->grid_groups * ctx->waves_per_group;
     ctx->scratch_per_wave = fksd::make_scratch_layout(3u * P, R.D, (int)P, G).total;
+    /* the per-wave workspace grows with 3P x D (the stacked Jacobian) and the robot's
+     * geometry count: for very large robots the persistent grid keeps only as many waves
+     * as half the free HBM holds (the ticket queue hands out the work either way) */
+    {
+        size_t free_b = 0, total_b = 0;
+        HIP_TRY(ctx, hipMemGetInfo(&free_b, &total_b));
+        const size_t per_group = (size_t)ctx->waves_per_group * ctx->scratch_per_wave * sizeof(double);
+        const size_t max_groups = std::max<size_t>(1, (free_b / 2) / std::max<size_t>(1, per_group));
+        if ((size_t)ctx->grid_groups > max_groups) {
+            ctx->grid_groups = (uint32_t)max_groups;
+            ctx->grid_waves = ctx->grid_groups * ctx->waves_per_group;
+        }
+    }
     HIP_TRY(ctx, hipMalloc((void**)&ctx->d_scratch, (size_t)ctx->grid_waves * ctx->scratch_per_wave * sizeof(double)));
     ctx->R = R;
     ctx->has_robot = true;
@@ -953,12 +975,12 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     *ctx->h_args = a;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice, s));
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, fksd::kCounterWords * sizeof(unsigned long long), s));
-    const uint64_t groups_needed = (n + fksd::kWavesPerGroup - 1) / fksd::kWavesPerGroup;
+    const uint64_t groups_needed = (n + ctx->waves_per_group - 1) / ctx->waves_per_group;
     const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? (groups_needed > 0 ? groups_needed : 1)
                                                                                   : ctx->grid_groups);
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
     hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type) : kernel_for(ctx->R.type, ctx->individual_jacobians != 0), dim3(grid),
-                       dim3(64 * fksd::kWavesPerGroup), ctx->lds_bytes, s, static_cast<const fksd::SimArgs*>(ctx->d_args));
+                       dim3(64 * ctx->waves_per_group), ctx->lds_bytes, s, static_cast<const fksd::SimArgs*>(ctx->d_args));
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_counters, ctx->d_counters, fksd::kCounterWords * sizeof(unsigned long long),
@@ -1026,10 +1048,10 @@ fks_status fks_check_config_collision_device(fks_context* ctx, const double* d_c
     *ctx->h_args = a;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice, s));
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, fksd::kCounterWords * sizeof(unsigned long long), s));
-    const uint64_t groups_needed = (n + fksd::kWavesPerGroup - 1) / fksd::kWavesPerGroup;
+    const uint64_t groups_needed = (n + ctx->waves_per_group - 1) / ctx->waves_per_group;
     const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? groups_needed : ctx->grid_groups);
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
-    hipLaunchKernelGGL(check_kernel_for(ctx->R.type), dim3(grid), dim3(64 * fksd::kWavesPerGroup), ctx->lds_bytes, s,
+    hipLaunchKernelGGL(check_kernel_for(ctx->R.type), dim3(grid), dim3(64 * ctx->waves_per_group), ctx->lds_bytes, s,
                        static_cast<const fksd::SimArgs*>(ctx->d_args));
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
@@ -1311,11 +1333,11 @@ fks_status fks_kinematics(fks_context* ctx, int32_t mode, const double* configs,
     *ctx->h_args = a;
     e = hipMemcpy(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice);
     if (e == hipSuccess) {
-        const uint64_t groups_needed = (n + fksd::kWavesPerGroup - 1) / fksd::kWavesPerGroup;
+        const uint64_t groups_needed = (n + ctx->waves_per_group - 1) / ctx->waves_per_group;
         const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? groups_needed : ctx->grid_groups);
         sim_kernel_t k = (ctx->R.type == FKS_ROBOT_SE2) ? fks_kinematics_se2
                                                         : (ctx->R.type == FKS_ROBOT_SE3 ? fks_kinematics_se3 : fks_kinematics_linked);
-        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * fksd::kWavesPerGroup), ctx->lds_bytes, nullptr,
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64 * ctx->waves_per_group), ctx->lds_bytes, nullptr,
                            static_cast<const fksd::SimArgs*>(ctx->d_args));
         e = hipGetLastError();
     }

@@ -99,7 +99,8 @@ struct RobotDev {
 };
 
 /* LDS carve-out (in doubles), identical on host and device.  A workgroup holds
- * kWavesPerGroup waves, one particle each.  The robot tables (joints ... gpairs) are
+ * kWavesPerGroup waves, one particle each (2 or 1 for robots whose blocks do not fit
+ * four times in the 160 KiB of a CU, fks_set_robot).  The robot tables (joints ... gpairs) are
  * one shared copy at the start of the workgroup's LDS (offsets relative to it,
  * `shared_total` doubles); every other offset is relative to the wave's own block of
  * `total` doubles that follows. */
@@ -136,8 +137,8 @@ inline
     l.shared_total = o;
     /* per wave */
     o = 0;
-    l.rstate = o; /* kRoundState per round, persists across the wave's particles */
-    o += (uint32_t)kRoundState * (NR > 0 ? NR : 1);
+    l.rstate = o; /* kRoundState per round r < 64 (the 64-bit skip masks), persists across the wave's particles */
+    o += (uint32_t)kRoundState * (uint32_t)(NR < 1 ? 1 : (NR > 64 ? 64 : NR));
     l.noise = o; /* actuator noise samples of the next floor(64/D) microsteps, [micro][dof] */
     o += 64;
     l.noise_err = o; /* their error bits, 64 x u32 */

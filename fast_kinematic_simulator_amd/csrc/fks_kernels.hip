@@ -2467,7 +2467,7 @@ __device__ __forceinline__ void setup_wave(const SimArgs* __restrict__ args, dou
     s.shared = shared;
     s.lds = lds_mem + A.L.shared_total + (uint64_t)wave * A.L.total;
     s.ldsi = reinterpret_cast<int32_t*>(s.lds + A.L.ints);
-    s.scratch = A.scratch + ((uint64_t)blockIdx.x * kWavesPerGroup + (uint64_t)wave) * A.scratch_per_wave;
+    s.scratch = A.scratch + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)wave) * A.scratch_per_wave;
     s.lane = lane_id();
     s.stats = reinterpret_cast<uint32_t*>(s.lds + s.A->L.misc + 24);
     s.phase = reinterpret_cast<uint64_t*>(s.lds + s.A->L.misc + 8);
@@ -2599,9 +2599,9 @@ __device__ __forceinline__ void check_configs(const SimArgs* __restrict__ args, 
     const int ln = s.lane;
     double* cfg = s.lds + A.L.cfg;
     double* T = s.lds + A.L.Tcur;
-    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerGroup;
+    const uint64_t stride = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint64_t bytes_total = 0;
-    for (uint64_t c = (uint64_t)blockIdx.x * kWavesPerGroup + (threadIdx.x >> 6); c < A.n; c += stride) {
+    for (uint64_t c = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < A.n; c += stride) {
         set_position<RT>(s, A.starts + c * (uint64_t)R.W, cfg);
         fk<RT>(s, cfg, T);
         /* CheckEnvironmentCollision: pairs of 64-point rounds, bytes up to the first
@@ -2656,8 +2656,8 @@ __device__ __forceinline__ void kinematics(const SimArgs* __restrict__ args, dou
     double* cfg = s.lds + A.L.cfg;
     double* out_cfg = s.lds + A.L.cfg_tmp;
     double* T = s.lds + A.L.Tcur;
-    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerGroup;
-    for (uint64_t c = (uint64_t)blockIdx.x * kWavesPerGroup + (threadIdx.x >> 6); c < A.n; c += stride) {
+    const uint64_t stride = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t c = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < A.n; c += stride) {
         set_position<RT>(s, A.starts + c * (uint64_t)R.W, cfg);
         if (A.kin_mode == FKS_KIN_APPLY_CONTROL_INPUT) {
             double* in = s.lds + A.L.u;
@@ -2720,7 +2720,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     s.shared = shared;
     s.lds = lds_mem + A.L.shared_total + (uint64_t)wave * A.L.total;
     s.ldsi = reinterpret_cast<int32_t*>(s.lds + A.L.ints);
-    s.scratch = A.scratch + ((uint64_t)blockIdx.x * kWavesPerGroup + (uint64_t)wave) * A.scratch_per_wave;
+    s.scratch = A.scratch + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)wave) * A.scratch_per_wave;
     s.lane = lane_id();
     s.stats = reinterpret_cast<uint32_t*>(s.lds + s.A->L.misc + 24); /* 8 x u32 */
     s.phase = reinterpret_cast<uint64_t*>(s.lds + s.A->L.misc + 8); /* FKS_NUM_PHASES x u64 */
@@ -2728,7 +2728,8 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     s.ctrl = reinterpret_cast<const fks_dof_controller*>(shared + A.L.ctrl);
     s.dofj = reinterpret_cast<const int32_t*>(shared + A.L.dofj);
     s.base = shared + A.L.base;
-    for (int r = s.lane; r < R.nrounds; r += kWave) s.lds[A.L.rstate + kRoundState * r + 12] = kInvalidRound;
+    /* skip-proof cache of the first 64 rounds (the skip masks are 64-bit; later rounds are always read) */
+    if (s.lane < R.nrounds) s.lds[A.L.rstate + kRoundState * s.lane + 12] = kInvalidRound;
     wsync();
     const int ln = s.lane;
     const int W = R.W, D = R.D;

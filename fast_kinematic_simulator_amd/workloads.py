@@ -367,13 +367,15 @@ def crowded_cell(scale: float = 1.0, links: int = 10) -> Workload:
                     solver, 100.0, 22, True, 128, 0.01)
 
 
-def long_chain_robot(dofs: int = 32) -> RobotDescription:
-    """A `dofs`-DOF serial chain of short links (alternating y / x axes), 16 points per link."""
-    joints, geoms = [], [(0, cylinder_points(0.05, 0.03, 16, 4))]
+def long_chain_robot(dofs: int = 32, points_per_link: int = 16) -> RobotDescription:
+    """A `dofs`-DOF serial chain of short links (alternating y / x axes), `points_per_link`
+    points per link."""
+    k = points_per_link
+    joints, geoms = [], [(0, cylinder_points(0.05, 0.03, k, k // 4))]
     for i in range(dofs):
         joints.append(Joint(parent=i, child=i + 1, type=_capi.JOINT_REVOLUTE, origin=transform34([0, 0, 0.05 if i == 0 else 0.03]),
                             axis=(0.0, 1.0, 0.0) if i % 2 == 0 else (1.0, 0.0, 0.0), lower=-2.5, upper=2.5))
-        geoms.append((i + 1, cylinder_points(0.03, 0.012, 16, 4)))
+        geoms.append((i + 1, cylinder_points(0.03, 0.012, k, k // 4)))
     allowed = [(i, i + 1) for i in range(dofs)] + [(i, i + 2) for i in range(dofs - 1)]
     return make_linked_robot(transform34([0, 0, 0]), dofs + 1, joints, geoms, allowed, _arm_controllers(dofs, vmax=1.0),
                              [1.0] * dofs, name=f"chain_{dofs}dof")
@@ -411,5 +413,20 @@ def pid_free_space(scale: float = 1.0) -> Workload:
     return wl
 
 
-COVERAGE: Dict[str, Callable[..., Workload]] = {"folding_arm": folding_arm, "crowded_cell": crowded_cell,
+def giant_chain(scale: float = 1.0) -> Workload:
+    """The largest robot the descriptor admits: 64 links, 63 dofs, 64 geometries of 64
+    points (4096 points, 64 rounds).  Its per-wave LDS block does not fit four times in
+    a CU, so it runs with fewer waves per workgroup (fks_set_robot); the reference has no
+    size limit (TNUVA:486-517)."""
+    robot = long_chain_robot(63, 64)
+    rng = np.random.default_rng(13)
+    n = max(1, int(round(4 * scale)))
+    starts = np.tile(np.linspace(0.02, 0.08, 63), (n, 1)) + rng.uniform(-0.01, 0.01, size=(n, 63))
+    target = np.tile(np.array([0.3, -0.2]), 32)[None, :63]
+    solver = SimulatorSolverParameters(forward_simulation_time=0.05)
+    return Workload("giant_chain", "64-link, 63-DOF chain, 4096 points", robot, _open_space_env, starts, target, solver, 100.0,
+                    24, True, 128, 0.01)
+
+
+COVERAGE: Dict[str, Callable[..., Workload]] = {"giant_chain": giant_chain, "folding_arm": folding_arm, "crowded_cell": crowded_cell,
                                                 "long_chain": long_chain, "pid_free_space": pid_free_space}

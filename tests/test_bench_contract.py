@@ -32,8 +32,12 @@ def test_bench_json_line():
     assert d["dtype"] == "f64" and "workload" in d["config"]
     r = d["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    f = r["fp64"]
+    assert f["unit"] == "TFLOP/s" and f["achieved"] > 0 and abs(f["frac"] - f["achieved"] / f["peak"]) < 1e-12
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+    assert c["host"]["nproc"] >= 1 and abs(c["per_core"] * c["cores"] - c["value"]) < 1e-6 * c["value"]
+    assert d["statistics"]["successful_resolves"] > 0
     assert d["pcie_inclusive"]["value"] > 0
 
 

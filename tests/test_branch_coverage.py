@@ -7,7 +7,9 @@ impulse solve (ExtractSelfCollidingPoints SPCS:983-1171) applied as corrections
 non-default decay / initial-step / min-scaling / iteration limits (SPCS:1624, 1705-1761),
 continuous joints (angle wrap), the individual-Jacobian solve (SPCS:1966-1988, the
 simulate_with_individual_jacobians flag of SPCS:420, 1629), a self-collision cell shared by
-ten links (no capacity limit, as the reference's maps), and a 32-DOF chain.
+ten links (no capacity limit, as the reference's maps), a 32-DOF chain, and the largest
+robot the descriptor admits (64 links, 63 dofs, 4096 points; run with fewer waves per
+workgroup since its LDS block does not fit four times in a CU).
 
 The CPU tests show on the oracle that each scene reaches its branch (counter > 0); the
 GPU tests compare the HIP path with the oracle on the same scenes, every output, statistic
@@ -60,13 +62,16 @@ def _scene(name):
     if name == "crowded_cell":
         # more than 8 links corrected in one iteration: all 10 links x 8 points share one cell
         return W.crowded_cell(), {}, lambda c, s, r: c["self_corrected_points"] >= 80 * c["resolver_iterations"] > 0
+    if name == "giant_chain":
+        # 64 links / 63 dofs / 4096 points: fewer waves per workgroup (its LDS block does not fit four times)
+        return W.giant_chain(), {}, lambda c, s, r: c["microsteps"] > 0 and r["positions"].shape[1] == 63
     if name == "chain_32dof":
         return W.long_chain(), {}, lambda c, s, r: c["resolver_iterations"] > 0 and c["self_collision_checks"] > 0
     raise KeyError(name)
 
 
 SCENES = ["self_collision", "no_end_on_failure", "shortcut", "resolver_params", "continuous", "individual_jacobians",
-          "individual_jacobians_cfg3", "crowded_cell", "chain_32dof"]
+          "individual_jacobians_cfg3", "crowded_cell", "chain_32dof", "giant_chain"]
 
 
 @pytest.mark.parametrize("name", SCENES)

@@ -44,6 +44,8 @@ def main():
         "hbm_bytes_per_launch": fetch_b + write_b,
         "l2_hit_rate": sum(hits) / (sum(hits) + sum(misses)),
         "note": "FETCH_SIZE/WRITE_SIZE from separate rocprofv3 --pmc passes of bench.py --steps 2 --warmup 1; raw (uncalibrated for gathers)",
+        "source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / TCC_HIT_sum+TCC_MISS_sum passes of "
+                  "bench.py --steps 2 --warmup 1, tools/profile_pmc.py)",
     }
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for name in (f"{tag}_pmc.json", "latest_pmc.json"):
