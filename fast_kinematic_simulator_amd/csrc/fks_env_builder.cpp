@@ -208,25 +208,10 @@ extern "C" fks_status fks_env_build(const fks_obstacle* obstacles, int32_t num_o
                         if (!((double)distance > -(resolution * 1.5))) continue;
                         std::vector<Entry> list;
                         for (int a = 0; a < 3; ++a) {
-                            double normal[3] = {0, 0, 0}, entry[3] = {0, 0, 0};
-                            if (id3[a] == 0) {
-                                normal[a] = -1.0;
-                                entry[a] = 1.0;
-                            } else if (id3[a] == nc[a] - 1) {
-                                normal[a] = 1.0;
-                                entry[a] = -1.0;
-                            } else {
-                                continue;
-                            }
-                            double rn[3], re[3];
-                            rotate3(ob.pose, normal, rn);
-                            rotate3(ob.pose, entry, re);
+                            if (id3[a] != 0 && id3[a] != nc[a] - 1) continue;
                             /* StoredSurfaceNormal: SafeNormal(normal), SafeNormal((entry, 0)) */
                             Entry E;
-                            const double en = fks_math::dsqrt(((re[0] * re[0] + re[1] * re[1]) + re[2] * re[2]) + 0.0 * 0.0);
-                            for (int b = 0; b < 3; ++b) E.e[b] = (en > 2.220446049250313e-16) ? re[b] / en : re[b];
-                            const double nn = fks_math::dsqrt((rn[0] * rn[0] + rn[1] * rn[1]) + rn[2] * rn[2]);
-                            for (int b = 0; b < 3; ++b) E.e[3 + b] = (nn > 2.220446049250313e-16) ? rn[b] / nn : rn[b];
+                            fks_env::face_entry(ob.pose, a, id3[a] == 0, E.e);
                             list.push_back(E);
                         }
                         surface[grid.linear(idx[0], idx[1], idx[2])] = list;

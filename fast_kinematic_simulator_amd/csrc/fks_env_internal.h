@@ -97,7 +97,9 @@ FKS_HD inline void obstacle_sample_world(const fks_obstacle& ob, double resoluti
 }
 
 /* StoredSurfaceNormal entry of a boundary sample along axis a (SEB.cpp:300-460):
- * SafeNormal((entry, 0)) then SafeNormal(normal), rotated into the world */
+ * SafeNormal((entry, 0)) then SafeNormal(normal), rotated into the world.  The
+ * Vector4d norm is Eigen's two-lane packet reduction (x^2 + z^2) + (y^2 + w^2)
+ * (DESIGN.md §2.3); the Vector3d norm is sequential. */
 FKS_HD inline void face_entry(const double* pose, int a, bool low_face, double E[6]) {
     double normal[3] = {0, 0, 0}, entry[3] = {0, 0, 0};
     normal[a] = low_face ? -1.0 : 1.0;
@@ -105,7 +107,7 @@ FKS_HD inline void face_entry(const double* pose, int a, bool low_face, double E
     double rn[3], re[3];
     rotate3(pose, normal, rn);
     rotate3(pose, entry, re);
-    const double en = fks_math::dsqrt(((re[0] * re[0] + re[1] * re[1]) + re[2] * re[2]) + 0.0 * 0.0);
+    const double en = fks_math::dsqrt((re[0] * re[0] + re[2] * re[2]) + (re[1] * re[1] + 0.0 * 0.0));
     for (int b = 0; b < 3; ++b) E[b] = (en > 2.220446049250313e-16) ? re[b] / en : re[b];
     const double nn = fks_math::dsqrt((rn[0] * rn[0] + rn[1] * rn[1]) + rn[2] * rn[2]);
     for (int b = 0; b < 3; ++b) E[3 + b] = (nn > 2.220446049250313e-16) ? rn[b] / nn : rn[b];

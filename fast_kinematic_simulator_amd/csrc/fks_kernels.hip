@@ -80,7 +80,10 @@ __device__ __forceinline__ D3 cross(const D3& a, const D3& b) {
     c.z = a.x * b.y - a.y * b.x;
     return c;
 }
-__device__ __forceinline__ double sqnorm4(const D4& v) { return ((v.x * v.x + v.y * v.y) + v.z * v.z) + v.w * v.w; }
+/* Eigen Vector4d squaredNorm / norm / dot reduce two-lane packets: (x + z) + (y + w)
+ * (SSE2 Packet2d, the reference's -O3 x86-64 build).  Vector3d
+ * reductions are sequential. */
+__device__ __forceinline__ double sqnorm4(const D4& v) { return (v.x * v.x + v.z * v.z) + (v.y * v.y + v.w * v.w); }
 __device__ __forceinline__ double sqnorm3(const D3& v) { return (v.x * v.x + v.y * v.y) + v.z * v.z; }
 __device__ __forceinline__ D4 safe_normal4(const D4& v) {
     const double n = dsqrt(sqnorm4(v));
@@ -584,7 +587,8 @@ __device__ bool lookup_normal(const SimArgs& A, const D4& loc, const D4& dir, D3
     double best_dot = -__builtin_huge_val();
     for (uint32_t e = begin; e < end; ++e) {
         const FKS_GLOBAL double* ent = gp(A.nent) + 6ull * e;
-        const double dot = (ent[0] * ux + ent[1] * uy) + ent[2] * uz;
+        /* EntryDirection4d().dot(unit_direction), packet order; both w terms are +0 */
+        const double dot = (ent[0] * ux + ent[2] * uz) + ent[1] * uy;
         if (dot > best_dot) {
             best_dot = dot;
             best = (int64_t)e;

@@ -36,6 +36,15 @@
 #define FKS_HD
 #endif
 
+#ifdef FKS_MATH_AUDIT_SYSTEM_LIBM
+/* restatement audit only (oracle/Makefile `audit`, host code): the system libm in place
+ * of the portable kernels, to measure how far results depend on them */
+#include <math.h>
+#define FKS_MATH_AUDIT_RETURN(expr) return (expr)
+#else
+#define FKS_MATH_AUDIT_RETURN(expr) (void)0
+#endif
+
 namespace fks_math {
 
 FKS_HD inline uint64_t bits(double x) { return __builtin_bit_cast(uint64_t, x); }
@@ -126,6 +135,7 @@ FKS_HD inline int32_t rem_pio2(double x, double* y0, double* y1) {
 }
 
 FKS_HD inline double sin(double x) {
+    FKS_MATH_AUDIT_RETURN(::sin(x));
     const uint32_t ix = hi_word(x) & 0x7fffffffu;
     if (ix <= 0x3fe921fbu) {
         if (ix < 0x3e500000u) return x;
@@ -144,6 +154,7 @@ FKS_HD inline double sin(double x) {
 }
 
 FKS_HD inline double cos(double x) {
+    FKS_MATH_AUDIT_RETURN(::cos(x));
     const uint32_t ix = hi_word(x) & 0x7fffffffu;
     if (ix <= 0x3fe921fbu) {
         if (ix < 0x3e46a09eu) return 1.0;
@@ -164,6 +175,11 @@ FKS_HD inline double cos(double x) {
 /* sin and cos of one argument sharing the argument reduction; bit-identical to
  * sin(x) and cos(x) */
 FKS_HD inline void sincos(double x, double* s, double* c) {
+#ifdef FKS_MATH_AUDIT_SYSTEM_LIBM
+    *s = ::sin(x);
+    *c = ::cos(x);
+    return;
+#endif
     const uint32_t ix = hi_word(x) & 0x7fffffffu;
     if (ix <= 0x3fe921fbu) {
         *s = (ix < 0x3e500000u) ? x : kernel_sin(x, 0.0, 0);
@@ -205,6 +221,7 @@ FKS_HD inline void sincos(double x, double* s, double* c) {
 
 /* ---------------- log ---------------- */
 FKS_HD inline double log(double x) {
+    FKS_MATH_AUDIT_RETURN(::log(x));
     const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
                  two54 = 1.80143985094819840000e+16, Lg1 = 6.666666666666735130e-01,
                  Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
@@ -260,6 +277,7 @@ FKS_HD inline double log(double x) {
 
 /* ---------------- atan / atan2 ---------------- */
 FKS_HD inline double atan(double x) {
+    FKS_MATH_AUDIT_RETURN(::atan(x));
     const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01,
                               9.82793723247329054082e-01, 1.57079632679489655800e+00};
     const double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17,
@@ -311,6 +329,7 @@ FKS_HD inline double atan(double x) {
 
 /* atan2 for finite arguments (the hot path never passes inf/nan) */
 FKS_HD inline double atan2(double y, double x) {
+    FKS_MATH_AUDIT_RETURN(::atan2(y, x));
     const double pi_o_2 = 1.5707963267948965580e+00, pi = 3.1415926535897931160e+00,
                  pi_lo = 1.2246467991473531772e-16;
     if (x != x || y != y) return x + y;

@@ -6,6 +6,7 @@ measured or shipped.  The product (fast_kinematic_simulator_amd) never imports i
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import subprocess
@@ -31,51 +32,75 @@ def lib():
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
             build()
-        from fast_kinematic_simulator_amd import _capi as C  # struct layouts only (the ABI types)
-
-        L = ctypes.CDLL(LIB_PATH)
-        L.oracle_forward_simulate.restype = c_int32
-        L.oracle_forward_simulate.argtypes = [
-            POINTER(C.Environment), POINTER(C.SolverParams), c_double, c_uint64, c_uint64, POINTER(C.RobotDesc),
-            POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_uint64, c_int32, c_int32, c_int32, POINTER(c_double),
-            POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32), POINTER(C.Statistics),
-            POINTER(C.CallCounters), c_int32, POINTER(c_double)]
-        L.oracle_check_config_collision.restype = c_int32
-        L.oracle_check_config_collision.argtypes = [
-            POINTER(C.Environment), POINTER(C.SolverParams), POINTER(C.RobotDesc), POINTER(c_double), c_uint64, c_double,
-            c_int32, POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint64)]
-        L.oracle_forward_simulate_traced.restype = c_int32
-        L.oracle_forward_simulate_traced.argtypes = [
-            POINTER(C.Environment), POINTER(C.SolverParams), c_double, c_uint64, c_uint64, POINTER(C.RobotDesc),
-            POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_int32, c_int32, POINTER(c_double), POINTER(c_uint8),
-            POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32), POINTER(C.Trace)]
-        L.oracle_philox4x32_10.restype = None
-        L.oracle_philox4x32_10.argtypes = [POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]
-        L.oracle_pid_sequence.restype = None
-        L.oracle_pid_sequence.argtypes = [c_double, c_double, c_double, c_double, POINTER(c_double), POINTER(c_double), c_int32,
-                                          POINTER(c_double)]
-        L.oracle_counter_truncated_normal.restype = c_double
-        L.oracle_counter_truncated_normal.argtypes = [c_uint64, c_uint64, c_uint64, c_uint32, c_uint32, c_uint32, POINTER(c_uint32)]
-        L.oracle_qr_solve.restype = None
-        L.oracle_qr_solve.argtypes = [POINTER(c_double), c_uint64, c_uint64, POINTER(c_double), POINTER(c_double)]
-        L.oracle_estimate_distance.restype = None
-        L.oracle_estimate_distance.argtypes = [POINTER(C.Environment), POINTER(c_double), c_uint64, POINTER(c_double),
-                                               POINTER(c_uint8), POINTER(ctypes.c_float)]
-        L.oracle_link_transforms.restype = c_int32
-        L.oracle_link_transforms.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), POINTER(c_double)]
-        L.oracle_apply_control_input.restype = c_int32
-        L.oracle_apply_control_input.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), POINTER(c_double), POINTER(c_double)]
-        L.oracle_point_jacobian.restype = c_int32
-        L.oracle_point_jacobian.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), c_int32, POINTER(c_double), POINTER(c_double)]
-        L.oracle_se3_exp.restype = None
-        L.oracle_se3_exp.argtypes = [POINTER(c_double), POINTER(c_double)]
-        L.oracle_se3_log.restype = None
-        L.oracle_se3_log.argtypes = [POINTER(c_double), POINTER(c_double)]
-        L.oracle_max_threads.restype = c_int32
-        L.oracle_portable_math.restype = None
-        L.oracle_portable_math.argtypes = [c_int32, POINTER(c_double), POINTER(c_double), c_uint64, POINTER(c_double)]
-        _LIB = L
+        _LIB = _load(LIB_PATH)
     return _LIB
+
+
+AUDIT_VARIANTS = ("v4seq", "seqsum", "libm", "fma")
+
+
+@contextlib.contextmanager
+def audit_variant(name):
+    """Run the oracle entry points on a restatement-audit build (oracle/Makefile `audit`,
+    DESIGN.md §2.3) inside the block.  Never a parity oracle."""
+    global _LIB
+    assert name in AUDIT_VARIANTS, name
+    path = os.path.join(HERE, "_build", "liboracle_%s.so" % name)
+    if not os.path.exists(path):
+        subprocess.run(["make", "-C", HERE, "audit"], check=True, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    saved = lib()
+    _LIB = _load(path)
+    try:
+        yield _LIB
+    finally:
+        _LIB = saved
+
+
+def _load(path):
+    from fast_kinematic_simulator_amd import _capi as C  # struct layouts only (the ABI types)
+
+    L = ctypes.CDLL(path)
+    L.oracle_forward_simulate.restype = c_int32
+    L.oracle_forward_simulate.argtypes = [
+        POINTER(C.Environment), POINTER(C.SolverParams), c_double, c_uint64, c_uint64, POINTER(C.RobotDesc),
+        POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_uint64, c_int32, c_int32, c_int32, POINTER(c_double),
+        POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32), POINTER(C.Statistics),
+        POINTER(C.CallCounters), c_int32, POINTER(c_double)]
+    L.oracle_check_config_collision.restype = c_int32
+    L.oracle_check_config_collision.argtypes = [
+        POINTER(C.Environment), POINTER(C.SolverParams), POINTER(C.RobotDesc), POINTER(c_double), c_uint64, c_double,
+        c_int32, POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint64)]
+    L.oracle_forward_simulate_traced.restype = c_int32
+    L.oracle_forward_simulate_traced.argtypes = [
+        POINTER(C.Environment), POINTER(C.SolverParams), c_double, c_uint64, c_uint64, POINTER(C.RobotDesc),
+        POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_int32, c_int32, POINTER(c_double), POINTER(c_uint8),
+        POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32), POINTER(C.Trace)]
+    L.oracle_philox4x32_10.restype = None
+    L.oracle_philox4x32_10.argtypes = [POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]
+    L.oracle_pid_sequence.restype = None
+    L.oracle_pid_sequence.argtypes = [c_double, c_double, c_double, c_double, POINTER(c_double), POINTER(c_double), c_int32,
+                                      POINTER(c_double)]
+    L.oracle_counter_truncated_normal.restype = c_double
+    L.oracle_counter_truncated_normal.argtypes = [c_uint64, c_uint64, c_uint64, c_uint32, c_uint32, c_uint32, POINTER(c_uint32)]
+    L.oracle_qr_solve.restype = None
+    L.oracle_qr_solve.argtypes = [POINTER(c_double), c_uint64, c_uint64, POINTER(c_double), POINTER(c_double)]
+    L.oracle_estimate_distance.restype = None
+    L.oracle_estimate_distance.argtypes = [POINTER(C.Environment), POINTER(c_double), c_uint64, POINTER(c_double),
+                                           POINTER(c_uint8), POINTER(ctypes.c_float)]
+    L.oracle_link_transforms.restype = c_int32
+    L.oracle_link_transforms.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), POINTER(c_double)]
+    L.oracle_apply_control_input.restype = c_int32
+    L.oracle_apply_control_input.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), POINTER(c_double), POINTER(c_double)]
+    L.oracle_point_jacobian.restype = c_int32
+    L.oracle_point_jacobian.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), c_int32, POINTER(c_double), POINTER(c_double)]
+    L.oracle_se3_exp.restype = None
+    L.oracle_se3_exp.argtypes = [POINTER(c_double), POINTER(c_double)]
+    L.oracle_se3_log.restype = None
+    L.oracle_se3_log.argtypes = [POINTER(c_double), POINTER(c_double)]
+    L.oracle_max_threads.restype = c_int32
+    L.oracle_portable_math.restype = None
+    L.oracle_portable_math.argtypes = [c_int32, POINTER(c_double), POINTER(c_double), c_uint64, POINTER(c_double)]
+    return L
 
 
 def _p(a, t):

@@ -135,7 +135,15 @@ inline V3 cross(const V3& a, const V3& b) {
     return c;
 }
 
+/* Eigen Vector4d squaredNorm (and norm, dot): the vectorised redux over two Packet2d
+ * lanes, (x + z) + (y + w) -- the reference's -O3 x86-64 (SSE2, no FMA) build
+ * (CMakeLists.txt:66).  ORACLE_AUDIT_V4_SEQUENTIAL is the restatement
+ * audit's alternative (tools/restatement_audit.py), never the parity oracle. */
+#ifdef ORACLE_AUDIT_V4_SEQUENTIAL
 inline double sqnorm4(const V4& v) { return ((v.x * v.x + v.y * v.y) + v.z * v.z) + v.w * v.w; }
+#else
+inline double sqnorm4(const V4& v) { return (v.x * v.x + v.z * v.z) + (v.y * v.y + v.w * v.w); }
+#endif
 inline double sqnorm3(const V3& v) { return (v.x * v.x + v.y * v.y) + v.z * v.z; }
 
 /* EigenHelpers::SafeNormal: v / norm if norm > DBL_EPSILON else v */

@@ -92,6 +92,11 @@ static inline bool trunc_index(double v, int64_t* out) {
  * kernel's 64-lane wavefront reduction (DPP within rows, readlane across rows) produces; it is the oracle's definition
  * of every long sum in the least-squares solve (DESIGN.md §Canonical sums). */
 static double canon_sum(const std::vector<double>& terms, size_t begin, size_t end) {
+#ifdef ORACLE_AUDIT_SEQUENTIAL_SUMS /* restatement audit alternative: ascending scalar sum */
+    double acc = 0.0;
+    for (size_t r = begin; r < end; ++r) acc = acc + terms[r];
+    return acc;
+#endif
     double partial[64];
     for (int l = 0; l < 64; ++l) partial[l] = 0.0;
     for (size_t r = begin; r < end; ++r) partial[r % 64] = partial[r % 64] + terms[r];
@@ -210,7 +215,13 @@ struct NormalGrid {
         double best_dot = -HUGE_VAL;
         for (uint32_t e = begin; e < end; ++e) {
             const double* ent = entries + 6 * (size_t)e;
+            /* EntryDirection4d().dot(unit_direction) SPCS:122 in Eigen's packet order; both
+             * w terms are +0 (SPCS:62 stores (entry, 0); the motion's w is 1 - 1) */
+#ifdef ORACLE_AUDIT_V4_SEQUENTIAL
             const double dot = (ent[0] * ux + ent[1] * uy) + ent[2] * uz;
+#else
+            const double dot = (ent[0] * ux + ent[2] * uz) + ent[1] * uy;
+#endif
             if (dot > best_dot) {
                 best_dot = dot;
                 best = (int64_t)e;
