@@ -248,14 +248,18 @@ __device__ __forceinline__ SampledDev load_sampled(const SampledDev* p, int d) {
     o.samples = g->samples;
     return o;
 }
-/* 64-bit lane moves: DPP within rows of 16, readlane across rows */
+/* 64-bit lane moves: DPP within rows of 16, readlane across rows.  Every control used
+ * (quad_perm, row_mirror, row_half_mirror) reads a valid lane for every lane, so the
+ * "old" operand is never selected and needs no zero-initialised register. */
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
+    static_assert(CTRL <= 0xFF || CTRL == 0x140 || CTRL == 0x141, "full-permutation DPP controls only");
     const uint64_t b = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
+__device__ __forceinline__ int readlane_i32(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
     const uint64_t b = (uint64_t)__double_as_longlong(v);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, lane);
@@ -395,6 +399,16 @@ __device__ double sampled_pick(uint32_t k0, uint32_t k1, uint64_t particle, uint
 #ifndef FKS_HOT_ATTR
 #define FKS_HOT_ATTR
 #endif
+
+/* Phase-cost profiling builds only (tools/phase_cost.sh): bit b of FKS_PROF_DUP runs
+ * phase b of the microstep / resolver loop a second time with identical inputs and
+ * outputs, so the difference of SQ_INSTS_* and kernel time against the plain build is
+ * that phase's cost.  0 (the product) compiles every repeat away. */
+#ifndef FKS_PROF_DUP
+#define FKS_PROF_DUP 0
+#endif
+enum { kDupFk = 0, kDupInput, kDupEnv, kDupSelf, kDupCorr, kDupSolve, kDupApply, kDupRefill, kDupEnvFull };
+constexpr int prof_reps(int bit) { return 1 + ((FKS_PROF_DUP >> bit) & 1); }
 
 struct Sim;
 __device__ void refill_noise(Sim& s, uint32_t micro0, uint32_t M);
@@ -637,8 +651,7 @@ __device__ void fk(Sim& s, const double* cfg, double* T) {
         /* 12-lane chain: lane 4r+c owns element (r, c) of the running transform; the
          * row a lane needs is broadcast inside its quad (DPP), so the chain never
          * goes through memory.  T_child = (T_parent * origin) * motion, each element
-         * the same dot3 as the oracle.  The next joint's origin / motion columns are
-         * loaded one joint ahead. */
+         * the same dot3 as the oracle. */
         const int r = ln >> 2, c = ln & 3;
         const bool act = ln < 12;
         double own = act ? s.base[4 * r + c] : 0.0;
@@ -647,28 +660,14 @@ __device__ void fk(Sim& s, const double* cfg, double* T) {
                p3 = dpp_f64<kDppQuadBcast3>(own);
         int last = 0;
         const int J = R.J;
-        double o0 = 0.0, o1 = 0.0, o2 = 0.0, m0 = 0.0, m1 = 0.0, m2 = 0.0;
-        if (J > 0) {
-            o0 = JD[0].origin[c];
-            o1 = JD[0].origin[4 + c];
-            o2 = JD[0].origin[8 + c];
-            m0 = jm[c];
-            m1 = jm[4 + c];
-            m2 = jm[8 + c];
-        }
+        /* the joint's origin / motion columns are read at the top of its iteration (no
+         * prefetch registers to rotate: the other waves of the SIMD hide the LDS latency) */
         for (int j = 0; j < J; ++j) {
             const int parent = __builtin_amdgcn_readfirstlane(JD[j].parent);
             const int child = __builtin_amdgcn_readfirstlane(JD[j].child);
             const int type = __builtin_amdgcn_readfirstlane(JD[j].type);
-            const double co0 = o0, co1 = o1, co2 = o2, cm0 = m0, cm1 = m1, cm2 = m2;
-            if (j + 1 < J) {
-                o0 = JD[j + 1].origin[c];
-                o1 = JD[j + 1].origin[4 + c];
-                o2 = JD[j + 1].origin[8 + c];
-                m0 = jm[12 * (j + 1) + c];
-                m1 = jm[12 * (j + 1) + 4 + c];
-                m2 = jm[12 * (j + 1) + 8 + c];
-            }
+            const double co0 = JD[j].origin[c], co1 = JD[j].origin[4 + c], co2 = JD[j].origin[8 + c];
+            const double cm0 = jm[12 * j + c], cm1 = jm[12 * j + 4 + c], cm2 = jm[12 * j + 8 + c];
             if (parent != last) {
                 const double* Tp = T + 12 * parent + 4 * (act ? r : 0);
                 p0 = Tp[0];
@@ -1099,10 +1098,21 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
  * colliding point; algorithmic bytes are counted up to that point, as the reference
  * reads them (its loop returns at the first colliding point).  Provably-free rounds
  * are not read but still counted (4 B per point, all in bounds). */
+template <bool FULL = false>
 __device__ FKS_HOT_ATTR bool env_collision(Sim& s, const double* T) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
-    const uint64_t skip = skippable_rounds(s, T, kSkipCheck);
+    const uint64_t skip = FULL ? 0ull : skippable_rounds(s, T, kSkipCheck);
+    /* every round proven free (the common microstep): the reference reads 4 bytes per
+     * point and finds nothing; account those reads without walking the rounds */
+    if (R.nrounds <= kWave) {
+        const uint64_t all = (R.nrounds == kWave) ? ~0ull : ((1ull << R.nrounds) - 1ull);
+        if ((skip & all) == all) {
+            if (s.lane < R.P) s.lane_bytes += 4ull * (uint64_t)((R.P - s.lane + kWave - 1) / kWave);
+            count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (uint64_t)R.nrounds);
+            return false;
+        }
+    }
     for (int base = 0, r = 0; base < R.P; base += 2 * kWave, r += 2) {
         const bool sk0 = r < kWave && ((skip >> r) & 1ull);
         const bool sk1 = r + 1 < kWave && ((skip >> (r + 1)) & 1ull);
@@ -1119,8 +1129,8 @@ __device__ FKS_HOT_ATTR bool env_collision(Sim& s, const double* T) {
             b1 = (i1 < R.P) ? 4 : 0;
         else
             c1 = env_point(A, T, i1, &b1, &S1, &G1, &C1);
-        if (!sk0) round_update(s, r, T, S0, G0, C0);
-        if (!sk1 && base + kWave < R.P) round_update(s, r + 1, T, S1, G1, C1);
+        if (!sk0 && !FULL) round_update(s, r, T, S0, G0, C0);
+        if (!sk1 && !FULL && base + kWave < R.P) round_update(s, r + 1, T, S1, G1, C1);
         count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (sk0 ? 1 : 0) + ((sk1 && base + kWave < R.P) ? 1 : 0));
         count_event(s, FKS_PHASE_ENV_ROUNDS_EVALUATED, (sk0 ? 0 : 1) + ((!sk1 && base + kWave < R.P) ? 1 : 0));
         const uint64_t m0 = __ballot(c0);
@@ -1410,13 +1420,16 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
     const SimArgs& A = *Ap;
     const RobotDev& R = A.R;
     const double* box = lds + A.L.box;
-    /* exact path: extended cell keys of every point (SPCS:1173-1181: division, trunc) */
+    /* exact path: extended cell keys (SPCS:1173-1181: division, trunc).  The keys are
+     * needed for the points of the geometries in a box-overlapping pair; every other
+     * point's key only matters once some cell is shared, so it is computed then. */
     const ScratchLayout& SL = A.SL;
     int64_t* keys = reinterpret_cast<int64_t*>(scratch + SL.keys);
     double* flag = scratch + SL.flag;
     double* cand = scratch + SL.cand;
     int32_t* list = reinterpret_cast<int32_t*>(scratch + SL.list);
-    for (int i = ln; i < R.P; i += kWave) {
+    int32_t* listb = list + R.P; /* second half of the list region: one pair's b points */
+    auto key_point = [&](int i) {
         const D4 p = load_point(R, i);
         const int link = gp(R.point_link)[i];
         const D4 x = xform4(Tc + 12 * link, p);
@@ -1438,22 +1451,90 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
         }
         flag[i] = 0.0;
         cand[i] = 0.0;
-    }
-    wsync();
-    /* exact candidate marking over pairs whose boxes overlap */
-    for (int k = 0; k < R.npairs; ++k) {
-        const int a = gp(R.pairs)[2 * k], b = gp(R.pairs)[2 * k + 1];
+    };
+    /* a point's key lies in geometry g's conservative cell box (self_collisions) */
+    auto in_box = [&](int i, int g) {
+        bool in = true;
+        for (int a = 0; a < 3; ++a) {
+            const double k = (double)keys[3 * i + a];
+            in = in && box[6 * g + a] <= k && k <= box[6 * g + 3 + a];
+        }
+        return in;
+    };
+    auto overlap = [&](int a, int b) {
         bool ov = true;
         for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
-        if (!ov) continue;
+        return ov;
+    };
+    /* geometries of the overlapping pairs; every geometry when a box is not finite (the
+     * key-range error is then raised exactly as a pass over all points would) */
+    const bool unbounded = wave_any(ln < R.G && !(box[6 * ln] > -__builtin_huge_val()));
+    uint64_t need = 0ull;
+    for (int k0 = 0; k0 < R.npairs; k0 += kWave) {
+        const int k = k0 + ln;
+        int a = 0, b = 0;
+        bool ov = false;
+        if (k < R.npairs) {
+            a = gp(R.pairs)[2 * k];
+            b = gp(R.pairs)[2 * k + 1];
+            ov = overlap(a, b);
+        }
+        uint64_t m = __ballot(ov);
+        while (m) {
+            const int bit = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1ull;
+            need |= (1ull << readlane_i32(a, bit)) | (1ull << readlane_i32(b, bit));
+        }
+    }
+    uint64_t done = 0ull;
+    for (int g = 0; g < R.G; ++g) {
+        if (!unbounded && !((need >> g) & 1ull)) continue;
+        done |= 1ull << g;
+        for (int i = (int)gp(R.geom_off)[g] + ln; i < (int)gp(R.geom_off)[g + 1]; i += kWave) key_point(i);
+    }
+    wsync();
+    /* exact candidate marking over pairs whose boxes overlap: a point of a can share a
+     * cell only with the points of b whose keys lie in a's box (and only if its own key
+     * lies in b's box), so b's points are first compacted to that list */
+    bool any_cand = false;
+    for (int k = 0; k < R.npairs; ++k) {
+        const int a = gp(R.pairs)[2 * k], b = gp(R.pairs)[2 * k + 1];
+        if (!overlap(a, b)) continue;
         const int a0 = (int)gp(R.geom_off)[a], a1 = (int)gp(R.geom_off)[a + 1];
         const int b0 = (int)gp(R.geom_off)[b], b1 = (int)gp(R.geom_off)[b + 1];
+        int nb = 0;
+        for (int j0 = b0; j0 < b1; j0 += kWave) {
+            const int j = j0 + ln;
+            const bool in = j < b1 && in_box(j, a);
+            const uint64_t mm = __ballot(in);
+            if (in) listb[nb + __popcll(mm & ((1ull << ln) - 1ull))] = j;
+            nb += __popcll(mm);
+        }
+        if (nb == 0) continue;
+        wsync();
         for (int i = a0 + ln; i < a1; i += kWave) {
+            if (!in_box(i, b)) continue;
             const int64_t kx = keys[3 * i], ky = keys[3 * i + 1], kz = keys[3 * i + 2];
             bool hit = false;
-            for (int j = b0; j < b1 && !hit; ++j) hit = (keys[3 * j] == kx) && (keys[3 * j + 1] == ky) && (keys[3 * j + 2] == kz);
-            if (hit) cand[i] = 1.0;
+            for (int t = 0; t < nb && !hit; ++t) {
+                const int j = listb[t];
+                hit = (keys[3 * j] == kx) && (keys[3 * j + 1] == ky) && (keys[3 * j + 2] == kz);
+            }
+            if (hit) {
+                cand[i] = 1.0;
+                any_cand = true;
+            }
         }
+        wsync();
+    }
+    if (!wave_any(any_cand)) {
+        err = wave_or(err);
+        return err << 1;
+    }
+    /* some cell is shared: the cell members below come from every point */
+    for (int g = 0; g < R.G; ++g) {
+        if ((done >> g) & 1ull) continue;
+        for (int i = (int)gp(R.geom_off)[g] + ln; i < (int)gp(R.geom_off)[g + 1]; i += kWave) key_point(i);
     }
     wsync();
     /* process each candidate cell once */
@@ -1502,12 +1583,14 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
 template <int RT>
 __device__ bool check_collision(Sim& s, const double* Tp, const double* Tc) {
     uint64_t t0 = tick();
-    const bool env = env_collision(s, Tc);
+    bool env = env_collision(s, Tc);
+    for (int k = 1; k < prof_reps(kDupEnv); ++k) env = env_collision(s, Tc);
+    for (int k = 1; k < prof_reps(kDupEnvFull); ++k) env = env_collision<true>(s, Tc) || env;
     tock(s, FKS_PHASE_ENV_CHECK, t0);
     bool self = false;
     if constexpr (RT == FKS_ROBOT_LINKED) {
         t0 = tick();
-        self = self_collisions(s, Tp, Tc);
+        for (int k = 0; k < prof_reps(kDupSelf); ++k) self = self_collisions(s, Tp, Tc);
         tock(s, FKS_PHASE_SELF_CHECK, t0);
     }
     s.self_nonempty = self;
@@ -1917,7 +2000,11 @@ __device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double
     const double threshold_helper = maxsq * (eps * eps) / (double)Rn;
     const int size = ((int)Rn < D) ? (int)Rn : D;
     int nz = size;
-    for (int k = 0; k < size; ++k) {
+    /* k is a compile-time constant in every unrolled step: the row selections below
+     * fold to plain register reads instead of RM-way selects */
+#pragma unroll
+    for (int k = 0; k < RM; ++k) {
+        if (k >= size) break;
         const int biggest = wave_first_argmax(cs, ln, k, D);
         double bsq;
         {
@@ -2017,7 +2104,9 @@ __device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double
     double bu[RM];
 #pragma unroll
     for (int r = 0; r < RM; ++r) bu[r] = ((uint32_t)r < Rn) ? readlane_f64(a[r], D) : 0.0;
-    for (int ii = nz - 1; ii >= 0; --ii) {
+#pragma unroll
+    for (int ii = RM - 1; ii >= 0; --ii) {
+        if (ii >= nz) continue;
         double ci = 0.0;
 #pragma unroll
         for (int r = 0; r < RM; ++r)
@@ -2320,8 +2409,9 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
         }
         wsync();
         t0 = tick();
-        if (micro % (uint32_t)(kWave / R.D) == 0u) refill_noise(s, micro, M);
-        apply_input<RT>(s, cfg_prev, ustep, cfg, true, micro);
+        if (micro % (uint32_t)(kWave / R.D) == 0u)
+            for (int k = 0; k < prof_reps(kDupRefill); ++k) refill_noise(s, micro, M);
+        for (int k = 0; k < prof_reps(kDupInput); ++k) apply_input<RT>(s, cfg_prev, ustep, cfg, true, micro);
         s.err = wave_or(s.err);
         tock(s, FKS_PHASE_MICRO_INPUT, t0);
         if (s.err) {
@@ -2330,7 +2420,7 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
             return 1;
         }
         t0 = tick();
-        fk<RT>(s, cfg, Tcur);
+        for (int k = 0; k < prof_reps(kDupFk); ++k) fk<RT>(s, cfg, Tcur);
         tock(s, FKS_PHASE_MICRO_FK, t0);
         bool in_collision = check_collision<RT>(s, Tprev, Tcur);
         if (s.err) return 1;
@@ -2344,12 +2434,14 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
             while (in_collision) {
                 s.resolver_count++;
                 t0 = tick();
-                const uint32_t Rn = collect_corrections<RT>(s, Tprev, Tcur, cfg_act);
+                uint32_t Rn = collect_corrections<RT>(s, Tprev, Tcur, cfg_act);
+                for (int k = 1; k < prof_reps(kDupCorr); ++k) Rn = collect_corrections<RT>(s, Tprev, Tcur, cfg_act);
                 s.lsq_rows += Rn;
                 s.err = wave_or(s.err);
                 tock(s, FKS_PHASE_CORRECTIONS, t0);
                 if (s.err) return 1;
                 t0 = tick();
+                for (int k = 0; k < prof_reps(kDupSolve); ++k)
                 if (IND || (TR && A.individual_jacobians)) {
                     individual_jacobians_solve(s, Rn, x);
                 } else if (Rn <= 8u && R.D < kWave)
@@ -2360,13 +2452,16 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
                     qr_solve_regs<8>(s.A, s.lds, s.scratch, ln, Rn, x);
                 else if (RT == FKS_ROBOT_LINKED && Rn <= (uint32_t)kWave && R.D <= 16)
                     qr_solve_regs<RT == FKS_ROBOT_LINKED ? 16 : 8>(s.A, s.lds, s.scratch, ln, Rn, x);
-                else
+                else if (k == 0) /* factors in place: never repeated */
                     qr_solve(s.A, s.lds, s.scratch, ln, Rn, x);
                 tock(s, FKS_PHASE_SOLVE, t0);
                 t0 = tick();
-                apply_input<RT>(s, cfg_act, x, cfg_tmp, false, 0);
-                fk<RT>(s, cfg_tmp, Ttmp);
-                const double est = max_point_motion(s, Tcur, Ttmp);
+                double est = 0.0;
+                for (int k = 0; k < prof_reps(kDupApply); ++k) {
+                    apply_input<RT>(s, cfg_act, x, cfg_tmp, false, 0);
+                    fk<RT>(s, cfg_tmp, Ttmp);
+                    est = max_point_motion(s, Tcur, Ttmp);
+                }
                 const double step_fraction = dmax(est / A.allowed_micro, 1.0);
                 if (step_fraction == 1.0 && dabs(scaling) == 1.0) {
                     /* real_correction_step = (x / 1) * 1 == x bit for bit (SPCS:1681-1682): the
