@@ -21,6 +21,9 @@ from fast_kinematic_simulator_amd import workloads as W  # noqa: E402
 from fast_kinematic_simulator_amd.simulator import make_linked_simulator  # noqa: E402
 
 
+COUNTS = ("env_rounds_skipped", "env_rounds_evaluated", "corr_rounds_skipped", "corr_rounds_evaluated")
+
+
 def run(sim, wl, starts, first_id, dev):
     n = starts.shape[0]
     d_starts = torch.from_numpy(np.ascontiguousarray(starts)).to(dev)
@@ -49,8 +52,9 @@ def main():
     run(sim, wl, wl.starts[:256], 0, dev)
     m, it, kms, ph = run(sim, wl, wl.starts, 0, dev)
     out = {"workload": a.workload, "batch_kernel_ms": kms, "particles": int(m.size), "alone": [],
-           "batch_phase_share": ({k: round(v / max(1, ph.get("particle", 0)), 4) for k, v in ph.items()}
-                                 if ph.get("control", 0) > 0 else None)}
+           "batch_phase_share": ({k: round(v / max(1, ph.get("particle", 0)), 4) for k, v in ph.items() if k not in COUNTS}
+                                 if ph.get("control", 0) > 0 else None),
+           "batch_phase_counts": {k: ph[k] for k in COUNTS if k in ph}}
     for i in np.argsort(-it)[:a.top]:
         i = int(i)
         m1, it1, k1, ph1 = run(sim, wl, wl.starts[i:i + 1], i, dev)
@@ -58,7 +62,9 @@ def main():
         out["alone"].append({"particle": i, "microsteps": int(m1[0]), "resolver_iterations": int(it1[0]), "kernel_ms": k1,
                              "same_as_in_batch": bool(m1[0] == m[i] and it1[0] == it[i]),
                              "us_per_resolver_iteration_upper": 1e3 * k1 / max(int(it1[0]), 1),
-                             "phase_share": ({k: round(v / tot, 4) for k, v in ph1.items()} if ph1.get("control", 0) > 0 else None)})
+                             "phase_share": ({k: round(v / tot, 4) for k, v in ph1.items() if k not in COUNTS}
+                                             if ph1.get("control", 0) > 0 else None),
+                             "phase_counts": {k: ph1[k] for k in COUNTS if k in ph1}})
     print(json.dumps(out, indent=1))
     if a.json:
         with open(a.json, "w") as f:
