@@ -146,9 +146,14 @@ def main():
     for label, pat in (("microstep loop", "refill_noise_lanes"), ("resolver loop", "qr_solve_cols")):
         h, body = loop_with(pat)
         if h is None:
-            print(label, "not found")
+            print(label, "not found (callee inlined?)")
             continue
         print(f"{label}: header {blocks[h][0]}, {len(body)} blocks", census(lines, blocks, body))
+    # the largest loops whatever they call: with everything inlined the hot loops are
+    # the few nests of several hundred blocks
+    print("largest loops:")
+    for size, h in sorted(((len(b), h) for h, b in loops.items()), reverse=True)[:6]:
+        print(f"  header {blocks[h][0]}, {size} blocks", census(lines, blocks, loops[h]))
 
 
 if __name__ == "__main__":
