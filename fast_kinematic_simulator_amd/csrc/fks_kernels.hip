@@ -458,6 +458,15 @@ struct Sim {
     uint32_t tr_steps, tr_cfgs; /* trace records produced so far (traced kernels) */
 };
 
+/* The lane index made opaque to the optimiser at the head of the microstep and
+ * resolver loops: the per-lane LDS / workspace addresses derived from it are then
+ * recomputed inside the loop instead of being hoisted out of it into VGPRs that stay
+ * live across the whole loop nest. */
+__device__ __forceinline__ int opaque_lane(int ln) {
+    asm volatile("" : "+v"(ln));
+    return ln;
+}
+
 /* wave totals of the self-collision branch (kCntSelfChecks, kCntSelfPoints), kept in the
  * wave's LDS block (misc + 28, + 29) rather than in registers: the branch is rare */
 __device__ __forceinline__ uint64_t* self_counters(const Sim& s) { return reinterpret_cast<uint64_t*>(s.lds + s.A->L.misc + 28); }
@@ -2400,6 +2409,8 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
     trace_step<TR>(s, u, ustep, M);
     bool collided = false;
     for (uint32_t micro = 0; micro < M; ++micro) {
+        s.lane = opaque_lane(s.lane);
+        const int ln = s.lane;
         s.micro_count++;
         if (ln < W) cfg_prev[ln] = cfg[ln];
         {
@@ -2432,6 +2443,8 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
             uint32_t iters = 0;
             double scaling = A.S.resolve_correction_initial_step_size;
             while (in_collision) {
+                s.lane = opaque_lane(s.lane);
+                const int ln = s.lane;
                 s.resolver_count++;
                 t0 = tick();
                 uint32_t Rn = collect_corrections<RT>(s, Tprev, Tcur, cfg_act);
