@@ -2992,6 +2992,8 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         bool ended = false;
         /* ForwardSimulateMutableRobot (SPCS:843-919) */
         for (uint32_t step = step_begin; step < step_end; ++step) {
+            s.lane = opaque_lane(s.lane);
+            const int ln = s.lane;
             s.step = step;
             s.step_count++;
             double* tgt_lds = s.lds + s.A->L.tgt;
