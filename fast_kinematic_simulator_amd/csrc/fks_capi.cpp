@@ -245,6 +245,7 @@ struct fks_context {
     uint32_t heavy_per_step = kHeavyResolverPerStep; /* fks_set_segment_policy */
     uint32_t heavy_priority = 1;
     int32_t individual_jacobians = 0; /* fks_set_individual_jacobians (SPCS:420-423) */
+    bool fk_pair = false;             /* paired FK of free microsteps (fks_set_robot) */
     double* d_seg_state = nullptr;
     uint32_t* d_seg_done = nullptr;
     size_t cap_seg_state = 0, cap_seg_done = 0;
@@ -756,7 +757,19 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
         R.sampled = dsd;
     }
     /* launch geometry: one wave per workgroup, as many resident waves as fit */
-    const fksd::LdsLayout L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds);
+    fksd::LdsLayout L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds);
+    /* the paired FK of free microsteps (linked chains of <= 32 joints) needs a second set
+     * of joint motion matrices per wave: taken only when it costs no workgroup per CU */
+    ctx->fk_pair = false;
+    if (R.type == FKS_ROBOT_LINKED && R.J >= 1 && R.J <= 32) {
+        const fksd::LdsLayout Lp = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, true);
+        const size_t g0 = (160 * 1024) / (((size_t)L.shared_total + (size_t)fksd::kWavesPerGroup * L.total) * sizeof(double));
+        const size_t g1 = (160 * 1024) / (((size_t)Lp.shared_total + (size_t)fksd::kWavesPerGroup * Lp.total) * sizeof(double));
+        if (g1 >= 1 && g1 >= std::min<size_t>(g0, 5)) {
+            L = Lp;
+            ctx->fk_pair = true;
+        }
+    }
     /* four waves share one LDS copy of the robot tables; robots whose per-wave blocks do
      * not fit four times in the CU's 160 KiB run two or one wave per workgroup (the
      * largest robot the descriptor admits, 64 links / dofs / geometries, fits at one) */
@@ -927,7 +940,7 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     /* controller-step segments: automatically only when the batch outnumbers the
      * resident waves (otherwise every particle has a wave from the start), always
@@ -1043,7 +1056,7 @@ fks_status fks_check_config_collision_device(fks_context* ctx, const double* d_c
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     *ctx->h_args = a;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice, s));
@@ -1326,7 +1339,7 @@ fks_status fks_kinematics(fks_context* ctx, int32_t mode, const double* configs,
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     a.kin_mode = mode;
     a.kin_out = d_out;

@@ -108,14 +108,15 @@ constexpr int kWavesPerGroup = 4;
 struct LdsLayout {
     uint32_t joints, ctrl, base, dofj, gbox, gpairs, rounds, shared_total;
     uint32_t rstate, noise, noise_err, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u,
-        ustep, x, real, axis_w, orig_w, colsq, hcoef, box, misc, ints, total;
+        ustep, x, real, axis_w, orig_w, colsq, hcoef, box, misc, ints, jm2, total;
+    uint32_t fk_pair; /* 1: the free-motion microsteps pair their FK chains (jm2 allocated) */
 };
 
 inline
 #if defined(__HIPCC__)
     __host__ __device__
 #endif
-    LdsLayout make_lds_layout(int L, int J, int D, int W, int G, int NR) {
+    LdsLayout make_lds_layout(int L, int J, int D, int W, int G, int NR, bool fk_pair = false) {
     LdsLayout l;
     uint32_t o = 0;
     /* shared: the robot tables the hot loops read (filled once per workgroup) */
@@ -189,6 +190,10 @@ inline
     o += 32;
     l.ints = o; /* int32 region: perm[64], transpositions[64], 16 spare words */
     o += (2 * kMaxDofs + 16) / 2;
+    /* the second FK chain's joint motion matrices (paired FK of the next free microstep) */
+    l.fk_pair = fk_pair ? 1u : 0u;
+    l.jm2 = o;
+    if (fk_pair) o += 12u * (uint32_t)(J > 0 ? J : 1);
     o = (o + 1u) & ~1u; /* 16-byte alignment */
     l.total = o;
     return l;

@@ -715,6 +715,82 @@ __device__ void fk(Sim& s, const double* cfg, double* T) {
     }
 }
 
+/* FK of two configurations of a linked robot in one pass (J <= 32): the chain of cfgA
+ * runs on lanes 0-11 and the chain of cfgB on lanes 16-27 (quads 0-2 and 4-6), their
+ * joint motion matrices on lanes j and 32 + j.  Every instruction of the chain serves
+ * both, so the pair costs about one FK; each chain is the same arithmetic as fk(). */
+__device__ void fk_pair(Sim& s, const double* cfgA, double* TA, const double* cfgB, double* TB) {
+    const RobotDev& R = s.A->R;
+    const int ln = s.lane;
+    double* jmA = s.lds + s.A->L.jm;
+    double* jmB = s.lds + s.A->L.jm2;
+    const JointDev* JD = s.joints;
+    {
+        const int j = ln & 31;
+        const bool second = ln >= 32;
+        if (j < R.J) {
+            const JointDev& jd = JD[j];
+            const double* cfg = second ? cfgB : cfgA;
+            double* jm = second ? jmB : jmA;
+            if (jd.type == FKS_JOINT_REVOLUTE || jd.type == FKS_JOINT_CONTINUOUS) {
+                double M[12];
+                angle_axis34(cfg[jd.dof], jd.axis[0], jd.axis[1], jd.axis[2], M);
+                M[3] = 0.0;
+                M[7] = 0.0;
+                M[11] = 0.0;
+                for (int e = 0; e < 12; ++e) jm[12 * j + e] = M[e];
+            } else if (jd.type == FKS_JOINT_PRISMATIC) {
+                const double v = cfg[jd.dof];
+                const double M[12] = {1.0, 0.0, 0.0, jd.axis[0] * v, 0.0, 1.0, 0.0, jd.axis[1] * v, 0.0, 0.0, 1.0, jd.axis[2] * v};
+                for (int e = 0; e < 12; ++e) jm[12 * j + e] = M[e];
+            }
+        }
+    }
+    wsync();
+    const int local = ln & 15;
+    const bool chainB = (ln & 16) != 0;
+    const int r = local >> 2, c = local & 3;
+    const bool act = local < 12 && ln < 32;
+    double* T = chainB ? TB : TA;
+    const double* jm = chainB ? jmB : jmA;
+    double own = act ? s.base[4 * r + c] : 0.0;
+    if (act) T[4 * r + c] = own;
+    double p0 = dpp_f64<kDppQuadBcast0>(own), p1 = dpp_f64<kDppQuadBcast1>(own), p2 = dpp_f64<kDppQuadBcast2>(own),
+           p3 = dpp_f64<kDppQuadBcast3>(own);
+    int last = 0;
+    const int J = R.J;
+    for (int j = 0; j < J; ++j) {
+        const int parent = __builtin_amdgcn_readfirstlane(JD[j].parent);
+        const int child = __builtin_amdgcn_readfirstlane(JD[j].child);
+        const int type = __builtin_amdgcn_readfirstlane(JD[j].type);
+        const double co0 = JD[j].origin[c], co1 = JD[j].origin[4 + c], co2 = JD[j].origin[8 + c];
+        const double cm0 = jm[12 * j + c], cm1 = jm[12 * j + 4 + c], cm2 = jm[12 * j + 8 + c];
+        if (parent != last) {
+            const double* Tp = T + 12 * parent + 4 * (act ? r : 0);
+            p0 = Tp[0];
+            p1 = Tp[1];
+            p2 = Tp[2];
+            p3 = Tp[3];
+        }
+        double a = dot3(p0, p1, p2, co0, co1, co2);
+        if (c == 3) a = a + p3;
+        double out = a;
+        if (type != FKS_JOINT_FIXED) {
+            const double a0 = dpp_f64<kDppQuadBcast0>(a), a1 = dpp_f64<kDppQuadBcast1>(a),
+                         a2 = dpp_f64<kDppQuadBcast2>(a), a3 = dpp_f64<kDppQuadBcast3>(a);
+            out = dot3(a0, a1, a2, cm0, cm1, cm2);
+            if (c == 3) out = out + a3;
+        }
+        if (act) T[12 * child + 4 * r + c] = out;
+        p0 = dpp_f64<kDppQuadBcast0>(out);
+        p1 = dpp_f64<kDppQuadBcast1>(out);
+        p2 = dpp_f64<kDppQuadBcast2>(out);
+        p3 = dpp_f64<kDppQuadBcast3>(out);
+        last = child;
+    }
+    wsync();
+}
+
 /* noisy actuator of dof `dof` on its clamped command `real` (TNUVA:568-596):
  * TruncatedNormalUncertainVelocityActuator (UNC:77-90), or the sampled one
  * (UNC:270-279: first matching bin, then the picked sample) */
@@ -2363,7 +2439,15 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
     double* cfg_act = s.lds + s.A->L.cfg_act;
     double* x = s.lds + s.A->L.x;
     double* real = s.lds + s.A->L.real;
-    double* Ttmp = s.lds + s.A->L.Ttmp;
+    /* the trial transforms live in whichever of the three transform buffers is neither
+     * Tcur nor Tprev (the paired FK below rotates all three) */
+    double* Ttmp;
+    {
+        double* b0 = s.lds + s.A->L.Tcur;
+        double* b1 = s.lds + s.A->L.Tprev;
+        double* b2 = s.lds + s.A->L.Ttmp;
+        Ttmp = (b0 != Tcur && b0 != Tprev) ? b0 : ((b1 != Tcur && b1 != Tprev) ? b1 : b2);
+    }
     double* cfg = s.lds + s.A->L.cfg_work; /* robot(immutable_robot->Clone()) SPCS:1548 */
     *out_collided = false;
     *out_failed = false;
@@ -2408,16 +2492,19 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
     tock(s, FKS_PHASE_STEP_SETUP, t0);
     trace_step<TR>(s, u, ustep, M);
     bool collided = false;
+    /* Paired FK (linked robots, A.L.fk_pair): while a microstep runs its FK, the chain's
+     * idle lanes compute the FK of the NEXT microstep's configuration as it will be if
+     * this one ends without contact (apply_input with the next noise sample, already in
+     * the noise buffer); the next microstep uses those transforms when its configuration
+     * equals that one bit for bit, and runs its own FK otherwise.  Results are unchanged;
+     * the FK instructions per free microstep halve. */
+    const uint32_t noise_per = (uint32_t)(kWave / R.D);
+    bool pair_ready = false; /* Ttmp holds FK(cfg_tmp), cfg_tmp = the predicted configuration */
     for (uint32_t micro = 0; micro < M; ++micro) {
         s.lane = opaque_lane(s.lane);
         const int ln = s.lane;
         s.micro_count++;
         if (ln < W) cfg_prev[ln] = cfg[ln];
-        {
-            double* t = Tprev;
-            Tprev = Tcur;
-            Tcur = t;
-        }
         wsync();
         t0 = tick();
         if (micro % (uint32_t)(kWave / R.D) == 0u)
@@ -2431,10 +2518,45 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
             return 1;
         }
         t0 = tick();
-        for (int k = 0; k < prof_reps(kDupFk); ++k) fk<RT>(s, cfg, Tcur);
+        bool predicted = false;
+        if (pair_ready) {
+            const bool same = ln >= W || __double_as_longlong(cfg[ln]) == __double_as_longlong(cfg_tmp[ln]);
+            predicted = !wave_any(!same);
+        }
+        if (predicted) {
+            /* this microstep's transforms were computed with the previous one's */
+            double* t = Tprev;
+            Tprev = Tcur;
+            Tcur = Ttmp;
+            Ttmp = t;
+            pair_ready = false;
+        } else {
+            {
+                double* t = Tprev;
+                Tprev = Tcur;
+                Tcur = t;
+            }
+            pair_ready = false;
+            bool pair = false;
+            if constexpr (RT == FKS_ROBOT_LINKED) {
+                pair = A.L.fk_pair && micro + 1u < M && ((micro + 1u) % noise_per) != 0u;
+                if (pair) {
+                    /* the next microstep's configuration if this one ends free of contact;
+                     * its error bits are the next microstep's, not this one's */
+                    const uint32_t err_keep = s.err;
+                    apply_input<RT>(s, cfg, ustep, cfg_tmp, true, micro + 1u);
+                    s.err = err_keep;
+                    for (int k = 0; k < prof_reps(kDupFk); ++k) fk_pair(s, cfg, Tcur, cfg_tmp, Ttmp);
+                    pair_ready = true;
+                }
+            }
+            if (!pair)
+                for (int k = 0; k < prof_reps(kDupFk); ++k) fk<RT>(s, cfg, Tcur);
+        }
         tock(s, FKS_PHASE_MICRO_FK, t0);
         bool in_collision = check_collision<RT>(s, Tprev, Tcur);
         if (s.err) return 1;
+        if (in_collision) pair_ready = false; /* the resolver reuses cfg_tmp / Ttmp */
         trace_config<TR>(s, cfg, micro, FKS_TRACE_POST_ACTION);
         if (in_collision) collided = true;
         if (in_collision && allow_contacts) {
