@@ -2495,11 +2495,14 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
     /* Paired FK (linked robots, A.L.fk_pair): while a microstep runs its FK, the chain's
      * idle lanes compute the FK of the NEXT microstep's configuration as it will be if
      * this one ends without contact (apply_input with the next noise sample, already in
-     * the noise buffer); the next microstep uses those transforms when its configuration
-     * equals that one bit for bit, and runs its own FK otherwise.  Results are unchanged;
-     * the FK instructions per free microstep halve. */
+     * the noise buffer).  If this microstep ends without contact, the next one's
+     * apply_input would see exactly those inputs, so it takes that configuration, its
+     * actuator error bits and those transforms instead of recomputing them; after a
+     * contact the prediction is dropped (the resolver reuses cfg_tmp / Ttmp).  Results are
+     * unchanged; free microsteps pay about half an FK and half an apply_input each. */
     const uint32_t noise_per = (uint32_t)(kWave / R.D);
     bool pair_ready = false; /* Ttmp holds FK(cfg_tmp), cfg_tmp = the predicted configuration */
+    uint32_t pair_err = 0;   /* the predicted configuration's actuator error bits (per lane) */
     for (uint32_t micro = 0; micro < M; ++micro) {
         s.lane = opaque_lane(s.lane);
         const int ln = s.lane;
@@ -2507,9 +2510,18 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
         if (ln < W) cfg_prev[ln] = cfg[ln];
         wsync();
         t0 = tick();
-        if (micro % (uint32_t)(kWave / R.D) == 0u)
-            for (int k = 0; k < prof_reps(kDupRefill); ++k) refill_noise(s, micro, M);
-        for (int k = 0; k < prof_reps(kDupInput); ++k) apply_input<RT>(s, cfg_prev, ustep, cfg, true, micro);
+        /* a predicted microstep (the previous one ended free of contact) takes the
+         * configuration apply_input produced for it then: the same inputs, so the same bits */
+        const bool predicted = pair_ready;
+        if (predicted) {
+            if (ln < W) cfg[ln] = cfg_tmp[ln];
+            s.err |= pair_err;
+            wsync();
+        } else {
+            if (micro % (uint32_t)(kWave / R.D) == 0u)
+                for (int k = 0; k < prof_reps(kDupRefill); ++k) refill_noise(s, micro, M);
+            for (int k = 0; k < prof_reps(kDupInput); ++k) apply_input<RT>(s, cfg_prev, ustep, cfg, true, micro);
+        }
         s.err = wave_or(s.err);
         tock(s, FKS_PHASE_MICRO_INPUT, t0);
         if (s.err) {
@@ -2518,11 +2530,6 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
             return 1;
         }
         t0 = tick();
-        bool predicted = false;
-        if (pair_ready) {
-            const bool same = ln >= W || __double_as_longlong(cfg[ln]) == __double_as_longlong(cfg_tmp[ln]);
-            predicted = !wave_any(!same);
-        }
         if (predicted) {
             /* this microstep's transforms were computed with the previous one's */
             double* t = Tprev;
@@ -2545,6 +2552,7 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
                      * its error bits are the next microstep's, not this one's */
                     const uint32_t err_keep = s.err;
                     apply_input<RT>(s, cfg, ustep, cfg_tmp, true, micro + 1u);
+                    pair_err = s.err; /* err_keep is 0 here: errors end the step above */
                     s.err = err_keep;
                     for (int k = 0; k < prof_reps(kDupFk); ++k) fk_pair(s, cfg, Tcur, cfg_tmp, Ttmp);
                     pair_ready = true;
