@@ -30,6 +30,7 @@ extern "C" __global__ void fks_simulate_linked(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se2(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se3(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_indiv(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_linked_jp(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se2_indiv(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se3_indiv(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_traced(const fksd::SimArgs* args);
@@ -213,6 +214,7 @@ struct fks_context {
     std::vector<void*> robot_allocs;
     /* launch resources */
     double* d_scratch = nullptr;
+    size_t cap_scratch = 0; /* doubles allocated at d_scratch */
     uint64_t scratch_per_wave = 0;
     uint32_t grid_waves = 0;
     uint32_t grid_groups = 0;
@@ -246,6 +248,8 @@ struct fks_context {
     uint32_t heavy_priority = 1;
     int32_t individual_jacobians = 0; /* fks_set_individual_jacobians (SPCS:420-423) */
     bool fk_pair = false;             /* paired FK of free microsteps (fks_set_robot) */
+    bool jp_layout = false;           /* LDS holds the joint-space proof's anchor and slack (fks_set_robot) */
+    int32_t joint_proof = 0;          /* fks_set_joint_proof (off by default: DESIGN.md §4.3) */
     double* d_seg_state = nullptr;
     uint32_t* d_seg_done = nullptr;
     size_t cap_seg_state = 0, cap_seg_done = 0;
@@ -279,6 +283,7 @@ static void free_robot(fks_context* ctx) {
     ctx->robot_allocs.clear();
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     ctx->d_scratch = nullptr;
+    ctx->cap_scratch = 0;
     ctx->has_robot = false;
 }
 
@@ -467,6 +472,99 @@ void fks_destroy(fks_context* ctx) {
 const char* fks_get_last_error(const fks_context* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
 
 int32_t fks_config_width(const fks_context* ctx) { return (ctx && ctx->has_robot) ? ctx->R.W : 0; }
+
+/* Launch geometry of the current robot: the LDS layout (the paired FK's second set of
+ * joint motion matrices, linked chains of <= 32 joints; the joint-space proof's anchor,
+ * slack and box regions when fks_set_joint_proof is on), workgroup size, resident
+ * workgroups per CU and the per-wave workspace.  Either extra region is taken only when
+ * the occupancy it leaves equals the plain layout's. */
+static hipError_t launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
+    const int P = R.P, G = R.G;
+    auto blocks = [&](const fksd::LdsLayout& l, uint32_t* wpg, size_t* bytes) -> int {
+        uint32_t w = fksd::kWavesPerGroup;
+        size_t b = 0;
+        for (;;) {
+            b = ((size_t)l.shared_total + (size_t)w * l.total) * sizeof(double);
+            if (b <= 160 * 1024 || w == 1) break;
+            w /= 2;
+        }
+        *wpg = w;
+        *bytes = b;
+        if (b > 160 * 1024) return 0;
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kernel_for(R.type)), 64 * (int)w, b) !=
+            hipSuccess)
+            return 0;
+        return n * (int)w; /* resident waves per CU */
+    };
+    uint32_t wpg = 0;
+    size_t bytes = 0;
+    const bool linked_pairable = R.type == FKS_ROBOT_LINKED && R.J >= 1 && R.J <= 32;
+    const bool jp_want = R.jp_ok && ctx->joint_proof;
+    fksd::LdsLayout L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds);
+    const int w0 = blocks(L, &wpg, &bytes);
+    /* the paired FK: when it keeps the plain layout's occupancy */
+    bool pair = false, jp = false;
+    size_t base_bytes = bytes;
+    if (linked_pairable && w0 > 0) {
+        uint32_t w = 0;
+        size_t b = 0;
+        if (blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, true), &w, &b) >= w0) {
+            pair = true;
+            base_bytes = b;
+        }
+    }
+    /* the joint-space proof: only in no more LDS than the layout above plus its anchor and
+     * slack (measured: a layout the occupancy query admits at 5 workgroups per CU but 1.3 KB
+     * larger ran the fifth workgroup late), with the paired FK if that fits, else without */
+    if (jp_want && w0 > 0) {
+        const size_t allow = base_bytes + (size_t)fksd::kWavesPerGroup * (size_t)(R.D + R.L + 2) * sizeof(double);
+        for (int v = 0; v < 2 && !jp; ++v) {
+            const bool tp = pair && v == 0;
+            if (v == 1 && !pair) break;
+            uint32_t w = 0;
+            size_t b = 0;
+            if (blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, tp, true), &w, &b) >= w0 && b <= allow) {
+                jp = true;
+                pair = tp;
+            }
+        }
+    }
+    L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, pair, jp);
+    const int waves_per_cu = blocks(L, &wpg, &bytes);
+    ctx->fk_pair = pair;
+    ctx->jp_layout = jp;
+    ctx->waves_per_group = wpg;
+    ctx->lds_bytes = bytes;
+    if (waves_per_cu < 1) return hipErrorInvalidValue;
+    int cus = 0;
+    hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    if (e != hipSuccess) return e;
+    ctx->grid_groups = (uint32_t)(cus * (waves_per_cu / (int)wpg));
+    ctx->grid_waves = ctx->grid_groups * ctx->waves_per_group;
+    ctx->scratch_per_wave = fksd::make_scratch_layout(3u * P, R.D, (int)P, G).total;
+    /* the per-wave workspace grows with 3P x D (the stacked Jacobian) and the robot's
+     * geometry count: for very large robots the persistent grid keeps only as many waves
+     * as half the free HBM holds (the ticket queue hands out the work either way) */
+    size_t free_b = 0, total_b = 0;
+    if ((e = hipMemGetInfo(&free_b, &total_b)) != hipSuccess) return e;
+    free_b += ctx->cap_scratch * sizeof(double); /* the current workspace is given back below */
+    const size_t per_group = (size_t)ctx->waves_per_group * ctx->scratch_per_wave * sizeof(double);
+    const size_t max_groups = std::max<size_t>(1, (free_b / 2) / std::max<size_t>(1, per_group));
+    if ((size_t)ctx->grid_groups > max_groups) {
+        ctx->grid_groups = (uint32_t)max_groups;
+        ctx->grid_waves = ctx->grid_groups * ctx->waves_per_group;
+    }
+    const size_t words = (size_t)ctx->grid_waves * ctx->scratch_per_wave;
+    if (words > ctx->cap_scratch || !ctx->d_scratch) {
+        if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+        ctx->d_scratch = nullptr;
+        ctx->cap_scratch = 0;
+        if ((e = hipMalloc((void**)&ctx->d_scratch, words * sizeof(double))) != hipSuccess) return e;
+        ctx->cap_scratch = words;
+    }
+    return hipSuccess;
+}
 
 fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
@@ -667,6 +765,45 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
             lever[k] = (std::fabs(an - 1.0) < 1e-12 && std::isfinite(worst)) ? worst * (1.0 + 1e-9) + 1e-12 : HUGE_VAL;
         }
     }
+    /* per (link, dof): the lever bound over link l's points only (reach from dof d's joint
+     * frame down to link l + |p|; |axis| for prismatic joints), 0 if d does not move l */
+    std::vector<double> link_lever((size_t)std::max(1, R.L) * (size_t)std::max(1, R.D), 0.0);
+    if (d->robot_type == FKS_ROBOT_LINKED) {
+        for (int k = 0; k < R.D; ++k) {
+            const int jd = dof_joint[k];
+            const double* ax = joints[jd].axis;
+            const double an = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+            for (int g = 0; g < G; ++g) {
+                const int l = d->geometry_link[g];
+                if (!((link_mask[l] >> k) & 1ull)) continue;
+                double& out = link_lever[(size_t)l * R.D + k];
+                if (!std::isfinite(lever[k])) {
+                    out = HUGE_VAL;
+                    continue;
+                }
+                if (joints[jd].type == FKS_JOINT_PRISMATIC) {
+                    out = lever[k];
+                    continue;
+                }
+                double reach = 0.0;
+                for (int cur = l; cur != joints[jd].child;) {
+                    const JointDev& jp = joints[link_parent_joint[cur]];
+                    reach += std::sqrt(jp.origin[3] * jp.origin[3] + jp.origin[7] * jp.origin[7] + jp.origin[11] * jp.origin[11]);
+                    if (jp.type == FKS_JOINT_PRISMATIC)
+                        reach += std::max(std::fabs(jp.lo), std::fabs(jp.hi)) *
+                                 std::sqrt(jp.axis[0] * jp.axis[0] + jp.axis[1] * jp.axis[1] + jp.axis[2] * jp.axis[2]);
+                    cur = jp.parent;
+                }
+                double worst = 0.0;
+                for (uint32_t i = d->geometry_point_offset[g]; i < d->geometry_point_offset[g + 1]; ++i) {
+                    const double* p = d->points + 4 * (size_t)i;
+                    worst = std::max(worst, reach + std::sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]));
+                }
+                const double b = (std::fabs(an - 1.0) < 1e-12 && std::isfinite(worst)) ? worst * (1.0 + 1e-9) + 1e-12 : HUGE_VAL;
+                out = std::max(out, b);
+            }
+        }
+    }
     std::vector<double> weights;
     if (d->robot_type == FKS_ROBOT_LINKED) {
         for (int k = 0; k < R.D; ++k) weights.push_back(d->distance_weights ? d->distance_weights[k] : 1.0);
@@ -719,6 +856,8 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     HIP_TRY(ctx, up(&drounds, rounds.data(), rounds.size()));
     double* dlever = nullptr;
     HIP_TRY(ctx, up(&dlever, lever.data(), lever.size()));
+    double* dllever = nullptr;
+    HIP_TRY(ctx, up(&dllever, link_lever.data(), link_lever.size()));
     R.joints = dj;
     R.geom_link = dgl;
     R.geom_off = dgo;
@@ -735,6 +874,7 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     R.weights = dw;
     R.rounds = drounds;
     R.dof_lever = dlever;
+    R.link_lever = dllever;
     R.sampled_mask = 0;
     R.sampled = nullptr;
     if (d->sampled_actuators) {
@@ -756,53 +896,19 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
         HIP_TRY(ctx, up(&dsd, sd.data(), sd.size()));
         R.sampled = dsd;
     }
-    /* launch geometry: one wave per workgroup, as many resident waves as fit */
-    fksd::LdsLayout L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds);
-    /* the paired FK of free microsteps (linked chains of <= 32 joints) needs a second set
-     * of joint motion matrices per wave: taken only when it costs no workgroup per CU */
-    ctx->fk_pair = false;
-    if (R.type == FKS_ROBOT_LINKED && R.J >= 1 && R.J <= 32) {
-        const fksd::LdsLayout Lp = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, true);
-        const size_t g0 = (160 * 1024) / (((size_t)L.shared_total + (size_t)fksd::kWavesPerGroup * L.total) * sizeof(double));
-        const size_t g1 = (160 * 1024) / (((size_t)Lp.shared_total + (size_t)fksd::kWavesPerGroup * Lp.total) * sizeof(double));
-        if (g1 >= 1 && g1 >= std::min<size_t>(g0, 5)) {
-            L = Lp;
-            ctx->fk_pair = true;
-        }
+    /* joint-space proof of free microsteps: every 64-point round on one
+     * link with w = 1 points (the per-round SDF proofs it extends), at most 64 rounds (the
+     * skip masks), finite lever bounds and w = 1 geometry boxes (the self-collision gap) */
+    R.jp_ok = 0;
+    if (d->robot_type == FKS_ROBOT_LINKED && NR >= 1 && NR <= 64 && R.L <= 64) {
+        bool ok = true;
+        for (int r = 0; r < NR; ++r) ok = ok && rounds[r].link >= 0;
+        for (int k = 0; k < R.D; ++k) ok = ok && std::isfinite(lever[k]);
+        for (double v : link_lever) ok = ok && std::isfinite(v);
+        for (int g = 0; g < G; ++g) ok = ok && box[7 * g + 6] == 1.0;
+        R.jp_ok = ok ? 1 : 0;
     }
-    /* four waves share one LDS copy of the robot tables; robots whose per-wave blocks do
-     * not fit four times in the CU's 160 KiB run two or one wave per workgroup (the
-     * largest robot the descriptor admits, 64 links / dofs / geometries, fits at one) */
-    ctx->waves_per_group = fksd::kWavesPerGroup;
-    for (;;) {
-        ctx->lds_bytes = ((size_t)L.shared_total + (size_t)ctx->waves_per_group * L.total) * sizeof(double);
-        if (ctx->lds_bytes <= 160 * 1024 || ctx->waves_per_group == 1) break;
-        ctx->waves_per_group /= 2;
-    }
-    if (ctx->lds_bytes > 160 * 1024) return fail(ctx, FKS_ERR_UNSUPPORTED, "robot too large for the LDS layout");
-    int blocks_per_cu = 0;
-    HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, reinterpret_cast<const void*>(kernel_for(R.type)),
-                                                              64 * ctx->waves_per_group, ctx->lds_bytes));
-    if (blocks_per_cu < 1) return fail(ctx, FKS_ERR_UNSUPPORTED, "kernel does not fit on a CU");
-    int cus = 0;
-    HIP_TRY(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    ctx->grid_groups = (uint32_t)(cus * blocks_per_cu);
-    ctx->grid_waves = ctx->grid_groups * ctx->waves_per_group;
-    ctx->scratch_per_wave = fksd::make_scratch_layout(3u * P, R.D, (int)P, G).total;
-    /* the per-wave workspace grows with 3P x D (the stacked Jacobian) and the robot's
-     * geometry count: for very large robots the persistent grid keeps only as many waves
-     * as half the free HBM holds (the ticket queue hands out the work either way) */
-    {
-        size_t free_b = 0, total_b = 0;
-        HIP_TRY(ctx, hipMemGetInfo(&free_b, &total_b));
-        const size_t per_group = (size_t)ctx->waves_per_group * ctx->scratch_per_wave * sizeof(double);
-        const size_t max_groups = std::max<size_t>(1, (free_b / 2) / std::max<size_t>(1, per_group));
-        if ((size_t)ctx->grid_groups > max_groups) {
-            ctx->grid_groups = (uint32_t)max_groups;
-            ctx->grid_waves = ctx->grid_groups * ctx->waves_per_group;
-        }
-    }
-    HIP_TRY(ctx, hipMalloc((void**)&ctx->d_scratch, (size_t)ctx->grid_waves * ctx->scratch_per_wave * sizeof(double)));
+    HIP_TRY(ctx, launch_layout(ctx, R));
     ctx->R = R;
     ctx->has_robot = true;
     return FKS_OK;
@@ -841,6 +947,7 @@ static fks_status settle(fks_context* ctx) {
     ctx->last.least_squares_rows = c[fksd::kCntLsqRows];
     ctx->last.self_collision_checks = c[fksd::kCntSelfChecks];
     ctx->last.self_corrected_points = c[fksd::kCntSelfPoints];
+    ctx->last.proven_free_microsteps = c[fksd::kCntProvenMicro];
     for (int k = 0; k < FKS_NUM_PHASES; ++k) {
         ctx->phase_last[k] = c[fksd::kPhaseBase + k];
         ctx->phase_total[k] += ctx->phase_last[k];
@@ -859,6 +966,7 @@ static fks_status settle(fks_context* ctx) {
     ctx->total.least_squares_rows += ctx->last.least_squares_rows;
     ctx->total.self_collision_checks += ctx->last.self_collision_checks;
     ctx->total.self_corrected_points += ctx->last.self_corrected_points;
+    ctx->total.proven_free_microsteps += ctx->last.proven_free_microsteps;
     ctx->total.kernel_ms += ctx->last.kernel_ms;
     ctx->total.call_ms += ctx->last.call_ms;
     ctx->total.calls += 1;
@@ -912,6 +1020,7 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.skip_enabled = ctx->skip_enabled;
     a.skip_lplus = ctx->skip_lplus;
     a.skip_cmax = ctx->skip_cmax;
+    a.skip_inv_lplus = (ctx->skip_lplus > 0.0) ? 1.0 / ctx->skip_lplus : 0.0;
     a.R = ctx->R;
     a.S = ctx->params;
     a.dt = 1.0 / ctx->frequency;
@@ -929,6 +1038,8 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.first_pid = first_particle_id;
     a.allow_contacts = allow_contacts ? 1 : 0;
     a.individual_jacobians = ctx->individual_jacobians;
+    /* traced calls record every microstep's configuration the reference's way: no proof */
+    a.jproof = (!tr && !ctx->individual_jacobians && ctx->jp_layout && ctx->R.jp_ok && ctx->skip_enabled && ctx->joint_proof) ? 1 : 0;
     a.out_q = d_out_positions;
     a.pid_io = d_pid_io;
     a.out_collided = d_out_collided;
@@ -940,7 +1051,7 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair, ctx->jp_layout);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     /* controller-step segments: automatically only when the batch outnumbers the
      * resident waves (otherwise every particle has a wave from the start), always
@@ -992,7 +1103,11 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? (groups_needed > 0 ? groups_needed : 1)
                                                                                   : ctx->grid_groups);
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
-    hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type) : kernel_for(ctx->R.type, ctx->individual_jacobians != 0), dim3(grid),
+    /* the joint-space proof runs in its own instantiation (fks_simulate_linked_jp): the
+     * paired FK it replaces stays out of it, and out of the other kernels goes the proof */
+    hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type)
+                          : (a.jproof ? fks_simulate_linked_jp : kernel_for(ctx->R.type, ctx->individual_jacobians != 0)),
+                       dim3(grid),
                        dim3(64 * ctx->waves_per_group), ctx->lds_bytes, s, static_cast<const fksd::SimArgs*>(ctx->d_args));
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
@@ -1056,7 +1171,7 @@ fks_status fks_check_config_collision_device(fks_context* ctx, const double* d_c
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair, ctx->jp_layout);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     *ctx->h_args = a;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice, s));
@@ -1339,7 +1454,7 @@ fks_status fks_kinematics(fks_context* ctx, int32_t mode, const double* configs,
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair, ctx->jp_layout);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     a.kin_mode = mode;
     a.kin_out = d_out;
@@ -1437,6 +1552,18 @@ fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_
     if (heavy_priority > 2u) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "heavy_priority must be 0, 1 or 2");
     ctx->heavy_per_step = heavy_resolver_per_step;
     ctx->heavy_priority = heavy_priority;
+    return FKS_OK;
+}
+
+fks_status fks_set_joint_proof(fks_context* ctx, int32_t enable) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    ctx->joint_proof = enable ? 1 : 0;
+    if (ctx->has_robot) {
+        const fks_status st = settle(ctx); /* a launch in flight still uses the old layout */
+        if (st != FKS_OK) return st;
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        HIP_TRY(ctx, launch_layout(ctx, ctx->R));
+    }
     return FKS_OK;
 }
 

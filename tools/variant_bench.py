@@ -17,17 +17,24 @@ def main():
     extra = []
     libs = []
     for a in sys.argv[1:]:
-        (extra if a.startswith("--") or (extra and not a.endswith(".so")) else libs).append(a)
-    for lib in libs:
+        # "lib.so+flag" runs that library with bench.py --flag (e.g. libfks_hip.so+joint-proof)
+        (extra if a.startswith("--") or (extra and ".so" not in a) else libs).append(a)
+    for spec in libs:
+        lib, _, flag = spec.partition("+")
         env = dict(os.environ, FKS_LIB_PATH=os.path.abspath(lib))
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1", "--no-cpu-baseline", *extra]
+        if flag:
+            cmd.append("--" + flag)
         p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=900)
         if p.returncode != 0:
             print(f"{lib}: FAILED rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
             sys.exit(p.returncode)
         line = json.loads(p.stdout.strip().splitlines()[-1])
-        print(json.dumps({"lib": os.path.basename(lib), "value": line["value"], "kernel_ms": line["roofline"]["avg_kernel_ms"],
-                          "frac": line["roofline"]["frac"], "phases": line.get("kernel_phases")}), flush=True)
+        print(json.dumps({"lib": os.path.basename(lib) + ("+" + flag if flag else ""), "value": line["value"], "kernel_ms": line["roofline"]["avg_kernel_ms"],
+                          "frac": line["roofline"]["frac"], "error_particles": line["config"].get("error_particles"),
+                          "proven": line["config"].get("proven_free_microsteps_fraction"),
+                          "busy": line.get("wave_slots", {}).get("busy_fraction"), "phases": line.get("kernel_phases")}),
+              flush=True)
 
 
 if __name__ == "__main__":
