@@ -286,7 +286,10 @@ struct SimArgs {
      * satisfies: axis neighbours with positive values differ by <= lplus*res, and
      * positive cells next to a non-positive one are <= cmax*res */
     int32_t skip_enabled;
-    int32_t pad_skip;
+    /* the SDF is the exact Euclidean distance transform of its own sign (the builders'
+     * sqrt(d_filled) res - sqrt(d_free) res) and the env threshold is <= 0: a free cell s
+     * cells from the nearest filled one has only free cells within s */
+    int32_t skip_euclid;
     double skip_lplus, skip_cmax;
     double skip_inv_lplus; /* 1 / skip_lplus (the joint-space proof's admissible motion) */
     RobotDev R;

@@ -456,6 +456,7 @@ struct Sim {
     bool tcur_valid; /* Tcur == FK(particle configuration) from the end of the last step */
     bool jp_valid;   /* the joint-space proof's anchor and slack (LDS) hold for this particle */
     bool jp_pending; /* the last controller step ended on a free check at Tcur = FK(cfg): anchor there */
+    bool jp_rest;    /* the last attempt proved nothing: the next step runs without one */
     uint64_t local;            /* particle index within the call (traced kernels) */
     uint32_t tr_steps, tr_cfgs; /* trace records produced so far (traced kernels) */
 };
@@ -1065,6 +1066,7 @@ __device__ __forceinline__ RoundDev lds_round(const Sim& s, int r) {
 __device__ __forceinline__ double round_admissible(const SimArgs& A, double S, double G, double C) {
     double bm = dmin(((S * A.sdf_g.inv_res - A.skip_cmax - 1e-9) * A.skip_inv_lplus - 2.0) * 0.57735026918962573, G - 1e-6);
     if (S >= A.thr_env) bm = dmax(bm, C - 1e-9);
+    if (A.skip_euclid) bm = dmax(bm, dmin(S * A.sdf_g.inv_res * (1.0 - 1e-6) - 1.7320508075688773 - 1e-6, G - 1.0 - 1e-6));
     return bm * (1.0 - 1e-6) - 1e-9;
 }
 
@@ -1093,7 +1095,11 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
             for (int e = 0; e < 12; ++e) still = still && (Tl[e] == st[e]);
             const bool same_cell = still || b < st[14] - 1e-9;
             if (what == kSkipCheck)
-                sk = (inb && (Sr - A.skip_cmax) > (K - 1.0) * lp + 1e-9) || (same_cell && st[12] >= A.thr_env);
+                sk = (inb && (Sr - A.skip_cmax) > (K - 1.0) * lp + 1e-9) || (same_cell && st[12] >= A.thr_env) ||
+                     /* exact EDT: every point ends in a cell whose centre is within b + sqrt(3)
+                      * of its old cell's, which is Sr or more from any filled cell; all
+                      * coordinates stay > 0 (st[13] - 1 > b), where a cell spans [i, i + 1) */
+                     (A.skip_euclid && b < Sr * (1.0 - 1e-6) - 1.7320508075688773 - 1e-6 && b < st[13] - 1.0 - 1e-6);
             else
                 sk = (inb && (Sr - A.skip_cmax) > K * lp + 1e-9 && (Sr - K * lp) > 0.5 + 1.5 * lp + 1e-6) ||
                      (same_cell && Sr > A.skip_cmax + 1e-9 && Sr > 0.5 + 1.5 * lp + 1e-6);
@@ -1766,6 +1772,11 @@ __device__ bool check_collision(Sim& s, const double* Tp, const double* Tc) {
 
 #ifndef FKS_VERIFY_JP
 #define FKS_VERIFY_JP 0
+#endif
+/* a controller step whose proof attempt proved nothing is followed by one without an
+ * attempt (near obstacles most attempts fail at once and cost a noise refill each) */
+#ifndef FKS_JP_BACKOFF
+#define FKS_JP_BACKOFF 1
 #endif
 constexpr uint32_t kErrProofViolation = 0x40000000u; /* FKS_VERIFY_JP builds only */
 
@@ -2746,10 +2757,14 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
          * ApplyControlInput (SPCS:1599) is applied and every CheckCollision (SPCS:1600-1602)
          * is proven free, so the step ends at the last microstep's configuration with no
          * contact; the reference reads 4 bytes per point per check (all in bounds) */
-        if (s.jp_valid || s.jp_pending) {
+        if (FKS_JP_BACKOFF && s.jp_rest) {
+            s.jp_rest = false;
+            s.jp_pending = false;
+        } else if (s.jp_valid || s.jp_pending) {
             jr = jp_step(s.A, s.lds, s.shared, s.scratch, s.lane, s.pid, s.step, M, s.jp_pending ? Tcur : nullptr, Tcur, Ttmp);
             if (s.jp_pending) s.jp_valid = (jr & 2u) != 0u;
             s.jp_pending = false;
+            s.jp_rest = (jr & 1u) == 0u && (jr >> 8) == 0u;
         }
         if (jr & 1u) {
             const int ln = s.lane;
@@ -2803,7 +2818,9 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
             s.err |= pair_err;
             wsync();
         } else {
-            if (micro % (uint32_t)(kWave / R.D) == 0u)
+            /* (after a jp_step attempt the buffer already holds the block of its first
+             * unproven microstep, where the loop starts) */
+            if (micro % (uint32_t)(kWave / R.D) == 0u && !(JP && jr != 0u && micro == (jr >> 8)))
                 for (int k = 0; k < prof_reps(kDupRefill); ++k) refill_noise(s, micro, M);
             for (int k = 0; k < prof_reps(kDupInput); ++k) apply_input<RT>(s, cfg_prev, ustep, cfg, true, micro);
         }
@@ -3372,6 +3389,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         s.tcur_valid = false;
         s.jp_valid = false;
         s.jp_pending = false;
+        s.jp_rest = false;
         const double* start = A.starts + local * (uint64_t)W;
         const double* target = (A.num_targets == A.n) ? A.targets + local * (uint64_t)W : A.targets;
         bool collided = false;

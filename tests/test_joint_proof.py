@@ -97,3 +97,31 @@ def test_joint_proof_full_cfg3_bit_identical(fks_lib):
     _assert_same(off, on)
     print("cfg3 full: proven", on["counters"]["proven_free_microsteps"], "of", on["counters"]["microsteps"])
     assert on["counters"]["proven_free_microsteps"] > on["counters"]["microsteps"] // 10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,scale", [("cfg2", 1.0), ("cfg3", 4096 / 65536)])
+def test_exact_edt_skip_route_bit_identical(fks_lib, name, scale):
+    """A simulator made from the GPU-built, device-resident environment also skips rounds by
+    the exact-EDT (Euclidean) proof (SimArgs.skip_euclid); the host copy of the same bytes
+    does not.  Results and counters must agree, with the joint-space proof off and on."""
+    wl = W.WORKLOADS[name](scale)
+    host_env = W.SCENES[name](device=0)
+    dev_env = W.SCENES[name](device=0, resident=True)
+    for proof in (False, True):
+        outs = []
+        for env in (host_env, dev_env):
+            sim = make_linked_simulator(env, wl.solver, wl.controller_frequency, wl.seed)
+            try:
+                sim.set_joint_proof(proof)
+                out = sim.forward_simulate_arrays(wl.robot, wl.starts, wl.targets, wl.allow_contacts)
+                out["statistics"] = sim.get_statistics()
+                out["counters"] = sim.last_call_counters()
+            finally:
+                sim.close()
+            outs.append(out)
+        _assert_same(outs[0], outs[1])
+        print(name, "proof", proof, "proven host/device", outs[0]["counters"]["proven_free_microsteps"],
+              outs[1]["counters"]["proven_free_microsteps"])
+        if proof:
+            assert outs[1]["counters"]["proven_free_microsteps"] >= outs[0]["counters"]["proven_free_microsteps"]
