@@ -1778,6 +1778,10 @@ __device__ bool check_collision(Sim& s, const double* Tp, const double* Tc) {
 #ifndef FKS_JP_BACKOFF
 #define FKS_JP_BACKOFF 1
 #endif
+/* a step whose proof stops at microstep m > 0 keeps microsteps 0 .. m - 1 */
+#ifndef FKS_JP_PREFIX
+#define FKS_JP_PREFIX 1
+#endif
 constexpr uint32_t kErrProofViolation = 0x40000000u; /* FKS_VERIFY_JP builds only */
 
 /* After a controller step whose last CheckCollision came back free at transforms T =
@@ -1886,13 +1890,15 @@ __device__ __attribute__((always_inline)) uint32_t jp_step(const SimArgs* __rest
     /* microsteps 0 .. m - 1 proven, microstep m not: the step resumes at m from their last
      * configuration (copied to cfg_work) and its transforms (FK into Tcur) */
     auto prefix = [&](uint32_t m) -> uint32_t {
+        /* bit 2: the noise buffer holds the block of the microstep the step resumes at */
+        if (!FKS_JP_PREFIX) return 2u | (m < per ? 4u : 0u); /* variant: the whole step runs again */
         if (m > 0u) {
             double* cw = lds + A.L.cfg_work;
             if (ln < R.W) cw[ln] = in[ln];
             wsync();
             fk<FKS_ROBOT_LINKED>(t, cw, Tcur);
         }
-        return 2u | (m << 8);
+        return 2u | 4u | (m << 8);
     };
     for (uint32_t m = 0; m < M; ++m) {
         double* out = buf[m & 1u];
@@ -2751,7 +2757,8 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
     const uint32_t noise_per = (uint32_t)(kWave / R.D);
     bool pair_ready = false; /* Ttmp holds FK(cfg_tmp), cfg_tmp = the predicted configuration */
     uint32_t pair_err = 0;   /* the predicted configuration's actuator error bits (per lane) */
-    uint32_t jr = 0; /* jp_step: bit 0 whole step proven, bit 1 anchor holds, bits 8.. proven prefix */
+    uint32_t jr = 0; /* jp_step: bit 0 whole step proven, bit 1 anchor holds, bit 2 noise block of the
+                      * resume microstep drawn, bits 8.. proven prefix */
     if constexpr (JP) {
         /* the whole controller step settled by the joint-space proof: every microstep's
          * ApplyControlInput (SPCS:1599) is applied and every CheckCollision (SPCS:1600-1602)
@@ -2820,7 +2827,7 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
         } else {
             /* (after a jp_step attempt the buffer already holds the block of its first
              * unproven microstep, where the loop starts) */
-            if (micro % (uint32_t)(kWave / R.D) == 0u && !(JP && jr != 0u && micro == (jr >> 8)))
+            if (micro % (uint32_t)(kWave / R.D) == 0u && !(JP && (jr & 4u) != 0u && micro == (jr >> 8)))
                 for (int k = 0; k < prof_reps(kDupRefill); ++k) refill_noise(s, micro, M);
             for (int k = 0; k < prof_reps(kDupInput); ++k) apply_input<RT>(s, cfg_prev, ustep, cfg, true, micro);
         }
