@@ -20,7 +20,9 @@
  *   - self-collision (SPCS:1183-1275): per-geometry conservative cell-key boxes
  *     (one lane per geometry) reject disallowed pairs; only overlapping pairs run
  *     the exact key comparison, and true self-contacts run the impulse solve
- *     (SPCS:983-1171) on one lane.
+ *     (SPCS:983-1171) on one lane;
+ *   - optionally (fks_simulate_linked_jp, fks_set_joint_proof) the joint-space proof
+ *     settles free microsteps from joint space without their FK and checks (jp_step).
  * All double arithmetic is IEEE (no contraction: built with -ffp-contract=off),
  * transcendentals come from include/fks_portable_math.h, so results are
  * bit-identical to the CPU oracle on the same inputs.

@@ -1,6 +1,10 @@
 # joint-proof round: full GPU suite (stop on failure), verification build with the proof on
 # (every proven microstep re-checked in full: error_particles must stay 0), A/B benches.
 # usage: bash tools/jp_check.sh <tag> <lib[+flag]> [...]
+# the verification build first, on the CPU side:
+#   python -c "from fast_kinematic_simulator_amd.build import build_variant; \
+#              build_variant('build/variants/libfks_verify.so', ['FKS_VERIFY_JP=1'])"
+# (a baseline library for the A/B: the same sources at another commit, built with build_variant)
 TAG=${1:-jpc}; shift
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
