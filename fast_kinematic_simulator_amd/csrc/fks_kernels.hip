@@ -2250,13 +2250,16 @@ __device__ FKS_QR_ATTR void qr_solve_regs(const SimArgs* __restrict__ Ap, double
  * (r2 + r3) of bfly_sum with r1 = r2 = r3 = +0.0) */
 template <int RM>
 __device__ __forceinline__ double lane_tree_sum(const double (&p)[RM]) {
-    static_assert(RM == 8 || RM == 16, "tree over 8 or 16 rows");
+    static_assert(RM == 4 || RM == 8 || RM == 16, "tree over 4, 8 or 16 rows");
     double l1[RM / 2];
 #pragma unroll
     for (int i = 0; i < RM / 2; ++i) l1[i] = p[2 * i] + p[2 * i + 1];
     double l2[RM / 4];
 #pragma unroll
     for (int i = 0; i < RM / 4; ++i) l2[i] = l1[2 * i] + l1[2 * i + 1];
+    /* 4 rows: the 8-row tree's other half is (+0 + +0) + (+0 + +0) = +0, and
+     * (x + +0) + +0 == x + +0 for every x, so the last "+ 0.0" alone keeps the bits */
+    if constexpr (RM == 4) return l2[0] + 0.0;
     double t = (l2[0] + l2[1]);
     if constexpr (RM == 16) t = t + ((l2[2] + l2[3]));
     return t + 0.0;
@@ -2294,8 +2297,8 @@ __device__ __forceinline__ int wave_first_argmax(double val, int ln, int first, 
  * of a wave butterfly, and the D - k - 1 column updates of step k run side by side
  * in their lanes.  Same arithmetic as qr_solve_regs / qr_solve, bit for bit. */
 template <int RM>
-__device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
-                                           uint32_t Rn, double* x, uint32_t row0 = 0) {
+__device__ __forceinline__ void qr_solve_cols_body(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
+                                                   uint32_t Rn, double* x, uint32_t row0) {
     const SimArgs& A = *Ap;
     const int D = A.R.D;
     const uint32_t rc = A.row_cap;
@@ -2462,6 +2465,21 @@ __device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double
         if (r == ln) mine = bu[r];
     if (ln < nz) x[perm[ln]] = mine;
     wsync();
+}
+
+/* the out-of-line entry (one call site per row bound in the resolver): a single corrected
+ * point (3 rows) runs the 4-row body, same arithmetic (lane_tree_sum<4>) with half the
+ * unrolled rows of the 8-row one */
+template <int RM>
+__device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
+                                           uint32_t Rn, double* x, uint32_t row0 = 0) {
+    if constexpr (RM == 8) {
+        if (Rn <= 4u) {
+            qr_solve_cols_body<4>(Ap, lds, scratch, ln, Rn, x, row0);
+            return;
+        }
+    }
+    qr_solve_cols_body<RM>(Ap, lds, scratch, ln, Rn, x, row0);
 }
 
 /* ColPivHouseholderQR::solve (Eigen 3.2 / 3.3-beta1), rows lane-strided; x -> LDS.
