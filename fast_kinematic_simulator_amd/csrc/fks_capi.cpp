@@ -78,7 +78,7 @@ using fksd::GridDev;
 /* controller steps per segment when a batch outnumbers the resident waves: short
  * enough that a contact-heavy particle progresses from the start of the launch, long
  * enough that the hand-over (resting state + one FK) costs < 1 % */
-constexpr uint32_t kDefaultSegmentSteps = 10;
+constexpr uint32_t kDefaultSegmentSteps = 14; /* re-swept in round 2: profiles/r02ar_sched_sweep_*.json */
 /* a segment averaging this many resolver iterations per controller step is
  * contact-heavy: its wave keeps the particle (the cfg3 batch averages 0.65) */
 constexpr uint32_t kHeavyResolverPerStep = 2;

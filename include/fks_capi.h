@@ -413,7 +413,7 @@ fks_status fks_get_phase_cycles(const fks_context* ctx, int which, uint64_t* out
 fks_status fks_get_launch_geometry(const fks_context* ctx, uint32_t* resident_waves, uint64_t* lds_bytes_per_group);
 /* Scheduling granularity of fks_forward_simulate*: when a batch holds more particles
  * than the grid has resident waves, each particle's controller steps are run in
- * segments of `controller_steps` (0 = automatic: 10 when the batch outnumbers the
+ * segments of `controller_steps` (0 = automatic: 14 when the batch outnumbers the
  * resident waves, else whole; nonzero: always), handed out segment-major so
  * that every particle progresses from the start of the launch and contact-heavy
  * particles do not start last (the batch's tail).  Results are bit-identical for

@@ -2,7 +2,7 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for p in a b; do
-  timeout -k 10 300 python tools/sched_sweep.py --segments 8,10,14 --heavy 1,2,3 --prio 1,2 --json gpurun_out/r02ar_sched_sweep_$p.json > gpurun_out/sweep_$p.log 2>&1 || exit 1
+  timeout -k 10 300 python tools/sched_sweep.py --segments ${SEGS:-8,10,14} --heavy ${HEAVY:-1,2,3} --prio ${PRIO:-1,2} --json gpurun_out/r02ar_sched_sweep_$p.json > gpurun_out/sweep_$p.log 2>&1 || exit 1
 done
 python3 - <<'PY'
 import json
