@@ -60,7 +60,11 @@ def build_variant(output: str, defines) -> str:
     return output
 
 
-def build_cpp_program(src: str, name: str, force: bool = False, extra_flags=()) -> str:
+def _headers(directory: str) -> list:
+    return [os.path.join(d, f) for d, _, fs in os.walk(directory) for f in fs]
+
+
+def build_cpp_program(src: str, name: str, force: bool = False, extra_flags=(), extra_deps=()) -> str:
     """Compile a host C++ program over the public headers (include/) and link
     libfks_hip.so: g++ only, no HIP toolchain, as a planner would build against the
     drop-in.  Output: build/<name>."""
@@ -70,7 +74,7 @@ def build_cpp_program(src: str, name: str, force: bool = False, extra_flags=()) 
     os.makedirs(out_dir, exist_ok=True)
     target = os.path.join(out_dir, name)
     inc = os.path.join(ROOT, "include")
-    headers = [os.path.join(d, f) for d, _, fs in os.walk(inc) for f in fs]
+    headers = _headers(inc) + list(extra_deps)
     if not force and os.path.exists(target) and all(os.path.getmtime(target) >= os.path.getmtime(p)
                                                     for p in [src, lib] + headers):
         return target
@@ -88,9 +92,17 @@ def build_example(force: bool = False) -> str:
     return build_cpp_program(os.path.join("examples", "cpp_forward_simulate.cpp"), "cpp_forward_simulate", force)
 
 
-def build_planner_test(force: bool = False) -> str:
+MOCK_WORKSPACE = os.path.join(ROOT, "tests", "cpp", "mock_workspace", "include")
+
+
+def build_planner_test(force: bool = False, workspace: bool = False) -> str:
     """Compile tests/cpp/planner_interface_test.cpp: the planner-side drop-in driven only
-    through std::shared_ptr<SimulatorInterface<...>> (fast_kinematic_simulator.hpp)."""
+    through std::shared_ptr<SimulatorInterface<...>> (fast_kinematic_simulator.hpp).
+    workspace=True puts the mock planner workspace (tests/cpp/mock_workspace) on the
+    include path, so fks_external_types.hpp takes the real-libraries branch."""
+    if workspace:
+        return build_cpp_program(os.path.join("tests", "cpp", "planner_interface_test.cpp"), "planner_interface_test_workspace",
+                                 force, extra_flags=(f"-I{MOCK_WORKSPACE}",), extra_deps=_headers(MOCK_WORKSPACE))
     return build_cpp_program(os.path.join("tests", "cpp", "planner_interface_test.cpp"), "planner_interface_test", force)
 
 

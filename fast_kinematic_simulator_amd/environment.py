@@ -51,7 +51,7 @@ class SimulatorEnvironment:
         self.normal_entries = np.ascontiguousarray(normal_entries, dtype=np.float64)
         self.oob_value = float(oob_value)
         self.occupancy = occupancy
-        self.frame = "world"  # TaggedObjectCollisionMapGrid::GetFrame (SPCS:519)
+        self.frame = "uncertainty_planning_simulator"  # TaggedObjectCollisionMapGrid::GetFrame (SPCS:519; SEB.cpp:148 names it)
 
     @property
     def resolution(self) -> float:
@@ -105,7 +105,7 @@ class DeviceEnvironment:
         g = _capi.GridGeometry()
         _capi.check(self._lib.fks_device_env_geometry(handle, ctypes.byref(g)), None, "fks_device_env_geometry")
         self.geometry = GridGeometry(np.array(g.origin[:]), g.resolution, tuple(g.num_cells[:]))
-        self.frame = "world"
+        self.frame = "uncertainty_planning_simulator"
         self._host = None
 
     @property

@@ -23,6 +23,9 @@
  *   - the reference's per-particle asserts (SPCS:1570-1575, 1882) become error bits,
  *     available from LastParticleErrors() after a batch call;
  *   - display_fn is accepted and never called (the batch path never draws, SPCS:801).
+ * The Eigen / ROS / sdf_tools / uncertainty_planning_core types in the signatures are the
+ * planner workspace's own when its headers are on the include path, stand-ins otherwise
+ * (fks_external_types.hpp).
  */
 #ifndef FAST_KINEMATIC_SIMULATOR_AMD_FAST_KINEMATIC_SIMULATOR_HPP
 #define FAST_KINEMATIC_SIMULATOR_AMD_FAST_KINEMATIC_SIMULATOR_HPP
@@ -37,7 +40,7 @@
 #include <vector>
 
 #include "fast_kinematic_simulator_amd/environment.hpp"
-#include "fast_kinematic_simulator_amd/simulator_interface.hpp"
+#include "fast_kinematic_simulator_amd/fks_external_types.hpp"
 #include "fast_kinematic_simulator_amd/tnuva_robot_models.hpp"
 #include "fks_capi.h"
 
@@ -100,8 +103,9 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
                                 const uint64_t prng_seed, const int32_t debug_level, const int32_t device = 0)
         : environment_(environment), environment_sdf_(environment_sdf), surface_normals_grid_(surface_normals_grid),
           solver_config_(solver_config), simulation_controller_frequency_(simulation_controller_frequency) {
+        std::vector<float> sdf_storage; /* the values fks_create uploads (real sdf_tools only) */
         const fks_environment env =
-            simulator_environment_builder::ToFksEnvironment(environment, environment_sdf, surface_normals_grid);
+            simulator_environment_builder::ToFksEnvironment(environment_, environment_sdf_, surface_normals_grid_, sdf_storage);
         const fks_solver_params p = solver_config.ToFks();
         fks_context* ctx = nullptr;
         Check(fks_create(&env, &p, simulation_controller_frequency, prng_seed, debug_level, device, &ctx), nullptr, "fks_create");
@@ -149,7 +153,8 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
                                                           Base::MakeColor(1.0f, 0.0f, 0.0f, 1.0f));
         fks_planner_types::Marker sdf_marker = MakeMarker("sim_environment_sdf", 1, fks_planner_types::Marker::CUBE_LIST, res,
                                                           Base::MakeColor(1.0f, 1.0f, 1.0f, 1.0f));
-        const double* O = environment_.Geometry().origin;
+        const fks_grid_geometry G = fks_ext::grid_geometry(environment_);
+        const double* O = G.origin;
         for (int64_t x = 0; x < environment_.GetNumXCells(); ++x)
             for (int64_t y = 0; y < environment_.GetNumYCells(); ++y)
                 for (int64_t z = 0; z < environment_.GetNumZCells(); ++z) {
@@ -158,7 +163,7 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
                     p.x = ((O[0] * c[0] + O[1] * c[1]) + O[2] * c[2]) + O[3];
                     p.y = ((O[4] * c[0] + O[5] * c[1]) + O[6] * c[2]) + O[7];
                     p.z = ((O[8] * c[0] + O[9] * c[1]) + O[10] * c[2]) + O[11];
-                    if (environment_.GetImmutable(x, y, z).first) env_marker.points.push_back(p);
+                    if (environment_.GetImmutable(x, y, z).first.occupancy > 0.5f) env_marker.points.push_back(p);
                     sdf_marker.points.push_back(p);
                     sdf_marker.colors.push_back(environment_sdf_.GetImmutable(x, y, z).first < 0.0f
                                                     ? Base::MakeColor(1.0f, 0.0f, 0.0f, 1.0f)
@@ -193,7 +198,7 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
                                            const int32_t starting_index, const std::string& control_input_marker_ns) const override {
         const DerivedRobotType& robot = Derived(immutable_robot);
         const std::vector<double> start = robot.ToFlat(configuration);
-        const std::vector<double> after = Kinematics(robot, FKS_KIN_APPLY_CONTROL_INPUT, {start}, {control_input.values()});
+        const std::vector<double> after = Kinematics(robot, FKS_KIN_APPLY_CONTROL_INPUT, {start}, {fks_ext::vecx_values(control_input)});
         const std::vector<double> pts = Kinematics(robot, FKS_KIN_POINTS, {start, after});
         const size_t P = pts.size() / 6;
         fks_planner_types::Marker m =
@@ -275,17 +280,31 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
                                                &collided, &micro, &resolver, &errors),
                   ctx_.get(), "ForwardSimulateMutableRobot");
         } else {
-            /* the trace holds one step record per controller step and every pushed configuration */
-            const uint32_t steps = ForwardSteps(), cap = 16384;
-            std::vector<double> inputs((size_t)steps * 2 * D), configs((size_t)cap * W);
-            std::vector<uint32_t> step_micro(steps), tags((size_t)cap * 3);
-            uint32_t num_steps = 0, num_configs = 0;
-            fks_trace tr{steps, cap, inputs.data(), step_micro.data(), configs.data(), tags.data(), &num_steps, &num_configs};
-            Check(fks_forward_simulate_traced_mutable(ctx_.get(), s.data(), 1, t.data(), 1, allow_contacts ? 1 : 0, pid.data(),
-                                                      q.data(), &collided, &micro, &resolver, &errors, &tr),
-                  ctx_.get(), "ForwardSimulateMutableRobot (traced)");
-            if (num_steps > steps || num_configs > cap) throw std::runtime_error("trace capacity exceeded");
-            AppendTrace(r, trace, inputs, num_steps, configs, tags, num_configs, D);
+            /* the trace holds one step record per controller step and every pushed
+             * configuration.  The capacity starts at 16384 configurations; a longer trace is
+             * re-run with the exact size, from the same RNG call index and controller state
+             * (the simulation is deterministic, so the rerun reproduces it) */
+            const uint32_t steps = ForwardSteps();
+            const uint64_t call = fks_get_call_index(ctx_.get());
+            const std::vector<double> pid0 = pid;
+            uint32_t cap = 16384;
+            for (int attempt = 0;; ++attempt) {
+                std::vector<double> inputs((size_t)steps * 2 * D), configs((size_t)cap * W);
+                std::vector<uint32_t> step_micro(steps), tags((size_t)cap * 3);
+                uint32_t num_steps = 0, num_configs = 0;
+                fks_trace tr{steps, cap, inputs.data(), step_micro.data(), configs.data(), tags.data(), &num_steps, &num_configs};
+                Check(fks_forward_simulate_traced_mutable(ctx_.get(), s.data(), 1, t.data(), 1, allow_contacts ? 1 : 0, pid.data(),
+                                                          q.data(), &collided, &micro, &resolver, &errors, &tr),
+                      ctx_.get(), "ForwardSimulateMutableRobot (traced)");
+                if (num_steps <= steps && num_configs <= cap) {
+                    AppendTrace(r, trace, inputs, num_steps, configs, tags, num_configs, D);
+                    break;
+                }
+                if (attempt > 0 || num_steps > steps) throw std::runtime_error("trace capacity exceeded");
+                cap = num_configs;
+                pid = pid0;
+                Check(fks_set_call_index(ctx_.get(), call), ctx_.get(), "fks_set_call_index");
+            }
         }
         last_errors_.assign(1, errors);
         r.SetPosition(r.FromFlat(q.data()));
@@ -343,7 +362,7 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
         m.ns = ns;
         m.id = id;
         m.type = type;
-        m.frame_id = GetFrame();
+        m.header.frame_id = GetFrame();
         m.scale.x = m.scale.y = m.scale.z = scale;
         m.color = color;
         return m;
@@ -352,10 +371,13 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
         const double raw = solver_config_.forward_simulation_time * std::fabs(simulation_controller_frequency_);
         return raw >= 1.0 && raw < 4294967295.0 ? (uint32_t)raw : 1u; /* SPCS:856 */
     }
-    /* the robot every particle clones: flattened once per description (clones share it) */
+    /* the robot every particle clones: flattened once per description (clones share it).
+     * The cache key owns the description, so a destroyed robot's address can never be
+     * mistaken for a new robot's (the description is immutable once built). */
     void SetRobot(const DerivedRobotType& robot) const {
-        const fks::RobotDescription* d = &robot.HipDescription();
+        const std::shared_ptr<const fks::RobotDescription>& d = robot.SharedHipDescription();
         if (d == robot_key_) return;
+        robot_key_.reset();
         const fks_robot_desc v = d->View();
         Check(fks_set_robot(ctx_.get(), &v), ctx_.get(), "fks_set_robot");
         robot_key_ = d;
@@ -414,10 +436,10 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
         const size_t base = trace.resolver_steps.size(), W = configs.size() / (tags.size() / 3);
         for (uint32_t k = 0; k < num_steps; ++k) {
             typename decltype(trace.resolver_steps)::value_type rs;
-            rs.control_input = fks_planner_types::VectorXd(
-                std::vector<double>(inputs.begin() + (long)(k * 2 * D), inputs.begin() + (long)(k * 2 * D + D)));
-            rs.control_input_step = fks_planner_types::VectorXd(
-                std::vector<double>(inputs.begin() + (long)(k * 2 * D + D), inputs.begin() + (long)((k + 1) * 2 * D)));
+            rs.control_input =
+                fks_ext::vecx(std::vector<double>(inputs.begin() + (long)(k * 2 * D), inputs.begin() + (long)(k * 2 * D + D)));
+            rs.control_input_step =
+                fks_ext::vecx(std::vector<double>(inputs.begin() + (long)(k * 2 * D + D), inputs.begin() + (long)((k + 1) * 2 * D)));
             trace.resolver_steps.push_back(rs);
         }
         int64_t last_step = -1, last_micro = -1;
@@ -437,7 +459,7 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
     SimulatorSolverParameters solver_config_;
     double simulation_controller_frequency_;
     std::unique_ptr<fks_context, Destroy> ctx_;
-    mutable const fks::RobotDescription* robot_key_ = nullptr;
+    mutable std::shared_ptr<const fks::RobotDescription> robot_key_;
     RNG rng_;
     std::vector<uint32_t> last_errors_, last_micro_, last_resolver_;
 };

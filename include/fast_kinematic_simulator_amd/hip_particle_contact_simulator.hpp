@@ -138,6 +138,45 @@ class RobotDescription {
     int32_t ConfigurationWidth() const {
         return type == FKS_ROBOT_SE2 ? 3 : (type == FKS_ROBOT_SE3 ? 12 : num_dofs);
     }
+    /* every byte the simulator receives (fields, tables and the sampled-actuator bins the
+     * pointers reach): equal fingerprints mean the same robot for the GPU */
+    std::vector<unsigned char> Fingerprint() const {
+        std::vector<unsigned char> out;
+        auto put = [&out](const void* p, size_t n) {
+            const unsigned char* b = static_cast<const unsigned char*>(p);
+            out.insert(out.end(), b, b + n);
+        };
+        auto put_size = [&put](size_t n) {
+            const uint64_t v = (uint64_t)n;
+            put(&v, sizeof(v));
+        };
+        put(&type, sizeof(type));
+        put(&num_links, sizeof(num_links));
+        put(&num_dofs, sizeof(num_dofs));
+        put(base_transform, sizeof(base_transform));
+        put_size(joints.size());
+        put(joints.data(), joints.size() * sizeof(fks_joint_desc));
+        put_size(geometry_link.size());
+        put(geometry_link.data(), geometry_link.size() * sizeof(int32_t));
+        put_size(geometry_point_offset.size());
+        put(geometry_point_offset.data(), geometry_point_offset.size() * sizeof(uint32_t));
+        put_size(points.size());
+        put(points.data(), points.size() * sizeof(double));
+        put_size(allowed_pairs.size());
+        put(allowed_pairs.data(), allowed_pairs.size() * sizeof(int32_t));
+        put_size(controllers.size());
+        put(controllers.data(), controllers.size() * sizeof(fks_dof_controller));
+        put_size(distance_weights.size());
+        put(distance_weights.data(), distance_weights.size() * sizeof(double));
+        put_size(sampled_actuators.size());
+        for (const fks_sampled_actuator& a : sampled_actuators) {
+            put(&a.num_bins, sizeof(a.num_bins));
+            put(&a.bin_elements, sizeof(a.bin_elements));
+            if (a.num_bins && a.bin_bounds) put(a.bin_bounds, 2 * (size_t)a.num_bins * sizeof(double));
+            if (a.num_bins && a.bin_samples) put(a.bin_samples, (size_t)a.num_bins * a.bin_elements * sizeof(double));
+        }
+        return out;
+    }
     fks_robot_desc View() const {
         fks_robot_desc d{};
         d.robot_type = type;
@@ -393,17 +432,21 @@ class HipParticleContactSimulator {
         void operator()(fks_context* c) const { fks_destroy(c); }
     };
     std::unique_ptr<fks_context, Destroy> ctx_;
-    const RobotDescription* robot_ = nullptr;
+    std::vector<unsigned char> robot_fingerprint_; /* the robot set last (RobotDescription::Fingerprint) */
     uint32_t forward_steps_ = 1; /* controller steps per simulation (SPCS:856): the trace's step capacity */
     double resolution_ = 0.0;
     std::string frame_ = "world";
     std::mt19937_64 rng_;
 
+    /* RobotDescription is a mutable value the caller owns, so the robot set last is
+     * recognised by content, never by address (a freed robot's address may be reused) */
     void SetRobot(const RobotDescription& robot) {
-        if (robot_ == &robot) return;
+        std::vector<unsigned char> fp = robot.Fingerprint();
+        if (!robot_fingerprint_.empty() && fp == robot_fingerprint_) return;
+        robot_fingerprint_.clear();
         const fks_robot_desc d = robot.View();
         check(fks_set_robot(ctx_.get(), &d), ctx_.get(), "fks_set_robot");
-        robot_ = &robot;
+        robot_fingerprint_ = std::move(fp);
     }
 
     std::vector<SimulationResult> Simulate(const RobotDescription& robot, const std::vector<Configuration>& starts,

@@ -1,22 +1,22 @@
 /*
- * tnuva_robot_models.hpp — the robot models the planner hands the simulator,
- * re-declared over the flattened description the GPU uses.
+ * tnuva_robot_models.hpp — the robot models the planner hands the simulator.
  *
  * Reference: tnuva_robot_models::TnuvaSE2Robot / TnuvaSE3Robot / TnuvaLinkedRobot
- * (TNUVA:26-615): arc_utilities PointSphereBasic*Robot models plus per-DOF
- * SimplePIDController + TruncatedNormalUncertainVelocityActuator groups.  Here each
- * class keeps the same constructor arguments (TNUVA:109-132, 293-325, 486-517), the
- * same configuration type, position semantics (SetPosition enforces joint limits /
- * wraps angles; ResetPosition also zeroes the controllers, TNUVA:524-536), the
- * robot-model interface the simulator receives (SimpleRobotModelInterface: Clone,
- * GetPosition, SetPosition, ComputeConfigurationDistanceTo), and the controller state a
- * mutable robot carries between simulator calls.  Kinematics, noise and control run on
- * the GPU from the flattened fks::RobotDescription each model builds once
- * (HipDescription()); the planner never needs host FK from these classes.
+ * (TNUVA:26-615): arc_utilities PointSphereBasic*Robot models (TNUVA:27, 202, 416) plus
+ * per-DOF SimplePIDController + TruncatedNormalUncertainVelocityActuator groups.  Here each
+ * class derives from the same arc_utilities base (the real one in a planner workspace, the
+ * stand-in otherwise: fks_external_types.hpp), passes it the same constructor arguments
+ * (TNUVA:109-132, 293-325, 486-517), and instead of the host controllers and actuators
+ * carries what the GPU simulates from: the flattened fks::RobotDescription built once in
+ * the constructor (HipDescription(), shared by clones and owned through a shared_ptr, so
+ * a simulator may keep it as its cache key) and the controller state a mutable robot
+ * carries between simulator calls (ResetPosition zeroes it, TNUVA:524-536).
  */
 #ifndef FAST_KINEMATIC_SIMULATOR_AMD_TNUVA_ROBOT_MODELS_HPP
 #define FAST_KINEMATIC_SIMULATOR_AMD_TNUVA_ROBOT_MODELS_HPP
 
+#include <algorithm>
+#include <array>
 #include <cmath>
 #include <memory>
 #include <stdexcept>
@@ -24,28 +24,8 @@
 #include <utility>
 #include <vector>
 
+#include "fast_kinematic_simulator_amd/fks_external_types.hpp"
 #include "fast_kinematic_simulator_amd/hip_particle_contact_simulator.hpp"
-#include "fast_kinematic_simulator_amd/simulator_interface.hpp"
-#include "fks_portable_math.h"
-
-namespace simple_robot_models {
-
-/* PointSphereGeometry: link-frame points (x, y, z, w); POINTS use w = 1 (SPCS:930-932) */
-class PointSphereGeometry {
-  public:
-    enum MODEL_GEOMETRY_TYPE { POINTS, SPHERES };
-    PointSphereGeometry() : type_(POINTS), points_(std::make_shared<std::vector<fks_planner_types::Vector4d>>()) {}
-    PointSphereGeometry(const MODEL_GEOMETRY_TYPE type, const std::shared_ptr<const std::vector<fks_planner_types::Vector4d>>& points)
-        : type_(type), points_(points) {}
-    MODEL_GEOMETRY_TYPE GeometryType() const { return type_; }
-    const std::shared_ptr<const std::vector<fks_planner_types::Vector4d>>& Geometry() const { return points_; }
-
-  private:
-    MODEL_GEOMETRY_TYPE type_;
-    std::shared_ptr<const std::vector<fks_planner_types::Vector4d>> points_;
-};
-
-}  // namespace simple_robot_models
 
 namespace tnuva_robot_models {
 
@@ -54,6 +34,10 @@ inline std::vector<double> flatten_points(const simple_robot_models::PointSphere
     std::vector<double> xyzw;
     for (const auto& p : *g.Geometry()) xyzw.insert(xyzw.end(), {p(0), p(1), p(2), p(3)});
     return xyzw;
+}
+inline void row_major34(const fks_planner_types::Isometry3d& T, double* out) {
+    const std::array<double, 12> m = fks_ext::iso_to_row_major34(T);
+    std::copy(m.begin(), m.end(), out);
 }
 /* the per-axis gains of an SE2/SE3_ROBOT_CONFIG (TNUVA:43-107, 227-291) */
 template <typename C>
@@ -91,14 +75,15 @@ struct AXIS_ROBOT_CONFIG {
           r_max_actuator_minimum_noise(in_r_max_actuator_minimum_noise) {}
 };
 
-/* What the HIP simulator needs from a DerivedRobotType: the flattened description, the
- * PID state (per dof: error integral, then per dof: last error) and the conversion of
- * configurations to and from the flat form of fks_capi.h. */
+/* What the HIP simulator needs from a DerivedRobotType: the flattened description (owned,
+ * immutable after construction), the PID state (per dof: error integral, then per dof:
+ * last error) and the conversion of configurations to and from the flat form of fks_capi.h. */
 template <typename Configuration>
 class HipRobotState {
   public:
     virtual ~HipRobotState() {}
     const fks::RobotDescription& HipDescription() const { return *desc_; }
+    const std::shared_ptr<const fks::RobotDescription>& SharedHipDescription() const { return desc_; }
     const std::vector<double>& ControllerState() const { return pid_; }
     void SetControllerState(const std::vector<double>& state) {
         if (state.size() != pid_.size()) throw std::invalid_argument("controller state has the wrong size");
@@ -124,10 +109,8 @@ class HipRobotState {
 
 /* ---------------------------------------------------------------- SE(2) (TNUVA:26-199) */
 template <typename Generator>
-class TnuvaSE2Robot
-    : public simple_robot_model_interface::SimpleRobotModelInterface<simple_se2_robot_model::SimpleSE2Configuration,
-                                                                     simple_se2_robot_model::SimpleSE2ConfigAlloc>,
-      public HipRobotState<simple_se2_robot_model::SimpleSE2Configuration> {
+class TnuvaSE2Robot : public simple_robot_models::PointSphereBasicSE2Robot,
+                      public HipRobotState<simple_se2_robot_model::SimpleSE2Configuration> {
   public:
     typedef simple_se2_robot_model::SimpleSE2Configuration Configuration;
     typedef AXIS_ROBOT_CONFIG SE2_ROBOT_CONFIG;
@@ -136,7 +119,8 @@ class TnuvaSE2Robot
     TnuvaSE2Robot(const Configuration& initial_position, const double position_distance_weight,
                   const double rotation_distance_weight, const std::string& link_name,
                   const simple_robot_models::PointSphereGeometry& geometry, const SE2_ROBOT_CONFIG& robot_config)
-        : link_name_(link_name) {
+        : simple_robot_models::PointSphereBasicSE2Robot(initial_position, position_distance_weight, rotation_distance_weight,
+                                                        link_name, geometry) {
         auto d = std::make_shared<fks::RobotDescription>();
         d->type = FKS_ROBOT_SE2;
         d->num_links = 1;
@@ -145,44 +129,24 @@ class TnuvaSE2Robot
         d->controllers = {detail::translation(robot_config), detail::translation(robot_config), detail::rotation(robot_config)};
         d->distance_weights = {position_distance_weight, rotation_distance_weight};
         InitState(d);
-        SetPosition(initial_position);
     }
     simple_robot_model_interface::SimpleRobotModelInterface<Configuration, simple_se2_robot_model::SimpleSE2ConfigAlloc>* Clone()
         const override {
         return new TnuvaSE2Robot(*this);
-    }
-    const Configuration& GetPosition() const override { return config_; }
-    /* SetPosition: theta wrapped to [-pi, pi] */
-    const Configuration& SetPosition(const Configuration& config) override {
-        config_ = Configuration(config(0), config(1), fks_math::enforce_continuous_revolute_bounds(config(2)));
-        return config_;
     }
     /* TNUVA:139-150 */
     const Configuration& ResetPosition(const Configuration& position) {
         this->ResetControllers();
         return SetPosition(position);
     }
-    double ComputeConfigurationDistanceTo(const Configuration& t) const override {
-        const double dx = t(0) - config_(0), dy = t(1) - config_(1);
-        const double dr = fks_math::enforce_continuous_revolute_bounds(t(2) - config_(2));
-        const auto& w = this->HipDescription().distance_weights;
-        return w[0] * std::sqrt(dx * dx + dy * dy) + w[1] * std::fabs(dr);
-    }
     std::vector<double> ToFlat(const Configuration& c) const override { return {c(0), c(1), c(2)}; }
     Configuration FromFlat(const double* f) const override { return Configuration(f[0], f[1], f[2]); }
-    const std::string& GetLinkName() const { return link_name_; }
-
-  private:
-    std::string link_name_;
-    Configuration config_;
 };
 
 /* ---------------------------------------------------------------- SE(3) (TNUVA:201-413) */
 template <typename Generator>
-class TnuvaSE3Robot
-    : public simple_robot_model_interface::SimpleRobotModelInterface<simple_se3_robot_model::SimpleSE3Configuration,
-                                                                     simple_se3_robot_model::SimpleSE3ConfigAlloc>,
-      public HipRobotState<simple_se3_robot_model::SimpleSE3Configuration> {
+class TnuvaSE3Robot : public simple_robot_models::PointSphereBasicSE3Robot,
+                      public HipRobotState<simple_se3_robot_model::SimpleSE3Configuration> {
   public:
     typedef simple_se3_robot_model::SimpleSE3Configuration Configuration;
     typedef AXIS_ROBOT_CONFIG SE3_ROBOT_CONFIG;
@@ -191,7 +155,8 @@ class TnuvaSE3Robot
     TnuvaSE3Robot(const Configuration& initial_position, const double position_distance_weight,
                   const double rotation_distance_weight, const std::string& link_name,
                   const simple_robot_models::PointSphereGeometry& geometry, const SE3_ROBOT_CONFIG& robot_config)
-        : link_name_(link_name) {
+        : simple_robot_models::PointSphereBasicSE3Robot(initial_position, position_distance_weight, rotation_distance_weight,
+                                                        link_name, geometry) {
         auto d = std::make_shared<fks::RobotDescription>();
         d->type = FKS_ROBOT_SE3;
         d->num_links = 1;
@@ -201,48 +166,27 @@ class TnuvaSE3Robot
         d->controllers = {t, t, t, r, r, r};
         d->distance_weights = {position_distance_weight, rotation_distance_weight};
         InitState(d);
-        SetPosition(initial_position);
     }
     simple_robot_model_interface::SimpleRobotModelInterface<Configuration, simple_se3_robot_model::SimpleSE3ConfigAlloc>* Clone()
         const override {
         return new TnuvaSE3Robot(*this);
     }
-    const Configuration& GetPosition() const override { return config_; }
-    const Configuration& SetPosition(const Configuration& config) override {
-        config_ = config;
-        return config_;
-    }
     const Configuration& ResetPosition(const Configuration& position) {
         this->ResetControllers();
         return SetPosition(position);
     }
-    /* weighted translation distance + rotation angle between the poses */
-    double ComputeConfigurationDistanceTo(const Configuration& t) const override {
-        const double* a = config_.data34();
-        const double* b = t.data34();
-        const double dx = b[3] - a[3], dy = b[7] - a[7], dz = b[11] - a[11];
-        double trace = 0.0; /* trace(Ra^T Rb) */
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) trace += a[4 * r + c] * b[4 * r + c];
-        const double cosang = std::max(-1.0, std::min(1.0, 0.5 * (trace - 1.0)));
-        const auto& w = this->HipDescription().distance_weights;
-        return w[0] * std::sqrt(dx * dx + dy * dy + dz * dz) + w[1] * std::acos(cosang);
+    /* the 3x4 row-major [R | t] */
+    std::vector<double> ToFlat(const Configuration& c) const override {
+        const std::array<double, 12> m = fks_ext::iso_to_row_major34(c);
+        return std::vector<double>(m.begin(), m.end());
     }
-    std::vector<double> ToFlat(const Configuration& c) const override { return std::vector<double>(c.data34(), c.data34() + 12); }
-    Configuration FromFlat(const double* f) const override { return Configuration::FromRowMajor34(f); }
-    const std::string& GetLinkName() const { return link_name_; }
-
-  private:
-    std::string link_name_;
-    Configuration config_;
+    Configuration FromFlat(const double* f) const override { return fks_ext::iso_from_row_major34(f); }
 };
 
 /* ---------------------------------------------------------------- linked (TNUVA:415-615) */
 template <typename Generator>
-class TnuvaLinkedRobot
-    : public simple_robot_model_interface::SimpleRobotModelInterface<simple_linked_robot_model::SimpleLinkedConfiguration,
-                                                                     simple_linked_robot_model::SimpleLinkedConfigAlloc>,
-      public HipRobotState<simple_linked_robot_model::SimpleLinkedConfiguration> {
+class TnuvaLinkedRobot : public simple_robot_models::PointSphereBasicLinkedRobot,
+                         public HipRobotState<simple_linked_robot_model::SimpleLinkedConfiguration> {
   public:
     typedef simple_linked_robot_model::SimpleLinkedConfiguration Configuration;
 
@@ -270,18 +214,20 @@ class TnuvaLinkedRobot
                      const std::vector<double>& joint_distance_weights,
                      const std::vector<std::pair<std::string, simple_robot_models::PointSphereGeometry>>& link_geometries,
                      const std::vector<std::pair<size_t, size_t>>& allowed_self_collisions,
-                     const std::vector<LINKED_ROBOT_CONFIG>& joint_configs) {
+                     const std::vector<LINKED_ROBOT_CONFIG>& joint_configs)
+        : simple_robot_models::PointSphereBasicLinkedRobot(base_transform, links, joints, initial_position, joint_distance_weights,
+                                                           link_geometries, allowed_self_collisions) {
         auto d = std::make_shared<fks::RobotDescription>();
         d->type = FKS_ROBOT_LINKED;
         d->num_links = (int32_t)links.size();
-        for (int i = 0; i < 12; ++i) d->base_transform[i] = base_transform.data34()[i];
+        detail::row_major34(base_transform, d->base_transform);
         int32_t active = 0;
         for (const auto& j : joints) {
             fks_joint_desc jd{};
             jd.parent_link = (int32_t)j.parent_link_index;
             jd.child_link = (int32_t)j.child_link_index;
             jd.type = (int32_t)j.joint_model.GetType();
-            for (int i = 0; i < 12; ++i) jd.origin[i] = j.joint_transform.data34()[i];
+            detail::row_major34(j.joint_transform, jd.origin);
             for (int i = 0; i < 3; ++i) jd.axis[i] = j.joint_axis(i);
             jd.limit_lower = j.joint_model.GetLimits().first;
             jd.limit_upper = j.joint_model.GetLimits().second;
@@ -309,40 +255,22 @@ class TnuvaLinkedRobot
         d->distance_weights = joint_distance_weights;
         if (d->distance_weights.size() != (size_t)active) throw std::invalid_argument("one distance weight per active joint");
         InitState(d);
-        SetPosition(initial_position);
     }
     simple_robot_model_interface::SimpleRobotModelInterface<Configuration, simple_linked_robot_model::SimpleLinkedConfigAlloc>* Clone()
         const override {
         return new TnuvaLinkedRobot(*this);
-    }
-    const Configuration& GetPosition() const override { return config_; }
-    /* SetPosition: each active joint's model with the new value (limits / wrap enforced) */
-    const Configuration& SetPosition(const Configuration& config) override {
-        if (config.size() != joint_models_.size()) throw std::invalid_argument("configuration has the wrong number of joints");
-        config_.clear();
-        for (size_t k = 0; k < config.size(); ++k) config_.push_back(joint_models_[k].CopyWithNewValue(config[k].GetValue()));
-        return config_;
     }
     /* TNUVA:524-536 */
     const Configuration& ResetPosition(const Configuration& position) {
         this->ResetControllers();
         return SetPosition(position);
     }
-    /* weighted joint-space distance (the simulation shortcut's metric, SPCS:898) */
-    double ComputeConfigurationDistanceTo(const Configuration& t) const override {
-        const auto& w = this->HipDescription().distance_weights;
-        double sum = 0.0;
-        for (size_t k = 0; k < config_.size(); ++k) {
-            const double d = w[k] * std::fabs(config_[k].SignedDistance(t[k].GetValue()));
-            sum += d * d;
-        }
-        return std::sqrt(sum);
-    }
     std::vector<double> ToFlat(const Configuration& c) const override {
         std::vector<double> f;
         for (const auto& j : c) f.push_back(j.GetValue());
         return f;
     }
+    /* each active joint's model with the value (limits / wrap enforced, TNUVA:556) */
     Configuration FromFlat(const double* f) const override {
         Configuration c;
         for (size_t k = 0; k < joint_models_.size(); ++k) c.push_back(joint_models_[k].CopyWithNewValue(f[k]));
@@ -351,7 +279,6 @@ class TnuvaLinkedRobot
 
   private:
     std::vector<simple_linked_robot_model::SimpleJointModel> joint_models_; /* active joints, in order */
-    Configuration config_;
 };
 
 }  // namespace tnuva_robot_models

@@ -43,7 +43,9 @@
 extern "C" {
 #endif
 
-#define FKS_ABI_VERSION 4
+/* 5: the opt-in joint-space proof (ABI 4: fks_set_joint_proof, fks_call_counters.
+ * proven_free_microsteps) removed: it broke even on the headline */
+#define FKS_ABI_VERSION 5
 
 typedef enum {
     FKS_OK = 0,
@@ -217,9 +219,7 @@ typedef struct {
                                        non-empty, i.e. ExtractSelfCollidingPoints produced corrections (SPCS:1264-1271) */
     uint64_t self_corrected_points; /* sum over resolver iterations of the points whose correction holds a
                                        self-collision term (SPCS:1846-1853, 1909-1916) */
-    /* ABI 4: microsteps whose CheckCollision (SPCS:1600-1602) the joint-space proof settled
-     * without FK or grid reads (fks_set_joint_proof); the results are those of the full check */
-    uint64_t proven_free_microsteps;
+    uint64_t reserved0;             /* ABI 4's proven_free_microsteps (removed in ABI 5); always 0 */
 } fks_call_counters;
 
 typedef struct fks_context fks_context;
@@ -436,18 +436,6 @@ fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_
  * FKS.cpp:22,45,68 hard-wire, the default), 1 = ComputeResolverCorrectionStepIndividualJacobians
  * (SPCS:1966-1988: one ColPivHouseholderQR solve per corrected point, summed in point order). */
 fks_status fks_set_individual_jacobians(fks_context* ctx, int32_t simulate_with_individual_jacobians);
-/* Joint-space proof of free microsteps (ABI 4; default 0 = off; linked robots; no
- * reference counterpart, results are bit-identical either way).  After a controller step
- * whose last collision check came back free, the kernel keeps that configuration as an
- * anchor and, per link, how far the link's points may move from there with the environment
- * check (the per-round SDF proofs) and the self-collision check (the gap between disallowed
- * geometries' cell boxes) still provably free.  The next step's microsteps whose joint
- * motion from the anchor, weighted by per-(link, dof) lever bounds, stays inside every
- * link's slack are free without their FK and grid reads (fks_simulate_linked_jp).  Off by
- * default: on the cfg3 headline it proves a third of the microsteps and cuts the issued
- * instructions, but the extra code costs the monolithic kernel registers and the launch
- * ends later. */
-fks_status fks_set_joint_proof(fks_context* ctx, int32_t enable);
 
 /* sums over every call since fks_create / fks_reset_total_counters */
 fks_status fks_get_total_counters(const fks_context* ctx, fks_call_counters* out);

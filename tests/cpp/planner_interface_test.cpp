@@ -18,6 +18,8 @@
 #include <memory>
 #include <sstream>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "fast_kinematic_simulator_amd/fast_kinematic_simulator.hpp"
@@ -26,6 +28,8 @@ namespace upc = uncertainty_planning_core;
 using fks_planner_types::Isometry3d;
 using fks_planner_types::Vector3d;
 using fks_planner_types::Vector4d;
+/* the point container PointSphereGeometry holds (EigenHelpers::VectorVector4d in a planner workspace) */
+typedef std::remove_cv<std::remove_reference<decltype(*std::declval<simple_robot_models::PointSphereGeometry>().Geometry())>::type>::type Points;
 
 struct Reader {
     std::ifstream in;
@@ -46,7 +50,7 @@ struct Reader {
     Isometry3d iso() {
         double m[12];
         for (double& v : m) v = num();
-        return Isometry3d::FromRowMajor34(m);
+        return fks_ext::iso_from_row_major34(m);
     }
     /* one value per call, in file order (function-argument evaluation order is unspecified) */
     Vector3d vec3() {
@@ -113,16 +117,17 @@ static Scene read_common(Reader& r) {
 
 static simple_robot_models::PointSphereGeometry read_points(Reader& r) {
     const int64_t n = r.integer();
-    auto pts = std::make_shared<std::vector<Vector4d>>();
+    auto pts = std::make_shared<Points>();
     for (int64_t i = 0; i < n; ++i) pts->push_back(r.vec4());
     return simple_robot_models::PointSphereGeometry(simple_robot_models::PointSphereGeometry::POINTS, pts);
 }
 
 /* --dump: the flattened robot the GPU receives and the flat starts / targets (no GPU needed) */
 static bool g_dump = false;
-template <typename Config, typename Robot>
-static int dump(const Robot& robot, const std::vector<Config>& starts, const std::vector<Config>& targets) {
+template <typename Configs, typename Robot>
+static int dump(const Robot& robot, const Configs& starts, const Configs& targets) {
     const fks::RobotDescription& d = robot.HipDescription();
+    std::printf("types %s\n", FKS_EXTERNAL_PLANNER_TYPES ? "workspace" : "standalone"); /* fks_external_types.hpp */
     std::printf("type %d links %d dofs %d\nbase", (int)d.type, d.num_links, d.num_dofs);
     for (double v : d.base_transform) hex(v);
     std::printf("\njoints");
@@ -278,7 +283,39 @@ int main(int argc, char** argv) {
             if (g_dump) return dump(*robot, starts, targets);
             upc::LinkedSimulatorPtr sim = fast_kinematic_simulator::MakeLinkedSimulator(
                 E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
-            return exercise<upc::LinkedConfig, upc::LinkedConfigAlloc>(s, sim, robot, starts, targets);
+            const int rc = exercise<upc::LinkedConfig, upc::LinkedConfigAlloc>(s, sim, robot, starts, targets);
+            if (rc != 0) return rc;
+            /* Two robots alternating on one simulator, each destroyed before the next is made
+             * (call indices 5-8): "other" keeps only the first point of every geometry, "same"
+             * is rebuilt from the scene's arguments and must reproduce the oracle's run of the
+             * scene robot; a simulator that recognised robots by address could hand a new robot
+             * a destroyed one's tables. */
+            auto make_other = [&]() {
+                std::vector<std::pair<std::string, simple_robot_models::PointSphereGeometry>> one;
+                for (const auto& g : geoms) {
+                    auto pts = std::make_shared<Points>(1, g.second.Geometry()->front());
+                    one.emplace_back(g.first, simple_robot_models::PointSphereGeometry(simple_robot_models::PointSphereGeometry::POINTS, pts));
+                }
+                return std::make_shared<Robot>(base, links, joints, initial, weights, one, allowed, ctrl);
+            };
+            typedef simple_simulator_interface::SimulatorInterface<upc::LinkedConfig, upc::PRNG, upc::LinkedConfigAlloc> Interface;
+            auto print_alt = [&](const char* tag, int call, const std::vector<Interface::SimulationResult>& res) {
+                for (size_t i = 0; i < res.size(); ++i) {
+                    std::printf("%s %d %zu", tag, call, i);
+                    for (double v : robot->ToFlat(res[i].result_config)) hex(v);
+                    std::printf(" %d\n", res[i].did_contact ? 1 : 0);
+                }
+            };
+            for (int call = 5; call < 9; call += 2) {
+                {
+                    std::shared_ptr<Interface::BaseRobotType> other = make_other();
+                    print_alt("alt_other", call, sim->ForwardSimulateRobots(other, starts, targets, s.allow, {}));
+                }
+                std::shared_ptr<Interface::BaseRobotType> same =
+                    std::make_shared<Robot>(base, links, joints, initial, weights, geoms, allowed, ctrl);
+                print_alt("alt_same", call + 1, sim->ForwardSimulateRobots(same, starts, targets, s.allow, {}));
+            }
+            return 0;
         }
         /* SE(2) / SE(3): pos weight, rot weight, points, the 18 gains of the config */
         const double pw = r.num(), rw = r.num();
@@ -311,7 +348,7 @@ int main(int argc, char** argv) {
         auto read_configs = [&](const char* tag) {
             r.expect(tag);
             const int64_t n = r.integer();
-            std::vector<upc::SE3Config> v;
+            std::vector<upc::SE3Config, upc::SE3ConfigAlloc> v; /* Eigen::aligned_allocator in the planner (UPC.cpp:131) */
             for (int64_t i = 0; i < n; ++i) {
                 const std::vector<double> f = r.nums(12);
                 v.push_back(robot->FromFlat(f.data()));

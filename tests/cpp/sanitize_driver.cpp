@@ -95,7 +95,7 @@ int main() {
         jt.parent_link_index = j;
         jt.child_link_index = j + 1;
         const double o[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, j == 0 ? 0.05 : 0.2};
-        jt.joint_transform = fks_planner_types::Isometry3d::FromRowMajor34(o);
+        jt.joint_transform = fks_ext::iso_from_row_major34(o);
         jt.joint_axis = fks_planner_types::Vector3d(0.0, 1.0, 0.0);
         jt.joint_model = simple_linked_robot_model::SimpleJointModel(
             {-2.5, 2.5}, 0.0, j == 2 ? simple_linked_robot_model::SimpleJointModel::CONTINUOUS : simple_linked_robot_model::SimpleJointModel::REVOLUTE);

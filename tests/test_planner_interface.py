@@ -96,9 +96,9 @@ def _hexrow(row):
     return np.array([float.fromhex(v) for v in row])
 
 
-def _run(name):
+def _run(name, workspace=False):
     family, wl, obstacles, grid = _scene(name)
-    exe = build_planner_test()
+    exe = build_planner_test(workspace=workspace)
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "scene.txt")
         _write_scene(path, family, wl, obstacles, grid)
@@ -106,18 +106,28 @@ def _run(name):
     return p, family, wl, obstacles, grid
 
 
-@pytest.mark.parametrize("name", ["linked", "se2", "se3"])
-def test_planner_robot_flattens_like_python(name):
-    """The TNUVA constructors of the C++ drop-in flatten the robot exactly as the Python
-    mirror does (the description the GPU receives), and configurations convert losslessly."""
+def _dump(name, workspace=False):
     family, wl, obstacles, grid = _scene(name)
-    exe = build_planner_test()
+    exe = build_planner_test(workspace=workspace)
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "scene.txt")
         _write_scene(path, family, wl, obstacles, grid)
         p = subprocess.run([exe, path, "--dump"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
     assert p.returncode == 0, p.stderr
-    rows = {line.split()[0]: line.split()[1:] for line in p.stdout.splitlines()}
+    return p.stdout
+
+
+@pytest.mark.parametrize("workspace", [False, True], ids=["standalone", "workspace"])
+@pytest.mark.parametrize("name", ["linked", "se2", "se3"])
+def test_planner_robot_flattens_like_python(name, workspace):
+    """The TNUVA constructors of the C++ drop-in flatten the robot exactly as the Python
+    mirror does (the description the GPU receives), and configurations convert losslessly —
+    with the stand-in planner types and inside the (mock) planner workspace, where the
+    robots derive from the workspace's PointSphereBasic*Robot and SE(3) configurations use
+    Eigen::aligned_allocator (fks_external_types.hpp)."""
+    family, wl, obstacles, grid = _scene(name)
+    rows = {line.split()[0]: line.split()[1:] for line in _dump(name, workspace).splitlines()}
+    assert rows["types"] == ["workspace" if workspace else "standalone"]
     r = wl.robot
     hx = lambda key: _hexrow(rows[key]) if rows[key] else np.zeros(0)
     assert int(rows["type"][0]) == r.robot_type and int(rows["type"][-1]) == r.num_dofs
@@ -142,21 +152,24 @@ def test_planner_robot_flattens_like_python(name):
             assert np.array_equal(_hexrow(f[18:20]), np.array([jt.lower, jt.upper]))
 
 
-def test_planner_program_builds_and_reads_scene():
+@pytest.mark.parametrize("workspace", [False, True], ids=["standalone", "workspace"])
+def test_planner_program_builds_and_reads_scene(workspace):
     """g++ over the public headers only; without a GPU the factory reports FKS_ERR_NO_DEVICE
-    (exit 3) after the scene and the environment were read and built."""
-    p, *_ = _run("linked")
+    (exit 3) after the scene and the environment were read and built (in the workspace build,
+    through the workspace's sdf_tools: SetValue + ExtractSignedDistanceField, SEB.cpp:148-153, 473)."""
+    p, *_ = _run("linked", workspace)
     assert p.returncode in (0, 3), p.stderr
     if p.returncode == 3:
         assert "no HIP device" in p.stderr
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("workspace", [False, True], ids=["standalone", "workspace"])
 @pytest.mark.parametrize("name", ["linked", "se2", "se3"])
-def test_planner_interface_matches_oracle(fks_lib, oracle_lib, name):
+def test_planner_interface_matches_oracle(fks_lib, oracle_lib, name, workspace):
     import oracle
 
-    p, family, wl, obstacles, (res, origin, cells) = _run(name)
+    p, family, wl, obstacles, (res, origin, cells) = _run(name, workspace)
     assert p.returncode == 0, p.stderr
     rows = _parse(p.stdout)
     env = build_complete_environment(obstacles, res, origin=origin, num_cells=cells)
@@ -199,4 +212,45 @@ def test_planner_interface_matches_oracle(fks_lib, oracle_lib, name):
     assert np.any(state != 0.0)
     # display helpers
     mk = rows["markers"][0]
-    assert int(mk[0]) == 1 and int(mk[1]) == wl.robot.num_points and mk[2] == "world"
+    assert int(mk[0]) == 1 and int(mk[1]) == wl.robot.num_points and mk[2] == "uncertainty_planning_simulator"
+    if family == "linked":
+        # two robots alternating on one simulator, each destroyed before the next is made
+        # (planner_interface_test.cpp, call indices 5-8): the rebuilt scene robot reproduces
+        # the oracle bit for bit every time, and the one-point robot really was simulated
+        for call in (6, 8):
+            o = run(wl.starts, wl.targets, call)
+            got = [r for r in rows["alt_same"] if int(r[0]) == call]
+            assert len(got) == len(wl.starts)
+            assert np.array_equal(np.array([_hexrow(r[2:2 + W_]) for r in got]), o["positions"]), call
+            assert [int(r[2 + W_]) for r in got] == [int(v) for v in o["collided"]]
+        other = np.array([_hexrow(r[2:2 + W_]) for r in rows["alt_other"] if int(r[0]) == 5])
+        same5 = run(wl.starts, wl.targets, 5)["positions"]
+        assert other.shape == same5.shape and not np.array_equal(other, same5)
+
+
+@pytest.mark.parametrize("name", ["linked", "se2", "se3"])
+def test_workspace_and_standalone_builds_agree(name):
+    """The same program built against the stand-ins and inside the (mock) planner workspace
+    hands the GPU the same robot, starts and targets, byte for byte."""
+    a = [l for l in _dump(name, False).splitlines() if not l.startswith("types")]
+    b = [l for l in _dump(name, True).splitlines() if not l.startswith("types")]
+    assert a == b
+
+
+def test_standalone_types_collide_with_a_workspace():
+    """Why the switch exists: forcing the stand-ins while the workspace's headers are included
+    redeclares the workspace's names and does not compile; the default (no macro) compiles."""
+    from fast_kinematic_simulator_amd.build import MOCK_WORKSPACE, ROOT
+
+    src = ("#include <uncertainty_planning_core/uncertainty_planning_core.hpp>\n"
+           "#include \"fast_kinematic_simulator_amd/fast_kinematic_simulator.hpp\"\n"
+           "int main() { uncertainty_planning_core::SE3SimulatorPtr p; return p ? 1 : 0; }\n")
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "t.cpp")
+        with open(path, "w") as f:
+            f.write(src)
+        base = ["g++", "-std=c++17", "-fsyntax-only", f"-I{MOCK_WORKSPACE}", f"-I{os.path.join(ROOT, 'include')}", path]
+        ok = subprocess.run(base, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        assert ok.returncode == 0, ok.stdout[-3000:]
+        bad = subprocess.run(base + ["-DFKS_STANDALONE_PLANNER_TYPES"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        assert bad.returncode != 0 and "redefinition" in bad.stdout
