@@ -174,7 +174,6 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=4096, help="particles in the CPU-baseline sample (SURVEY §8d: 4096)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config-check", action="store_true", help="skip the batched CheckConfigCollision line")
-    ap.add_argument("--joint-proof", action="store_true", help="A/B: the joint-space proof of free microsteps (off by default)")
     ap.add_argument("--segment-steps", type=int, default=-1, help="A/B: fks_set_segment_steps (default: automatic)")
     args = ap.parse_args()
 
@@ -213,8 +212,6 @@ def main():
     log(f"[rank {rank}] environment {env_stats['cells']} cells built on the GPU in {env_stats['gpu_ms']:.1f} ms device "
         f"time ({time.perf_counter() - t0:.2f}s call, {env_stats['normal_entries']} surface-normal entries)")
     sim = make_linked_simulator(denv, wl.solver, wl.controller_frequency, wl.seed, device=local_rank)
-    if args.joint_proof:
-        sim.set_joint_proof(True)
     if args.segment_steps >= 0:
         sim.set_segment_steps(args.segment_steps)
     sim.set_robot(wl.robot)
@@ -343,7 +340,6 @@ def main():
                 "resolver_iterations_per_step": tot["resolver_iterations"] / calls * world,
                 "mean_least_squares_rows": tot["least_squares_rows"] / max(1, tot["resolver_iterations"]),
                 "error_particles": tot["error_particles"],
-                "proven_free_microsteps_fraction": tot.get("proven_free_microsteps", 0) / max(1, tot["microsteps"]),
             },
             "roofline": {
                 "bound": "hbm",

@@ -165,7 +165,7 @@ class CallCounters(ctypes.Structure):
         ("least_squares_rows", c_uint64),
         ("self_collision_checks", c_uint64),
         ("self_corrected_points", c_uint64),
-        ("proven_free_microsteps", c_uint64),
+        ("reserved0", c_uint64),  # ABI 4: proven_free_microsteps
     ]
 
     def as_dict(self):
@@ -266,7 +266,6 @@ PROTOTYPES = [
     ("fks_set_segment_steps", c_int32, [c_void_p, c_uint32]),
     ("fks_set_segment_policy", c_int32, [c_void_p, c_uint32, c_uint32]),
     ("fks_set_individual_jacobians", c_int32, [c_void_p, c_int32]),
-    ("fks_set_joint_proof", c_int32, [c_void_p, c_int32]),
     ("fks_env_build", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), POINTER(c_void_p)]),
     ("fks_env_build_gpu", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), c_int32,
                                     POINTER(c_void_p), POINTER(EnvBuildStats)]),
@@ -319,9 +318,15 @@ def lib():
                 "(there is no CPU fallback for the HIP path)"
             )
         handle = ctypes.CDLL(LIB_PATH)
-        variant = "FKS_LIB_PATH" in os.environ  # tools/variant_bench.py: older builds may lack newer entries
+        # tools/variant_bench.py compares older builds, which may lack newer entries: only
+        # there (FKS_VARIANT_LIB=1) are missing symbols skipped; otherwise they fail the load
+        variant = os.environ.get("FKS_VARIANT_LIB") == "1"
+        missing = [name for name, _, _ in PROTOTYPES if not hasattr(handle, name)]
+        if missing and not variant:
+            raise RuntimeError(f"{LIB_PATH} lacks {len(missing)} symbol(s) of include/fks_capi.h: {', '.join(missing)} "
+                               "(a stale build? rebuild with fast_kinematic_simulator_amd/build.py)")
         for name, restype, argtypes in PROTOTYPES:
-            if variant and not hasattr(handle, name):
+            if not hasattr(handle, name):
                 continue
             fn = getattr(handle, name)
             fn.restype = restype

@@ -30,7 +30,6 @@ extern "C" __global__ void fks_simulate_linked(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se2(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se3(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_indiv(const fksd::SimArgs* args);
-extern "C" __global__ void fks_simulate_linked_jp(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se2_indiv(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se3_indiv(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_traced(const fksd::SimArgs* args);
@@ -207,7 +206,6 @@ struct fks_context {
     float oob = 0.0f;
     int32_t has_normals = 0;
     int32_t skip_enabled = 0;
-    bool sdf_euclid = false; /* the SDF came from the GPU builder: an exact EDT of its sign */
     double skip_lplus = 0.0, skip_cmax = 0.0;
     /* robot */
     bool has_robot = false;
@@ -249,8 +247,6 @@ struct fks_context {
     uint32_t heavy_priority = 1;
     int32_t individual_jacobians = 0; /* fks_set_individual_jacobians (SPCS:420-423) */
     bool fk_pair = false;             /* paired FK of free microsteps (fks_set_robot) */
-    bool jp_layout = false;           /* LDS holds the joint-space proof's anchor and slack (fks_set_robot) */
-    int32_t joint_proof = 0;          /* fks_set_joint_proof (off by default: DESIGN.md §4.3) */
     double* d_seg_state = nullptr;
     uint32_t* d_seg_done = nullptr;
     size_t cap_seg_state = 0, cap_seg_done = 0;
@@ -409,9 +405,6 @@ static fks_status create_impl(const fks_environment* henv, const fks_device_env*
             return bail(e, "sdf copy");
         analyzed = fks_env::analyze_sdf_device(ctx->d_sdf, denv->geometry.num_cells[0], denv->geometry.num_cells[1],
                                                denv->geometry.num_cells[2], denv->geometry.resolution, &lp, &cm);
-        /* fks_env_build_device: sqrt(d_filled) res - sqrt(d_free) res over exact squared
-         * integer distances (fks_env_gpu.hip env_sdf), i.e. an exact EDT of its own sign */
-        ctx->sdf_euclid = analyzed;
         if ((e = hipMalloc((void**)&ctx->d_noff, (cells + 1) * sizeof(uint32_t))) != hipSuccess) return bail(e, "offsets");
         if ((e = hipMemcpy(ctx->d_noff, denv->offsets, (cells + 1) * sizeof(uint32_t), hipMemcpyDeviceToDevice)) != hipSuccess)
             return bail(e, "offsets copy");
@@ -477,12 +470,11 @@ const char* fks_get_last_error(const fks_context* ctx) { return ctx ? ctx->last_
 
 int32_t fks_config_width(const fks_context* ctx) { return (ctx && ctx->has_robot) ? ctx->R.W : 0; }
 
-/* Launch geometry of the current robot: the LDS layout (the paired FK's second set of
- * joint motion matrices, linked chains of <= 32 joints; the joint-space proof's anchor,
- * slack and box regions when fks_set_joint_proof is on), workgroup size, resident
- * workgroups per CU and the per-wave workspace.  Either extra region is taken only when
- * the occupancy it leaves equals the plain layout's. */
-static hipError_t launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
+/* Launch geometry of the current robot: the LDS layout (with the paired FK's second set
+ * of joint motion matrices for linked chains of <= 32 joints when the occupancy it leaves
+ * equals the plain layout's), workgroup size, resident workgroups per CU and the per-wave
+ * workspace.  Computed into locals and committed to ctx only when all of it succeeds. */
+static fks_status launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
     const int P = R.P, G = R.G;
     auto blocks = [&](const fksd::LdsLayout& l, uint32_t* wpg, size_t* bytes) -> int {
         uint32_t w = fksd::kWavesPerGroup;
@@ -504,70 +496,45 @@ static hipError_t launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
     uint32_t wpg = 0;
     size_t bytes = 0;
     const bool linked_pairable = R.type == FKS_ROBOT_LINKED && R.J >= 1 && R.J <= 32;
-    const bool jp_want = R.jp_ok && ctx->joint_proof;
-    fksd::LdsLayout L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds);
-    const int w0 = blocks(L, &wpg, &bytes);
-    /* the paired FK: when it keeps the plain layout's occupancy */
-    bool pair = false, jp = false;
-    size_t base_bytes = bytes;
+    const int w0 = blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds), &wpg, &bytes);
+    bool pair = false;
     if (linked_pairable && w0 > 0) {
         uint32_t w = 0;
         size_t b = 0;
-        if (blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, true), &w, &b) >= w0) {
-            pair = true;
-            base_bytes = b;
-        }
+        pair = blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, true), &w, &b) >= w0;
     }
-    /* the joint-space proof: only in no more LDS than the layout above plus its anchor and
-     * slack (measured: a layout the occupancy query admits at 5 workgroups per CU but 1.3 KB
-     * larger ran the fifth workgroup late), with the paired FK if that fits, else without */
-    if (jp_want && w0 > 0) {
-        const size_t allow = base_bytes + (size_t)fksd::kWavesPerGroup * (size_t)(R.D + R.L + 2) * sizeof(double);
-        for (int v = 0; v < 2 && !jp; ++v) {
-            const bool tp = pair && v == 0;
-            if (v == 1 && !pair) break;
-            uint32_t w = 0;
-            size_t b = 0;
-            if (blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, tp, true), &w, &b) >= w0 && b <= allow) {
-                jp = true;
-                pair = tp;
-            }
-        }
-    }
-    L = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, pair, jp);
-    const int waves_per_cu = blocks(L, &wpg, &bytes);
-    ctx->fk_pair = pair;
-    ctx->jp_layout = jp;
-    ctx->waves_per_group = wpg;
-    ctx->lds_bytes = bytes;
-    if (waves_per_cu < 1) return hipErrorInvalidValue;
+    const int waves_per_cu = blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, pair), &wpg, &bytes);
+    if (waves_per_cu < 1)
+        return fail(ctx, FKS_ERR_UNSUPPORTED,
+                    "robot too large: one wave's LDS block (" + std::to_string(bytes) + " bytes) does not fit a CU");
     int cus = 0;
-    hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    if (e != hipSuccess) return e;
-    ctx->grid_groups = (uint32_t)(cus * (waves_per_cu / (int)wpg));
-    ctx->grid_waves = ctx->grid_groups * ctx->waves_per_group;
-    ctx->scratch_per_wave = fksd::make_scratch_layout(3u * P, R.D, (int)P, G).total;
+    HIP_TRY(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    uint32_t grid_groups = (uint32_t)(cus * (waves_per_cu / (int)wpg));
+    const uint64_t scratch_per_wave = fksd::make_scratch_layout(3u * P, R.D, (int)P, G).total;
     /* the per-wave workspace grows with 3P x D (the stacked Jacobian) and the robot's
      * geometry count: for very large robots the persistent grid keeps only as many waves
      * as half the free HBM holds (the ticket queue hands out the work either way) */
     size_t free_b = 0, total_b = 0;
-    if ((e = hipMemGetInfo(&free_b, &total_b)) != hipSuccess) return e;
+    HIP_TRY(ctx, hipMemGetInfo(&free_b, &total_b));
     free_b += ctx->cap_scratch * sizeof(double); /* the current workspace is given back below */
-    const size_t per_group = (size_t)ctx->waves_per_group * ctx->scratch_per_wave * sizeof(double);
+    const size_t per_group = (size_t)wpg * scratch_per_wave * sizeof(double);
     const size_t max_groups = std::max<size_t>(1, (free_b / 2) / std::max<size_t>(1, per_group));
-    if ((size_t)ctx->grid_groups > max_groups) {
-        ctx->grid_groups = (uint32_t)max_groups;
-        ctx->grid_waves = ctx->grid_groups * ctx->waves_per_group;
-    }
-    const size_t words = (size_t)ctx->grid_waves * ctx->scratch_per_wave;
+    if ((size_t)grid_groups > max_groups) grid_groups = (uint32_t)max_groups;
+    const size_t words = (size_t)grid_groups * wpg * scratch_per_wave;
     if (words > ctx->cap_scratch || !ctx->d_scratch) {
         if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
         ctx->d_scratch = nullptr;
         ctx->cap_scratch = 0;
-        if ((e = hipMalloc((void**)&ctx->d_scratch, words * sizeof(double))) != hipSuccess) return e;
+        HIP_TRY(ctx, hipMalloc((void**)&ctx->d_scratch, words * sizeof(double)));
         ctx->cap_scratch = words;
     }
-    return hipSuccess;
+    ctx->fk_pair = pair;
+    ctx->waves_per_group = wpg;
+    ctx->lds_bytes = bytes;
+    ctx->grid_groups = grid_groups;
+    ctx->grid_waves = grid_groups * wpg;
+    ctx->scratch_per_wave = scratch_per_wave;
+    return FKS_OK;
 }
 
 fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
@@ -769,45 +736,6 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
             lever[k] = (std::fabs(an - 1.0) < 1e-12 && std::isfinite(worst)) ? worst * (1.0 + 1e-9) + 1e-12 : HUGE_VAL;
         }
     }
-    /* per (link, dof): the lever bound over link l's points only (reach from dof d's joint
-     * frame down to link l + |p|; |axis| for prismatic joints), 0 if d does not move l */
-    std::vector<double> link_lever((size_t)std::max(1, R.L) * (size_t)std::max(1, R.D), 0.0);
-    if (d->robot_type == FKS_ROBOT_LINKED) {
-        for (int k = 0; k < R.D; ++k) {
-            const int jd = dof_joint[k];
-            const double* ax = joints[jd].axis;
-            const double an = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
-            for (int g = 0; g < G; ++g) {
-                const int l = d->geometry_link[g];
-                if (!((link_mask[l] >> k) & 1ull)) continue;
-                double& out = link_lever[(size_t)l * R.D + k];
-                if (!std::isfinite(lever[k])) {
-                    out = HUGE_VAL;
-                    continue;
-                }
-                if (joints[jd].type == FKS_JOINT_PRISMATIC) {
-                    out = lever[k];
-                    continue;
-                }
-                double reach = 0.0;
-                for (int cur = l; cur != joints[jd].child;) {
-                    const JointDev& jp = joints[link_parent_joint[cur]];
-                    reach += std::sqrt(jp.origin[3] * jp.origin[3] + jp.origin[7] * jp.origin[7] + jp.origin[11] * jp.origin[11]);
-                    if (jp.type == FKS_JOINT_PRISMATIC)
-                        reach += std::max(std::fabs(jp.lo), std::fabs(jp.hi)) *
-                                 std::sqrt(jp.axis[0] * jp.axis[0] + jp.axis[1] * jp.axis[1] + jp.axis[2] * jp.axis[2]);
-                    cur = jp.parent;
-                }
-                double worst = 0.0;
-                for (uint32_t i = d->geometry_point_offset[g]; i < d->geometry_point_offset[g + 1]; ++i) {
-                    const double* p = d->points + 4 * (size_t)i;
-                    worst = std::max(worst, reach + std::sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]));
-                }
-                const double b = (std::fabs(an - 1.0) < 1e-12 && std::isfinite(worst)) ? worst * (1.0 + 1e-9) + 1e-12 : HUGE_VAL;
-                out = std::max(out, b);
-            }
-        }
-    }
     std::vector<double> weights;
     if (d->robot_type == FKS_ROBOT_LINKED) {
         for (int k = 0; k < R.D; ++k) weights.push_back(d->distance_weights ? d->distance_weights[k] : 1.0);
@@ -860,8 +788,6 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     HIP_TRY(ctx, up(&drounds, rounds.data(), rounds.size()));
     double* dlever = nullptr;
     HIP_TRY(ctx, up(&dlever, lever.data(), lever.size()));
-    double* dllever = nullptr;
-    HIP_TRY(ctx, up(&dllever, link_lever.data(), link_lever.size()));
     R.joints = dj;
     R.geom_link = dgl;
     R.geom_off = dgo;
@@ -878,7 +804,6 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     R.weights = dw;
     R.rounds = drounds;
     R.dof_lever = dlever;
-    R.link_lever = dllever;
     R.sampled_mask = 0;
     R.sampled = nullptr;
     if (d->sampled_actuators) {
@@ -900,19 +825,10 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
         HIP_TRY(ctx, up(&dsd, sd.data(), sd.size()));
         R.sampled = dsd;
     }
-    /* joint-space proof of free microsteps: every 64-point round on one
-     * link with w = 1 points (the per-round SDF proofs it extends), at most 64 rounds (the
-     * skip masks), finite lever bounds and w = 1 geometry boxes (the self-collision gap) */
-    R.jp_ok = 0;
-    if (d->robot_type == FKS_ROBOT_LINKED && NR >= 1 && NR <= 64 && R.L <= 64) {
-        bool ok = true;
-        for (int r = 0; r < NR; ++r) ok = ok && rounds[r].link >= 0;
-        for (int k = 0; k < R.D; ++k) ok = ok && std::isfinite(lever[k]);
-        for (double v : link_lever) ok = ok && std::isfinite(v);
-        for (int g = 0; g < G; ++g) ok = ok && box[7 * g + 6] == 1.0;
-        R.jp_ok = ok ? 1 : 0;
+    {
+        const fks_status st = launch_layout(ctx, R);
+        if (st != FKS_OK) return st; /* has_robot stays false (free_robot above) */
     }
-    HIP_TRY(ctx, launch_layout(ctx, R));
     ctx->R = R;
     ctx->has_robot = true;
     return FKS_OK;
@@ -951,7 +867,6 @@ static fks_status settle(fks_context* ctx) {
     ctx->last.least_squares_rows = c[fksd::kCntLsqRows];
     ctx->last.self_collision_checks = c[fksd::kCntSelfChecks];
     ctx->last.self_corrected_points = c[fksd::kCntSelfPoints];
-    ctx->last.proven_free_microsteps = c[fksd::kCntProvenMicro];
     for (int k = 0; k < FKS_NUM_PHASES; ++k) {
         ctx->phase_last[k] = c[fksd::kPhaseBase + k];
         ctx->phase_total[k] += ctx->phase_last[k];
@@ -970,7 +885,6 @@ static fks_status settle(fks_context* ctx) {
     ctx->total.least_squares_rows += ctx->last.least_squares_rows;
     ctx->total.self_collision_checks += ctx->last.self_collision_checks;
     ctx->total.self_corrected_points += ctx->last.self_corrected_points;
-    ctx->total.proven_free_microsteps += ctx->last.proven_free_microsteps;
     ctx->total.kernel_ms += ctx->last.kernel_ms;
     ctx->total.call_ms += ctx->last.call_ms;
     ctx->total.calls += 1;
@@ -1024,7 +938,6 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.skip_enabled = ctx->skip_enabled;
     a.skip_lplus = ctx->skip_lplus;
     a.skip_cmax = ctx->skip_cmax;
-    a.skip_inv_lplus = (ctx->skip_lplus > 0.0) ? 1.0 / ctx->skip_lplus : 0.0;
     a.R = ctx->R;
     a.S = ctx->params;
     a.dt = 1.0 / ctx->frequency;
@@ -1042,11 +955,6 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.first_pid = first_particle_id;
     a.allow_contacts = allow_contacts ? 1 : 0;
     a.individual_jacobians = ctx->individual_jacobians;
-    /* traced calls record every microstep's configuration the reference's way: no proof */
-    a.jproof = (!tr && !ctx->individual_jacobians && ctx->jp_layout && ctx->R.jp_ok && ctx->skip_enabled && ctx->joint_proof) ? 1 : 0;
-    /* the exact-EDT route widens the joint-space proof's slack (33.6 -> 42.4 % of the cfg3
-     * microsteps proven); in the per-round skips of the default kernel it measured no gain */
-    a.skip_euclid = (a.jproof && ctx->sdf_euclid && ctx->params.environment_collision_check_tolerance >= 0.0) ? 1 : 0;
     a.out_q = d_out_positions;
     a.pid_io = d_pid_io;
     a.out_collided = d_out_collided;
@@ -1058,7 +966,7 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair, ctx->jp_layout);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     /* controller-step segments: automatically only when the batch outnumbers the
      * resident waves (otherwise every particle has a wave from the start), always
@@ -1110,10 +1018,7 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? (groups_needed > 0 ? groups_needed : 1)
                                                                                   : ctx->grid_groups);
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
-    /* the joint-space proof runs in its own instantiation (fks_simulate_linked_jp): the
-     * paired FK it replaces stays out of it, and out of the other kernels goes the proof */
-    hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type)
-                          : (a.jproof ? fks_simulate_linked_jp : kernel_for(ctx->R.type, ctx->individual_jacobians != 0)),
+    hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type) : kernel_for(ctx->R.type, ctx->individual_jacobians != 0),
                        dim3(grid),
                        dim3(64 * ctx->waves_per_group), ctx->lds_bytes, s, static_cast<const fksd::SimArgs*>(ctx->d_args));
     HIP_TRY(ctx, hipGetLastError());
@@ -1178,7 +1083,7 @@ fks_status fks_check_config_collision_device(fks_context* ctx, const double* d_c
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair, ctx->jp_layout);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     *ctx->h_args = a;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice, s));
@@ -1461,7 +1366,7 @@ fks_status fks_kinematics(fks_context* ctx, int32_t mode, const double* configs,
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair, ctx->jp_layout);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     a.kin_mode = mode;
     a.kin_out = d_out;
@@ -1559,18 +1464,6 @@ fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_
     if (heavy_priority > 2u) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "heavy_priority must be 0, 1 or 2");
     ctx->heavy_per_step = heavy_resolver_per_step;
     ctx->heavy_priority = heavy_priority;
-    return FKS_OK;
-}
-
-fks_status fks_set_joint_proof(fks_context* ctx, int32_t enable) {
-    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
-    ctx->joint_proof = enable ? 1 : 0;
-    if (ctx->has_robot) {
-        const fks_status st = settle(ctx); /* a launch in flight still uses the old layout */
-        if (st != FKS_OK) return st;
-        HIP_TRY(ctx, hipSetDevice(ctx->device));
-        HIP_TRY(ctx, launch_layout(ctx, ctx->R));
-    }
     return FKS_OK;
 }
 

@@ -72,11 +72,6 @@ struct RobotDev {
     int32_t type, L, J, G, D, P, W, npairs;
     int32_t self_possible;
     int32_t nrounds;
-    /* the joint-space proof of free microsteps applies: linked robot,
-     * every round on one link with w = 1 points, <= 64 rounds, finite lever bounds,
-     * every geometry box over w = 1 points */
-    int32_t jp_ok;
-    int32_t pad_jp;
     double base[12];
     const JointDev* joints;
     const int32_t* geom_link;
@@ -98,9 +93,6 @@ struct RobotDev {
      * unknown.  Lets the microstep-motion check of SPCS:1570-1575 be proven instead
      * of recomputed. */
     const double* dof_lever;
-    /* the same bound per (link, dof), [l * D + d]: over the points of link l only (0 when
-     * dof d does not move link l); the joint-space proof's per-link motion bound */
-    const double* link_lever;
     /* dofs whose actuator is a SampledUncertainVelocityActuator (bit d), their tables */
     uint64_t sampled_mask;
     const SampledDev* sampled;
@@ -116,19 +108,17 @@ constexpr int kWavesPerGroup = 4;
 struct LdsLayout {
     uint32_t joints, ctrl, base, dofj, gbox, gpairs, rounds, shared_total;
     uint32_t rstate, noise, noise_err, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u,
-        ustep, x, real, axis_w, orig_w, colsq, hcoef, box, misc, ints, jm2, jp_anchor, jp_slack, total;
+        ustep, x, real, axis_w, orig_w, colsq, hcoef, box, misc, ints, jm2, total;
     uint32_t fk_pair; /* 1: the free-motion microsteps pair their FK chains (jm2 allocated) */
-    uint32_t jp;      /* 1: joint-space proof of free microsteps (jp_anchor / jp_slack allocated) */
 };
 
 inline
 #if defined(__HIPCC__)
     __host__ __device__
 #endif
-    LdsLayout make_lds_layout(int L, int J, int D, int W, int G, int NR, bool fk_pair = false, bool jp = false) {
+    LdsLayout make_lds_layout(int L, int J, int D, int W, int G, int NR, bool fk_pair = false) {
     LdsLayout l;
     uint32_t o = 0;
-    bool box_own = false; /* the boxes have a region of their own (joint-space proof without jm2 room) */
     /* shared: the robot tables the hot loops read (filled once per workgroup) */
     l.joints = o;
     o += (uint32_t)kJointWords * (J > 0 ? J : 1);
@@ -164,11 +154,9 @@ inline
      * world joint frames (Jacobian), QR column norms / Householder coefficients and the
      * self-collision boxes only between fk() calls */
     {
-        /* (with the joint-space proof the self-collision boxes move out of this region: the
-         * next controller step's proof reads the last check's boxes after FKs have run) */
         const uint32_t motion = 12u * (uint32_t)(J > 0 ? J : 1);
         const uint32_t boxes = 6u * (uint32_t)(G > 0 ? G : 1);
-        const uint32_t others = 8u * (uint32_t)D + (jp ? 0u : boxes);
+        const uint32_t others = 8u * (uint32_t)D + boxes;
         l.jm = o;
         l.axis_w = o;
         l.orig_w = o + 3u * D;
@@ -176,11 +164,6 @@ inline
         l.hcoef = o + 7u * D;
         l.box = o + 8u * D;
         o += (motion > others) ? motion : others;
-        box_own = jp && !(fk_pair && 12u * (uint32_t)(J > 0 ? J : 1) >= boxes);
-        if (box_own) {
-            l.box = o;
-            o += boxes;
-        }
     }
     l.cfg = o;
     o += W;
@@ -208,21 +191,10 @@ inline
     o += 32;
     l.ints = o; /* int32 region: perm[64], transpositions[64], 16 spare words */
     o += (2 * kMaxDofs + 16) / 2;
-    /* the second FK chain's joint motion matrices (paired FK of the next free microstep);
-     * with the joint-space proof they also hold the self-collision boxes (written by every
-     * check after the microstep's FK, read by the next step's jp_step before any paired FK) */
+    /* the second FK chain's joint motion matrices (paired FK of the next free microstep) */
     l.fk_pair = fk_pair ? 1u : 0u;
     l.jm2 = o;
-    if (jp && !box_own) l.box = o;
     if (fk_pair) o += 12u * (uint32_t)(J > 0 ? J : 1);
-    /* joint-space proof: the anchor configuration (D) and, per link, how far its points may
-     * move from their anchor positions with the microstep provably free (L, non-negative
-     * doubles kept as their bit patterns so that LDS integer min-atomics order them) */
-    l.jp = jp ? 1u : 0u;
-    l.jp_anchor = o;
-    if (jp) o += (uint32_t)(D > 0 ? D : 1);
-    l.jp_slack = o;
-    if (jp) o += (uint32_t)(L > 0 ? L : 1);
     o = (o + 1u) & ~1u; /* 16-byte alignment */
     l.total = o;
     return l;
@@ -286,12 +258,8 @@ struct SimArgs {
      * satisfies: axis neighbours with positive values differ by <= lplus*res, and
      * positive cells next to a non-positive one are <= cmax*res */
     int32_t skip_enabled;
-    /* the SDF is the exact Euclidean distance transform of its own sign (the builders'
-     * sqrt(d_filled) res - sqrt(d_free) res) and the env threshold is <= 0: a free cell s
-     * cells from the nearest filled one has only free cells within s */
-    int32_t skip_euclid;
+    int32_t skip_pad;
     double skip_lplus, skip_cmax;
-    double skip_inv_lplus; /* 1 / skip_lplus (the joint-space proof's admissible motion) */
     RobotDev R;
     fks_solver_params S;
     double dt;               /* simulation_controller_interval_ = 1/frequency  (SPCS:427)   */
@@ -309,8 +277,6 @@ struct SimArgs {
     uint64_t first_pid;
     int32_t allow_contacts;
     int32_t individual_jacobians; /* ComputeResolverCorrectionStepIndividualJacobians (SPCS:1966-1988) */
-    int32_t jproof;               /* joint-space proof of free microsteps in use (L.jp, R.jp_ok, skip_enabled) */
-    int32_t pad_jproof;
     double* out_q;
     /* ForwardSimulateMutableRobot (fks_forward_simulate_mutable): per particle 2D doubles,
      * the PID error integrals then last errors the particle starts with, overwritten
@@ -376,9 +342,6 @@ enum {
     kCntSelfPoints,
     kNumCounters = 16
 };
-/* microsteps whose collision check the joint-space proof settled (the spare word after the
- * particle queue at kNumCounters) */
-constexpr int kCntProvenMicro = kNumCounters + 1;
 
 /* per-phase s_memtime cycle sums (lane 0 of every wave), after the counters and the
  * particle queue in the counter buffer; order = FKS_PHASE_* in fks_capi.h */

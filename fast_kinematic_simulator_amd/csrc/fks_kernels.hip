@@ -21,8 +21,6 @@
  *     (one lane per geometry) reject disallowed pairs; only overlapping pairs run
  *     the exact key comparison, and true self-contacts run the impulse solve
  *     (SPCS:983-1171) on one lane;
- *   - optionally (fks_simulate_linked_jp, fks_set_joint_proof) the joint-space proof
- *     settles free microsteps from joint space without their FK and checks (jp_step).
  * All double arithmetic is IEEE (no contraction: built with -ffp-contract=off),
  * transcendentals come from include/fks_portable_math.h, so results are
  * bit-identical to the CPU oracle on the same inputs.
@@ -456,9 +454,6 @@ struct Sim {
     double pid_integral, pid_last; /* DOF lanes */
     bool self_nonempty;
     bool tcur_valid; /* Tcur == FK(particle configuration) from the end of the last step */
-    bool jp_valid;   /* the joint-space proof's anchor and slack (LDS) hold for this particle */
-    bool jp_pending; /* the last controller step ended on a free check at Tcur = FK(cfg): anchor there */
-    bool jp_rest;    /* the last attempt proved nothing: the next step runs without one */
     uint64_t local;            /* particle index within the call (traced kernels) */
     uint32_t tr_steps, tr_cfgs; /* trace records produced so far (traced kernels) */
 };
@@ -796,26 +791,6 @@ __device__ void fk_pair(Sim& s, const double* cfgA, double* TA, const double* cf
     wsync();
 }
 
-/* out-of-line FK of linked robots for the paths the joint-space proof adds (the first
- * microstep after proven ones, a controller step starting after one): their own register
- * budget instead of more inlined chains in the microstep loop */
-__device__ __noinline__ void fk_pair_out(const SimArgs* __restrict__ Ap, double* lds, const double* shared, int ln,
-                                         const double* cfgA, double* TA, const double* cfgB, double* TB) {
-    Sim t;
-    t.A = Ap;
-    t.lds = lds;
-    t.shared = const_cast<double*>(shared);
-    t.lane = ln;
-    t.joints = reinterpret_cast<const JointDev*>(shared + Ap->L.joints);
-    t.base = shared + Ap->L.base;
-    if (Ap->L.fk_pair) {
-        fk_pair(t, cfgA, TA, cfgB, TB);
-    } else {
-        fk<FKS_ROBOT_LINKED>(t, cfgA, TA);
-        fk<FKS_ROBOT_LINKED>(t, cfgB, TB);
-    }
-}
-
 /* noisy actuator of dof `dof` on its clamped command `real` (TNUVA:568-596):
  * TruncatedNormalUncertainVelocityActuator (UNC:77-90), or the sampled one
  * (UNC:270-279: first matching bin, then the picked sample) */
@@ -1062,16 +1037,6 @@ __device__ __forceinline__ RoundDev lds_round(const Sim& s, int r) {
     return o;
 }
 
-/* joint-space proof: the largest motion (cells) from a round's cached
- * reference that the free proof below admits (the first disjunct of kSkipCheck solved for
- * b, or the same-cell disjunct), with a relative 1e-6 and an absolute 1e-9 margin */
-__device__ __forceinline__ double round_admissible(const SimArgs& A, double S, double G, double C) {
-    double bm = dmin(((S * A.sdf_g.inv_res - A.skip_cmax - 1e-9) * A.skip_inv_lplus - 2.0) * 0.57735026918962573, G - 1e-6);
-    if (S >= A.thr_env) bm = dmax(bm, C - 1e-9);
-    if (A.skip_euclid) bm = dmax(bm, dmin(S * A.sdf_g.inv_res * (1.0 - 1e-6) - 1.7320508075688773 - 1e-6, G - 1.0 - 1e-6));
-    return bm * (1.0 - 1e-6) - 1e-9;
-}
-
 /* which rounds (bit r, r < 64) may skip the env check / the correction estimate at
  * transforms T; lane r evaluates round r */
 __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, int what) {
@@ -1097,11 +1062,7 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
             for (int e = 0; e < 12; ++e) still = still && (Tl[e] == st[e]);
             const bool same_cell = still || b < st[14] - 1e-9;
             if (what == kSkipCheck)
-                sk = (inb && (Sr - A.skip_cmax) > (K - 1.0) * lp + 1e-9) || (same_cell && st[12] >= A.thr_env) ||
-                     /* exact EDT: every point ends in a cell whose centre is within b + sqrt(3)
-                      * of its old cell's, which is Sr or more from any filled cell; all
-                      * coordinates stay > 0 (st[13] - 1 > b), where a cell spans [i, i + 1) */
-                     (A.skip_euclid && b < Sr * (1.0 - 1e-6) - 1.7320508075688773 - 1e-6 && b < st[13] - 1.0 - 1e-6);
+                sk = (inb && (Sr - A.skip_cmax) > (K - 1.0) * lp + 1e-9) || (same_cell && st[12] >= A.thr_env);
             else
                 sk = (inb && (Sr - A.skip_cmax) > K * lp + 1e-9 && (Sr - K * lp) > 0.5 + 1.5 * lp + 1e-6) ||
                      (same_cell && Sr > A.skip_cmax + 1e-9 && Sr > 0.5 + 1.5 * lp + 1e-6);
@@ -1703,56 +1664,6 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
     return (err << 1) | (wave_any(nonempty) ? 1u : 0u);
 }
 
-/* ---------------- joint-space proof of free microsteps ----------------
- * A point of link l moves by at most sum over the dofs d moving l of |dq_d| * lever_d
- * for a joint motion dq (lever_d: fks_set_robot's configuration-independent bound on a
- * point's distance to dof d's axis, 1 per unit for prismatic joints).  After a microstep
- * whose collision check came back free at configuration q_a, jp_anchor() records q_a and,
- * per link, how far the link's points may still move from their positions at q_a with
- * both checks provably free:
- *   - environment (SPCS:921-981): per 64-point round, the largest motion from the round's
- *     cached reference that skippable_rounds' proof admits, minus the motion from that
- *     reference to q_a (the triangle inequality chains the two bounds);
- *   - self-collision (SPCS:1183-1275): per disallowed geometry pair whose cell-key boxes
- *     are separated, half of (gap - 4) cells: a key moves by less than motion / res + 2
- *     (truncation toward zero), so keys of the two geometries cannot meet while both
- *     move less than that.
- * A later microstep whose every link stays within its slack (jp_proven) is free: the
- * reference's CheckCollision returns false there, after reading 4 bytes per point (all in
- * bounds), which is what the kernel counts.  The slack is a fact about the geometry, not
- * about the particle's history, so it holds across microsteps and controller steps until
- * the particle leaves it; every bound carries a relative 1e-6 / absolute 1e-9 margin. */
-/* the microstep at configuration cfg is free by the anchor's slack (1, uniform) */
-__device__ __forceinline__ uint32_t jp_proven(const SimArgs* __restrict__ Ap, double* lds, int ln, const double* cfg) {
-    const SimArgs& A = *Ap;
-    const RobotDev& R = A.R;
-    const double* qa = lds + A.L.jp_anchor;
-    double* dq = lds + A.L.real; /* the resolver's correction-step scratch, unused here */
-    /* |dq_d| is 0 exactly when dof d has not moved (x - y == 0 iff x == y); NaN stays NaN */
-    if (ln < R.D) dq[ln] = dabs(cfg[ln] - qa[ln]);
-    wsync();
-    bool out = false;
-    if (ln < R.L) {
-        const FKS_GLOBAL double* lev = gp(R.link_lever) + (uint64_t)ln * (uint64_t)R.D;
-        double acc = 0.0;
-        bool moved = false;
-        for (int d = 0; d < R.D; ++d) {
-            const double v = dq[d], l = lev[d];
-            acc = acc + v * l;
-            moved = moved || (l > 0.0 && v != 0.0);
-        }
-        /* a link none of whose dofs moved sits exactly where its check was free (its
-         * transform is the same bits) */
-        const double delta = moved ? acc * (1.0 + 1e-9) + 1e-9 : 0.0;
-        const double slack1 = __builtin_bit_cast(double, reinterpret_cast<const uint64_t*>(lds + A.L.jp_slack)[ln]);
-        out = !(delta + 1.0 <= slack1);
-    }
-    return wave_any(out) ? 0u : 1u;
-}
-/* proven microsteps of the wave (flushed with the call counters), LDS misc + 6 */
-__device__ __forceinline__ uint64_t* jp_counter(const Sim& s) { return reinterpret_cast<uint64_t*>(s.lds + s.A->L.misc + 6); }
-
-
 /* CheckCollision (SPCS:1418-1436) */
 template <int RT>
 __device__ bool check_collision(Sim& s, const double* Tp, const double* Tc) {
@@ -1770,164 +1681,6 @@ __device__ bool check_collision(Sim& s, const double* Tp, const double* Tc) {
     s.self_nonempty = self;
     if (self && s.lane == 0) self_counters(s)[0]++;
     return env || self;
-}
-
-#ifndef FKS_VERIFY_JP
-#define FKS_VERIFY_JP 0
-#endif
-/* a controller step whose proof attempt proved nothing is followed by one without an
- * attempt (near obstacles most attempts fail at once and cost a noise refill each) */
-#ifndef FKS_JP_BACKOFF
-#define FKS_JP_BACKOFF 1
-#endif
-/* a step whose proof stops at microstep m > 0 keeps microsteps 0 .. m - 1 */
-#ifndef FKS_JP_PREFIX
-#define FKS_JP_PREFIX 1
-#endif
-constexpr uint32_t kErrProofViolation = 0x40000000u; /* FKS_VERIFY_JP builds only */
-
-/* After a controller step whose last CheckCollision came back free at transforms T =
- * FK(cfg): record cfg as the anchor and, per link, its slack (jp_slack, kept as 1 + metres
- * so that an unsigned LDS min orders them; 0 = never):
- *   - environment: per 64-point round, the motion from its cached reference that the free
- *     proof of skippable_rounds admits (round_admissible) minus the motion from that
- *     reference to T; a round with a point off the grid is never proven (the reference
- *     would not count its bytes);
- *   - self-collision: per disallowed geometry pair, half of (gap - 4) cells between their
- *     cell-key boxes at T (self_collisions left them in LDS): a key moves by less than
- *     motion / res + 2 (truncation toward zero), so two geometries whose points each move
- *     less than that cannot meet in a cell. */
-__device__ __noinline__ uint32_t jp_anchor(const SimArgs* __restrict__ Ap, const double* shared, double* lds, int ln,
-                                           const double* T, const double* cfg) {
-    const SimArgs& A = *Ap;
-    const RobotDev& R = A.R;
-    unsigned long long* slack = reinterpret_cast<unsigned long long*>(lds + A.L.jp_slack);
-    if (ln < R.L) slack[ln] = 0x7FF0000000000000ull; /* +inf */
-    if (ln < R.D) lds[A.L.jp_anchor + ln] = cfg[ln];
-    wsync();
-    auto take = [&](int link, double sl, bool never) {
-        const double c = never ? 0.0 : 1.0 + ((sl > 0.0) ? sl : 0.0); /* NaN or negative: no slack */
-        atomicMin(slack + link, (unsigned long long)__builtin_bit_cast(uint64_t, c));
-    };
-    if (ln < R.nrounds) {
-        const int link = (int)shared[A.L.rounds + 2 * ln];
-        const double radius = shared[A.L.rounds + 2 * ln + 1];
-        const double* st = lds + A.L.rstate + kRoundState * ln;
-        const bool never = !(st[12] > kInvalidRound);
-        double sl = 0.0;
-        if (!never) {
-            const double b = rigid_motion_bound(T + 12 * link, st, radius) * A.sdf_g.inv_res; /* cells */
-            sl = (round_admissible(A, st[12], st[13], st[14]) - b) * A.sdf_g.res - 1e-9;
-        }
-        take(link, sl, never);
-    }
-    if (R.self_possible) {
-        const double* box = lds + A.L.box;
-        const uint32_t* lpairs = reinterpret_cast<const uint32_t*>(shared + A.L.gpairs);
-        for (int k = ln; k < R.npairs; k += kWave) {
-            int a, b;
-            if (k < kLdsPairs) {
-                const uint32_t ab = lpairs[k];
-                a = (int)(ab & 0xffffu);
-                b = (int)(ab >> 16);
-            } else {
-                a = gp(R.pairs)[2 * k];
-                b = gp(R.pairs)[2 * k + 1];
-            }
-            double gap = -__builtin_huge_val();
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                gap = dmax(gap, box[6 * b + i] - box[6 * a + 3 + i]);
-                gap = dmax(gap, box[6 * a + i] - box[6 * b + 3 + i]);
-            }
-            const double sl = (((gap - 4.0) * A.env_g.res) * (1.0 - 1e-6) - 1e-9) * 0.5;
-            take((int)shared[A.L.gbox + 8 * a + 7], sl, false);
-            take((int)shared[A.L.gbox + 8 * b + 7], sl, false);
-        }
-    }
-    wsync();
-    return 1u;
-}
-
-/* One controller step of a linked robot settled by the joint-space proof, if it can be:
- * the M microsteps' ApplyControlInput with actuator noise (SPCS:1599) from the step's
- * start (cfg_work), each post-action configuration proven free by jp_proven.  Returns
- * bit 1 = the anchor holds (always, once made), bit 0 = the step is proven, its final
- * configuration in cfg_res; without bit 0 nothing but the noise buffer changed (some
- * microstep is not proven or its actuator raised an error: the step then runs in full and
- * reproduces both).  Inlined: as an out-of-line call (its register saves at the call
- * site) it tripled the spill reloads of the microstep loop (tools/loop_spills.py). */
-__device__ __attribute__((always_inline)) uint32_t jp_step(const SimArgs* __restrict__ Ap, double* lds, double* shared, double* scratch, int ln,
-                                         uint64_t pid, uint32_t step, uint32_t M, const double* Tanchor, double* Tcur,
-                                         double* Tv) {
-    const SimArgs& A = *Ap;
-    const RobotDev& R = A.R;
-    /* the previous step ended on a free check at Tanchor = FK(its configuration), which is
-     * this step's start (cfg_work): anchor there first */
-    if (Tanchor) jp_anchor(Ap, shared, lds, ln, Tanchor, lds + A.L.cfg_work);
-    Sim t;
-    t.A = Ap;
-    t.lds = lds;
-    t.shared = shared;
-    t.ldsi = reinterpret_cast<int32_t*>(lds + A.L.ints);
-    t.scratch = scratch;
-    t.lane = ln;
-    t.pid = pid;
-    t.step = step;
-    t.err = 0;
-    t.lane_bytes = 0;
-    t.stats = reinterpret_cast<uint32_t*>(lds + A.L.misc + 24);
-    t.phase = reinterpret_cast<uint64_t*>(lds + A.L.misc + 8);
-    t.joints = reinterpret_cast<const JointDev*>(shared + A.L.joints);
-    t.ctrl = reinterpret_cast<const fks_dof_controller*>(shared + A.L.ctrl);
-    t.dofj = reinterpret_cast<const int32_t*>(shared + A.L.dofj);
-    t.base = shared + A.L.base;
-    t.self_nonempty = false;
-    /* ping-pong between cfg_tmp and cfg_act (both free between steps), final copy to cfg_res */
-    const double* start = lds + A.L.cfg_work;
-    double* buf[2] = {lds + A.L.cfg_tmp, lds + A.L.cfg_act};
-    const double* ustep = lds + A.L.ustep;
-    const uint32_t per = (uint32_t)(kWave / R.D);
-    const double* in = start;
-    /* microsteps 0 .. m - 1 proven, microstep m not: the step resumes at m from their last
-     * configuration (copied to cfg_work) and its transforms (FK into Tcur) */
-    auto prefix = [&](uint32_t m) -> uint32_t {
-        /* bit 2: the noise buffer holds the block of the microstep the step resumes at */
-        if (!FKS_JP_PREFIX) return 2u | (m < per ? 4u : 0u); /* variant: the whole step runs again */
-        if (m > 0u) {
-            double* cw = lds + A.L.cfg_work;
-            if (ln < R.W) cw[ln] = in[ln];
-            wsync();
-            fk<FKS_ROBOT_LINKED>(t, cw, Tcur);
-        }
-        return 2u | 4u | (m << 8);
-    };
-    for (uint32_t m = 0; m < M; ++m) {
-        double* out = buf[m & 1u];
-        if (m % per == 0u) refill_noise(t, m, M);
-        apply_input<FKS_ROBOT_LINKED>(t, in, ustep, out, true, m);
-        t.err = wave_or(t.err);
-        if (t.err) return prefix(m);
-        if (jp_proven(Ap, lds, ln, out) == 0u) return prefix(m);
-        if constexpr (FKS_VERIFY_JP) {
-            /* verification builds: the full checks must agree (a violation is an error); Tv is
-             * the step's trial buffer, free here */
-            fk<FKS_ROBOT_LINKED>(t, out, Tv);
-            const bool env = env_collision<true>(t, Tv);
-            const bool self = self_collisions(t, Tv, Tv);
-            if (env || self) {
-                if (ln == 0)
-                    reinterpret_cast<uint32_t*>(lds + A.L.ints)[2 * kMaxDofs + 8] =
-                        (env ? kErrProofViolation : 0u) | (self ? kErrProofViolation >> 1 : 0u);
-                wsync();
-                return 2u;
-            }
-        }
-        in = out;
-    }
-    if (ln < R.W) lds[A.L.cfg_res + ln] = in[ln];
-    wsync();
-    return 3u;
 }
 
 /* world joint axes/origins per dof for the Jacobian (linked robots) */
@@ -2690,7 +2443,7 @@ __device__ __noinline__ void individual_jacobians_solve(Sim& s, uint32_t Rn, dou
  * IND: the individual-Jacobian solve (SPCS:1966-1988) is compiled into a kernel of its
  * own, so the default stacked-Jacobian kernel does not carry it; the traced kernels
  * (not on the hot path) read the choice at run time. */
-template <int RT, bool TR, bool IND, bool JP>
+template <int RT, bool TR, bool IND>
 __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg, bool allow_contacts, bool* out_collided,
                             bool* out_failed, double*& Tcur, double*& Tprev) {
     const SimArgs& A = *s.A;
@@ -2721,18 +2474,9 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
     wsync();
     /* real_control_input = u * dt (SPCS:1549), already in u.  FK of the start
      * configuration is still in Tcur when the previous step ended normally */
-    if constexpr (RT == FKS_ROBOT_LINKED && JP) {
-        apply_input<RT>(s, cfg, u, cfg_tmp, false, 0);
-        /* after a step that ended on a proven microstep (or in a new segment) both FKs in one pass */
-        if (!s.tcur_valid)
-            fk_pair_out(s.A, s.lds, s.shared, s.lane, cfg, Tcur, cfg_tmp, Ttmp);
-        else
-            fk<RT>(s, cfg_tmp, Ttmp);
-    } else {
-        if (!s.tcur_valid) fk<RT>(s, cfg, Tcur);
-        apply_input<RT>(s, cfg, u, cfg_tmp, false, 0);
-        fk<RT>(s, cfg_tmp, Ttmp);
-    }
+    if (!s.tcur_valid) fk<RT>(s, cfg, Tcur);
+    apply_input<RT>(s, cfg, u, cfg_tmp, false, 0);
+    fk<RT>(s, cfg_tmp, Ttmp);
     s.tcur_valid = false;
     const double computed_step_motion = max_point_motion(s, Tcur, Ttmp);
     const double raw_steps = __builtin_ceil(computed_step_motion / A.target_micro);
@@ -2777,60 +2521,7 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
     const uint32_t noise_per = (uint32_t)(kWave / R.D);
     bool pair_ready = false; /* Ttmp holds FK(cfg_tmp), cfg_tmp = the predicted configuration */
     uint32_t pair_err = 0;   /* the predicted configuration's actuator error bits (per lane) */
-    uint32_t jr = 0; /* jp_step: bit 0 whole step proven, bit 1 anchor holds, bit 2 noise block of the
-                      * resume microstep drawn, bits 8.. proven prefix */
-    if constexpr (JP) {
-        /* the whole controller step settled by the joint-space proof: every microstep's
-         * ApplyControlInput (SPCS:1599) is applied and every CheckCollision (SPCS:1600-1602)
-         * is proven free, so the step ends at the last microstep's configuration with no
-         * contact; the reference reads 4 bytes per point per check (all in bounds) */
-        if (FKS_JP_BACKOFF && s.jp_rest) {
-            s.jp_rest = false;
-            s.jp_pending = false;
-        } else if (s.jp_valid || s.jp_pending) {
-            jr = jp_step(s.A, s.lds, s.shared, s.scratch, s.lane, s.pid, s.step, M, s.jp_pending ? Tcur : nullptr, Tcur, Ttmp);
-            if (s.jp_pending) s.jp_valid = (jr & 2u) != 0u;
-            s.jp_pending = false;
-            s.jp_rest = (jr & 1u) == 0u && (jr >> 8) == 0u;
-        }
-        if (jr & 1u) {
-            const int ln = s.lane;
-            if (ln < R.P) s.lane_bytes += (uint64_t)M * 4ull * (uint64_t)((R.P - ln + kWave - 1) / kWave);
-            count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (uint64_t)M * (uint64_t)R.nrounds);
-            s.micro_count += M;
-            if (ln == 0) {
-                jp_counter(s)[0] += M;
-                s.stats[kCntSuccessful]++;
-                s.stats[kCntFree]++;
-            }
-            /* jp_step leaves the final configuration in res_cfg */
-            *out_collided = false;
-            s.tcur_valid = false;
-            return 0;
-        }
-        if constexpr (FKS_VERIFY_JP) {
-            uint32_t* vw = reinterpret_cast<uint32_t*>(s.lds + A.L.ints) + 2 * kMaxDofs + 8;
-            const uint32_t v = *vw;
-            wsync();
-            if (v) {
-                if (s.lane == 0) *vw = 0u;
-                wsync();
-                s.err |= v;
-                return 1;
-            }
-        }
-        /* a proven prefix: microsteps 0 .. k0 - 1 are done (cfg = their last configuration,
-         * Tcur = its FK); the step continues in full from microstep k0 */
-        const uint32_t k0 = jr >> 8;
-        if (k0) {
-            const int ln = s.lane;
-            if (ln < R.P) s.lane_bytes += (uint64_t)k0 * 4ull * (uint64_t)((R.P - ln + kWave - 1) / kWave);
-            count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (uint64_t)k0 * (uint64_t)R.nrounds);
-            s.micro_count += k0;
-            if (ln == 0) jp_counter(s)[0] += k0;
-        }
-    }
-    for (uint32_t micro = (JP ? jr >> 8 : 0u); micro < M; ++micro) {
+    for (uint32_t micro = 0; micro < M; ++micro) {
         s.lane = opaque_lane(s.lane);
         const int ln = s.lane;
         s.micro_count++;
@@ -2845,9 +2536,7 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
             s.err |= pair_err;
             wsync();
         } else {
-            /* (after a jp_step attempt the buffer already holds the block of its first
-             * unproven microstep, where the loop starts) */
-            if (micro % (uint32_t)(kWave / R.D) == 0u && !(JP && (jr & 4u) != 0u && micro == (jr >> 8)))
+            if (micro % (uint32_t)(kWave / R.D) == 0u)
                 for (int k = 0; k < prof_reps(kDupRefill); ++k) refill_noise(s, micro, M);
             for (int k = 0; k < prof_reps(kDupInput); ++k) apply_input<RT>(s, cfg_prev, ustep, cfg, true, micro);
         }
@@ -2994,10 +2683,7 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
     if (ln < W) res_cfg[ln] = cfg[ln];
     wsync();
     *out_collided = collided;
-    s.tcur_valid = true;
-    /* the step's last check (a microstep's or the resolver's) came back free at Tcur =
-     * FK(cfg): the next step's jp_step anchors there (one call site keeps the registers) */
-    if constexpr (JP) s.jp_pending = true;
+    s.tcur_valid = true; /* the step's last check came back free at Tcur = FK(cfg) */
     return 0;
 }
 
@@ -3258,7 +2944,7 @@ __device__ __forceinline__ void kinematics(const SimArgs* __restrict__ args, dou
     }
 }
 
-template <int RT, bool TR, bool IND = false, bool JP = false>
+template <int RT, bool TR, bool IND = false>
 __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ args, double* lds_mem) {
     const SimArgs& A = *args;
     const RobotDev& R = A.R;
@@ -3324,8 +3010,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     s.lane_bytes = 0;
     uint64_t w_steps = 0, w_micro = 0, w_resolver = 0, w_lsq = 0, w_errors = 0;
     if (ln < 2) self_counters(s)[ln] = 0;
-    if (ln == 0) jp_counter(s)[0] = 0;
-    if (ln == 0) reinterpret_cast<uint32_t*>(s.lds + A.L.ints)[2 * kMaxDofs + 8] = 0; /* FKS_VERIFY_JP violations */
     wsync();
     while (true) {
         /* ticket t: segment t / n of particle t % n, so every particle's first segment is
@@ -3379,7 +3063,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                     const uint64_t* sc = self_counters(s);
                     if (sc[0]) atomicAdd(A.counters + kCntSelfChecks, (unsigned long long)sc[0]);
                     if (sc[1]) atomicAdd(A.counters + kCntSelfPoints, (unsigned long long)sc[1]);
-                    if (jp_counter(s)[0]) atomicAdd(A.counters + kCntProvenMicro, (unsigned long long)jp_counter(s)[0]);
                     for (int k = 0; k < FKS_NUM_PHASES; ++k)
                         if (s.phase[k]) atomicAdd(A.counters + kPhaseBase + k, (unsigned long long)s.phase[k]);
                 }
@@ -3414,9 +3097,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         const uint64_t t_particle = __builtin_amdgcn_s_memtime();
         s.self_nonempty = false;
         s.tcur_valid = false;
-        s.jp_valid = false;
-        s.jp_pending = false;
-        s.jp_rest = false;
         const double* start = A.starts + local * (uint64_t)W;
         const double* target = (A.num_targets == A.n) ? A.targets + local * (uint64_t)W : A.targets;
         bool collided = false;
@@ -3472,7 +3152,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             wsync();
             tock(s, FKS_PHASE_CONTROL, t0);
             bool rc = false, rf = false;
-            const int status = resolve_step<RT, TR, IND, JP>(s, cfg, res_cfg, A.allow_contacts != 0, &rc, &rf, Tcur, Tprev);
+            const int status = resolve_step<RT, TR, IND>(s, cfg, res_cfg, A.allow_contacts != 0, &rc, &rf, Tcur, Tprev);
             s.err = wave_or(s.err);
             if (status != 0 || s.err) {
                 ended = true;
@@ -3604,12 +3284,6 @@ extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se2(const SimArgs* __re
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se3(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
     simulate_particles<FKS_ROBOT_SE3, false>(args, lds_mem);
-}
-
-/* the joint-space proof of free microsteps (fks_set_joint_proof; linked robots) */
-extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked_jp(const SimArgs* __restrict__ args) {
-    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
-    simulate_particles<FKS_ROBOT_LINKED, false, false, true>(args, lds_mem);
 }
 
 /* simulate_with_individual_jacobians = true (SPCS:420, 1629; fks_set_individual_jacobians) */

@@ -157,11 +157,6 @@ class HipParticleContactSimulator:
         _capi.check(self._lib.fks_set_segment_policy(self._ctx, int(heavy_resolver_per_step), int(heavy_priority)), self._ctx,
                     "segment policy")
 
-    def set_joint_proof(self, enable: bool):
-        """Joint-space proof of free microsteps (fks_set_joint_proof; off by default).  No
-        reference counterpart: results are bit-identical either way, only the work changes."""
-        _capi.check(self._lib.fks_set_joint_proof(self._ctx, 1 if enable else 0), self._ctx, "joint proof")
-
     def set_individual_jacobians(self, simulate_with_individual_jacobians: bool):
         """The simulate_with_individual_jacobians constructor flag of the reference class
         (SPCS:420-423, 1629): True selects ComputeResolverCorrectionStepIndividualJacobians

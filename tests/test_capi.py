@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol(fks_lib):
 def test_abi_basics(fks_lib):
     from fast_kinematic_simulator_amd import _capi, get_default_solver_parameters
 
-    assert fks_lib.fks_abi_version() == 4
+    assert fks_lib.fks_abi_version() == 5
     assert fks_lib.fks_status_string(0) == b"ok"
     p = _capi.SolverParams()
     assert fks_lib.fks_default_solver_params(ctypes.byref(p)) == 0
@@ -68,7 +68,6 @@ def test_argument_validation(fks_lib):
     assert fks_lib.fks_set_segment_steps(None, 10) == 1
     assert fks_lib.fks_set_segment_policy(None, 2, 1) == 1
     assert fks_lib.fks_set_individual_jacobians(None, 1) == 1
-    assert fks_lib.fks_set_joint_proof(None, 1) == 1
     waves, lds = ctypes.c_uint32(0), ctypes.c_uint64(0)
     assert fks_lib.fks_get_launch_geometry(None, ctypes.byref(waves), ctypes.byref(lds)) == 1
     assert _capi.PHASE_NAMES[15] == "wave_residency" and len(_capi.PHASE_NAMES) == _capi.NUM_PHASES

@@ -17,11 +17,11 @@ def main():
     extra = []
     libs = []
     for a in sys.argv[1:]:
-        # "lib.so+flag" runs that library with bench.py --flag (e.g. libfks_hip.so+joint-proof)
+        # "lib.so+flag" runs that library with bench.py --flag (e.g. libfks_hip.so+segment-steps=10)
         (extra if a.startswith("--") or (extra and ".so" not in a) else libs).append(a)
     for spec in libs:
         lib, _, flag = spec.partition("+")
-        env = dict(os.environ, FKS_LIB_PATH=os.path.abspath(lib))
+        env = dict(os.environ, FKS_LIB_PATH=os.path.abspath(lib), FKS_VARIANT_LIB="1")
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1", "--no-cpu-baseline", *extra]
         if flag:
             cmd.append("--" + flag)
@@ -32,7 +32,6 @@ def main():
         line = json.loads(p.stdout.strip().splitlines()[-1])
         print(json.dumps({"lib": os.path.basename(lib) + ("+" + flag if flag else ""), "value": line["value"], "kernel_ms": line["roofline"]["avg_kernel_ms"],
                           "frac": line["roofline"]["frac"], "error_particles": line["config"].get("error_particles"),
-                          "proven": line["config"].get("proven_free_microsteps_fraction"),
                           "busy": line.get("wave_slots", {}).get("busy_fraction"), "phases": line.get("kernel_phases")}),
               flush=True)
 
