@@ -100,6 +100,8 @@ GridDev make_grid(const fks_grid_geometry& g) {
     d.inv_res = 1.0 / g.resolution;
     for (int a = 0; a < 3; ++a) d.n[a] = g.num_cells[a];
     for (int w = 0; w < 3; ++w) d.inv_res_span[w] = 1.0 / (g.resolution * (double)w);
+    for (int a = 0; a < 3; ++a) d.nb[a] = (uint32_t)((g.num_cells[a] + 3) >> fksd::kBrickShift);
+    d.nb_pad = 0;
     return d;
 }
 
@@ -131,7 +133,10 @@ bool valid_grid(const fks_grid_geometry& g) {
     for (int a = 0; a < 3; ++a)
         if (g.num_cells[a] < 2 || g.num_cells[a] > 65535) return false;
     const double cells = (double)g.num_cells[0] * (double)g.num_cells[1] * (double)g.num_cells[2];
-    return cells < 4294967295.0;
+    /* the kernels address cells of the 4x4x4-brick layout with 32-bit indices */
+    const double padded = (double)((g.num_cells[0] + 3) & ~3ll) * (double)((g.num_cells[1] + 3) & ~3ll) *
+                          (double)((g.num_cells[2] + 3) & ~3ll);
+    return cells < 4294967295.0 && padded < 4294967295.0;
 }
 
 bool same_geometry(const fks_grid_geometry& a, const fks_grid_geometry& b) {
@@ -199,8 +204,9 @@ struct fks_context {
     uint64_t seed = 0;
     uint64_t call_index = 0;
     /* environment */
-    float* d_sdf = nullptr;
-    uint32_t* d_noff = nullptr;
+    float* d_sdf = nullptr;     /* bricked (fks_device.h brick_cell) */
+    uint32_t* d_noff = nullptr; /* VoxelGrid-order CSR offsets, only until they are bricked */
+    uint2* d_nrange = nullptr;  /* bricked [begin, end) per normal-grid cell */
     double* d_nent = nullptr;
     GridDev sdf_g, nrm_g, env_g;
     float oob = 0.0f;
@@ -421,6 +427,21 @@ static fks_status create_impl(const fks_environment* henv, const fks_device_env*
         ctx->skip_lplus = lp * (1.0 + 1e-6) + 1e-6;
         ctx->skip_cmax = cm * (1.0 + 1e-6) + 1e-6;
     }
+    /* the kernels' HBM layout: the SDF and the normal ranges in 4x4x4-cell bricks (the
+     * analysis above read the VoxelGrid order) */
+    {
+        float* bricked = nullptr;
+        if ((e = fks_env::brick_sdf_device(ctx->d_sdf, ctx->sdf_g.n, ctx->sdf_g.nb, &bricked)) != hipSuccess)
+            return bail(e, "sdf bricks");
+        (void)hipFree(ctx->d_sdf);
+        ctx->d_sdf = bricked;
+        if (ctx->d_noff) {
+            if ((e = fks_env::brick_normal_ranges_device(ctx->d_noff, ctx->nrm_g.n, ctx->nrm_g.nb, &ctx->d_nrange)) != hipSuccess)
+                return bail(e, "normal-range bricks");
+            (void)hipFree(ctx->d_noff);
+            ctx->d_noff = nullptr;
+        }
+    }
     if ((e = hipMalloc((void**)&ctx->d_counters, fksd::kCounterWords * sizeof(unsigned long long))) != hipSuccess)
         return bail(e, "counters");
     if ((e = hipHostMalloc((void**)&ctx->h_counters, fksd::kCounterWords * sizeof(unsigned long long), 0)) != hipSuccess)
@@ -456,6 +477,7 @@ void fks_destroy(fks_context* ctx) {
     free_staging(ctx);
     if (ctx->d_sdf) (void)hipFree(ctx->d_sdf);
     if (ctx->d_noff) (void)hipFree(ctx->d_noff);
+    if (ctx->d_nrange) (void)hipFree(ctx->d_nrange);
     if (ctx->d_nent) (void)hipFree(ctx->d_nent);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
@@ -931,7 +953,7 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.nrm_g = ctx->nrm_g;
     a.env_g = ctx->env_g;
     a.sdf = ctx->d_sdf;
-    a.noff = ctx->d_noff;
+    a.nrange = ctx->d_nrange;
     a.nent = ctx->d_nent;
     a.oob = ctx->oob;
     a.has_normals = ctx->has_normals;
@@ -1065,7 +1087,7 @@ fks_status fks_check_config_collision_device(fks_context* ctx, const double* d_c
     a.nrm_g = ctx->nrm_g;
     a.env_g = ctx->env_g;
     a.sdf = ctx->d_sdf;
-    a.noff = ctx->d_noff;
+    a.nrange = ctx->d_nrange;
     a.nent = ctx->d_nent;
     a.oob = ctx->oob;
     a.has_normals = ctx->has_normals;

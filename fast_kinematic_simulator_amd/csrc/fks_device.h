@@ -3,8 +3,12 @@
  * the host launcher fks_capi.cpp and the kernels in fks_kernels.hip).
  *
  * HBM layout (all resident for the life of a context / robot):
- *   SDF            float[nx*ny*nz], z fastest (arc_utilities VoxelGrid order)
- *   normal grid    CSR: uint32 offsets[cells+1], 6 doubles per entry
+ *   SDF            float per cell in 4x4x4-cell bricks (brick_cell below): a cell's
+ *                  7-point EstimateDistance4d stencil and the neighbouring points of a
+ *                  link fall in one or two 128-B lines instead of the five or more of
+ *                  the VoxelGrid's linear order (x neighbours nx*ny*4 bytes apart)
+ *   normal grid    per cell (in the same bricks) the (begin, end) range of its entries,
+ *                  6 doubles per entry in VoxelGrid cell order (the CSR of fks_environment)
  *   robot          JointDev[J], per-geometry tables, points as double4 (x,y,z,w)
  *                  in geometry-major order (the order of robot_link_geometries)
  *   per-wave scratch  least-squares matrix (column-major, 3P rows x (D+1) cols),
@@ -19,8 +23,20 @@
 #include <stdint.h>
 
 #include "fks_capi.h"
+#include "fks_portable_math.h"
 
 namespace fksd {
+
+/* 4x4x4-cell bricks, bricks in VoxelGrid order (z fastest), cells inside a brick x-major
+ * and z-fastest; nb = bricks per axis (ceil(n / 4)).  256 B of floats per brick (two
+ * 128-B lines); cells past the grid's edge in the last bricks are padding, never read. */
+constexpr int kBrickShift = 2;
+constexpr int kBrickCells = 64;
+FKS_HD inline uint32_t brick_cell(const uint32_t nb[3], uint32_t i, uint32_t j, uint32_t k) {
+    const uint32_t brick = ((i >> kBrickShift) * nb[1] + (j >> kBrickShift)) * nb[2] + (k >> kBrickShift);
+    return (brick << 6) | ((i & 3u) << 4) | ((j & 3u) << 2) | (k & 3u);
+}
+FKS_HD inline uint64_t brick_total(const uint32_t nb[3]) { return (uint64_t)nb[0] * nb[1] * nb[2] * kBrickCells; }
 
 constexpr int kWave = 64;
 constexpr int kMaxLinks = 64;
@@ -36,6 +52,8 @@ struct GridDev {
     /* 1 / (res * d) for the gradient stencil widths d = 0, 1, 2 of EstimateDistance4d
      * (the same correctly rounded division, done once on the host) */
     double inv_res_span[3];
+    uint32_t nb[3]; /* bricks per axis (brick_cell) */
+    uint32_t nb_pad;
 };
 
 struct JointDev {
@@ -249,8 +267,8 @@ inline
 
 struct SimArgs {
     GridDev sdf_g, nrm_g, env_g;
-    const float* sdf;
-    const uint32_t* noff;
+    const float* sdf;     /* bricked (brick_cell over sdf_g) */
+    const uint2* nrange;  /* bricked (brick_cell over nrm_g): [begin, end) of the cell's entries */
     const double* nent;
     float oob;
     int32_t has_normals;

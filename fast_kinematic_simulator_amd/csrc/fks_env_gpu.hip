@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "fks_capi.h"
+#include "fks_device.h"
 #include "fks_env_internal.h"
 #include "fks_portable_math.h"
 
@@ -442,7 +443,63 @@ __global__ void env_analyze(const float* __restrict__ sdf, int64_t nx, int64_t n
     }
 }
 
+__global__ void env_brick_sdf(const float* __restrict__ lin, float* __restrict__ out, int64_t nx, int64_t ny, int64_t nz, uint32_t nb0,
+                              uint32_t nb1, uint32_t nb2) {
+    const uint64_t total = (uint64_t)nx * (uint64_t)ny * (uint64_t)nz;
+    const uint32_t nb[3] = {nb0, nb1, nb2};
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total; c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = c % (uint64_t)nz, j = (c / (uint64_t)nz) % (uint64_t)ny, i = c / ((uint64_t)ny * (uint64_t)nz);
+        out[fksd::brick_cell(nb, (uint32_t)i, (uint32_t)j, (uint32_t)k)] = lin[c];
+    }
+}
+
+__global__ void env_brick_ranges(const uint32_t* __restrict__ off, uint2* __restrict__ out, int64_t nx, int64_t ny, int64_t nz,
+                                 uint32_t nb0, uint32_t nb1, uint32_t nb2) {
+    const uint64_t total = (uint64_t)nx * (uint64_t)ny * (uint64_t)nz;
+    const uint32_t nb[3] = {nb0, nb1, nb2};
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total; c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = c % (uint64_t)nz, j = (c / (uint64_t)nz) % (uint64_t)ny, i = c / ((uint64_t)ny * (uint64_t)nz);
+        out[fksd::brick_cell(nb, (uint32_t)i, (uint32_t)j, (uint32_t)k)] = make_uint2(off[c], off[c + 1]);
+    }
+}
+
 }  // namespace
+
+hipError_t fks_env::brick_sdf_device(const float* lin, const int64_t n[3], const uint32_t nb[3], float** out) {
+    *out = nullptr;
+    const uint64_t padded = fksd::brick_total(nb), total = (uint64_t)n[0] * (uint64_t)n[1] * (uint64_t)n[2];
+    hipError_t e = hipMalloc((void**)out, padded * sizeof(float));
+    if (e == hipSuccess) e = hipMemset(*out, 0, padded * sizeof(float));
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(env_brick_sdf, dim3(grid_for(total, 256, 65536)), dim3(256), 0, nullptr, lin, *out, n[0], n[1], n[2], nb[0],
+                           nb[1], nb[2]);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess && *out) {
+        (void)hipFree(*out);
+        *out = nullptr;
+    }
+    return e;
+}
+
+hipError_t fks_env::brick_normal_ranges_device(const uint32_t* off, const int64_t n[3], const uint32_t nb[3], uint2** out) {
+    *out = nullptr;
+    const uint64_t padded = fksd::brick_total(nb), total = (uint64_t)n[0] * (uint64_t)n[1] * (uint64_t)n[2];
+    hipError_t e = hipMalloc((void**)out, padded * sizeof(uint2));
+    if (e == hipSuccess) e = hipMemset(*out, 0, padded * sizeof(uint2));
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(env_brick_ranges, dim3(grid_for(total, 256, 65536)), dim3(256), 0, nullptr, off, *out, n[0], n[1], n[2], nb[0],
+                           nb[1], nb[2]);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess && *out) {
+        (void)hipFree(*out);
+        *out = nullptr;
+    }
+    return e;
+}
 
 bool fks_env::analyze_sdf_device(const float* d_sdf, int64_t nx, int64_t ny, int64_t nz, double res, double* lplus,
                                  double* cmax) {

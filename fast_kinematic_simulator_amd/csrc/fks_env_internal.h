@@ -13,6 +13,10 @@
 
 #include <vector>
 
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#endif
+
 #include "fks_capi.h"
 #include "fks_portable_math.h"
 
@@ -41,6 +45,15 @@ namespace fks_env {
 /* the SDF analysis behind the kernels' skip proofs (fks_capi.cpp analyze_sdf) on a
  * device-resident SDF; false when a value is not finite or the analysis failed */
 bool analyze_sdf_device(const float* d_sdf, int64_t nx, int64_t ny, int64_t nz, double res, double* lplus, double* cmax);
+
+#if defined(__HIPCC__)
+/* the simulation kernels' HBM layout (fks_device.h brick_cell): the VoxelGrid-order SDF
+ * `lin` (n cells per axis) copied into 4x4x4-cell bricks (nb bricks per axis), and the
+ * CSR offsets `off` (cells + 1) turned into a bricked [begin, end) range per cell; the
+ * outputs are new device allocations the caller frees */
+hipError_t brick_sdf_device(const float* lin, const int64_t n[3], const uint32_t nb[3], float** out);
+hipError_t brick_normal_ranges_device(const uint32_t* off, const int64_t n[3], const uint32_t nb[3], uint2** out);
+#endif
 
 FKS_HD inline double dot3(double a0, double a1, double a2, double b0, double b1, double b2) {
     return (a0 * b0 + a1 * b1) + a2 * b2;

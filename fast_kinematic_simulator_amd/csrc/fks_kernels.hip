@@ -429,8 +429,9 @@ __device__ __forceinline__ bool grid_index(const GridDev& g, const D4& p, int32_
     }
     return ok;
 }
-__device__ __forceinline__ uint32_t grid_linear(const GridDev& g, int32_t i, int32_t j, int32_t k) {
-    return ((uint32_t)i * (uint32_t)g.n[1] + (uint32_t)j) * (uint32_t)g.n[2] + (uint32_t)k;
+/* the SDF's and normal ranges' HBM position of in-bounds cell (i, j, k) (fks_device.h) */
+__device__ __forceinline__ uint32_t grid_brick(const GridDev& g, int32_t i, int32_t j, int32_t k) {
+    return brick_cell(g.nb, (uint32_t)i, (uint32_t)j, (uint32_t)k);
 }
 
 struct Sim {
@@ -576,12 +577,12 @@ __device__ double estimate_distance(const SimArgs& A, const D4& p, bool* inb, ui
         lo[a] = (idx[a] - 1 > 0) ? idx[a] - 1 : 0;
         hi[a] = ((int64_t)idx[a] + 1 < g.n[a] - 1) ? idx[a] + 1 : (int32_t)(g.n[a] - 1);
         const double inv = g.inv_res_span[hi[a] - lo[a]]; /* 1.0 / (g.res * (hi - lo)), hi - lo in {0, 1, 2} */
-        const float diff = gp(A.sdf)[grid_linear(g, hi[0], hi[1], hi[2])] - gp(A.sdf)[grid_linear(g, lo[0], lo[1], lo[2])];
+        const float diff = gp(A.sdf)[grid_brick(g, hi[0], hi[1], hi[2])] - gp(A.sdf)[grid_brick(g, lo[0], lo[1], lo[2])];
         grad[a] = (double)diff * inv;
     }
     const D3 c = xform3(g.org, D3{g.res * ((double)idx[0] + 0.5), g.res * ((double)idx[1] + 0.5), g.res * ((double)idx[2] + 0.5)});
     const double dx = p.x - c.x, dy = p.y - c.y, dz = p.z - c.z;
-    const double nominal = (double)gp(A.sdf)[grid_linear(g, idx[0], idx[1], idx[2])];
+    const double nominal = (double)gp(A.sdf)[grid_brick(g, idx[0], idx[1], idx[2])];
     const double corrected = (nominal >= 0.0) ? nominal - (g.res * 0.5) : nominal + (g.res * 0.5);
     const double adjustment = (dx * grad[0] + dy * grad[1]) + dz * grad[2];
     const double estimate = corrected + adjustment;
@@ -595,11 +596,13 @@ __device__ bool lookup_normal(const SimArgs& A, const D4& loc, const D4& dir, D3
     *out = D3{0.0, 0.0, 0.0};
     int32_t idx[3];
     if (!A.has_normals || !grid_index(A.nrm_g, loc, idx)) return false;
-    const uint32_t lin = grid_linear(A.nrm_g, idx[0], idx[1], idx[2]);
-    const uint32_t begin = gp(A.noff)[lin], end = gp(A.noff)[lin + 1];
-    *bytes += 8;
+    /* one 8-byte load: begin in the low word, end in the high word (uint2 x, y) */
+    const uint64_t range = gp(reinterpret_cast<const uint64_t*>(A.nrange))[grid_brick(A.nrm_g, idx[0], idx[1], idx[2])];
+    const uint32_t begin = (uint32_t)range, end = (uint32_t)(range >> 32);
+    /* 4 B for the cell, 56 B per entry examined (Vector4d + Vector3d, SPCS:52-53) */
+    *bytes += 4;
     if (begin == end) return true;
-    *bytes += 48ull * (uint64_t)(end - begin);
+    *bytes += 56ull * (uint64_t)(end - begin);
     const double direction_norm = dsqrt(sqnorm4(dir));
     if (!(direction_norm > 0.0)) {
         *err |= FKS_PARTICLE_ERR_ZERO_DIRECTION;
@@ -1158,7 +1161,7 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
     }
     float d = A.oob;
     if (ok) {
-        d = gp(A.sdf)[grid_linear(g, idx[0], idx[1], idx[2])];
+        d = gp(A.sdf)[grid_brick(g, idx[0], idx[1], idx[2])];
         *b += 4;
         *S = (double)d;
         *G = margin;

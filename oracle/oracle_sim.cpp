@@ -201,9 +201,11 @@ struct NormalGrid {
         if (offsets == nullptr || !g.LocationToGridIndex4d(location, idx)) return false;
         const size_t lin = g.Linear(idx[0], idx[1], idx[2]);
         const uint32_t begin = offsets[lin], end = offsets[lin + 1];
-        *bytes += 8;
+        /* 4 B for the cell, 56 B per entry examined (a StoredSurfaceNormal is a
+         * Vector4d entry direction + Vector3d normal, SPCS:52-53) */
+        *bytes += 4;
         if (begin == end) return true;
-        *bytes += 48ull * (uint64_t)(end - begin);
+        *bytes += 56ull * (uint64_t)(end - begin);
         const double direction_norm = fks_math::dsqrt(sqnorm4(direction));
         if (!(direction_norm > 0.0)) {
             *err |= FKS_PARTICLE_ERR_ZERO_DIRECTION; /* assert(direction_norm > 0.0), SPCS:115 */
