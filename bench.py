@@ -175,7 +175,6 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config-check", action="store_true", help="skip the batched CheckConfigCollision line")
     ap.add_argument("--segment-steps", type=int, default=-1, help="A/B: fks_set_segment_steps (default: automatic)")
-    ap.add_argument("--no-coop", action="store_true", help="A/B: fks_set_cooperative(0), one wave per particle")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -215,8 +214,6 @@ def main():
     sim = make_linked_simulator(denv, wl.solver, wl.controller_frequency, wl.seed, device=local_rank)
     if args.segment_steps >= 0:
         sim.set_segment_steps(args.segment_steps)
-    if args.no_coop:
-        sim.set_cooperative(False)
     sim.set_robot(wl.robot)
     Wd = wl.robot.config_width
     dev = torch.device("cuda", local_rank)

@@ -165,7 +165,7 @@ class CallCounters(ctypes.Structure):
         ("least_squares_rows", c_uint64),
         ("self_collision_checks", c_uint64),
         ("self_corrected_points", c_uint64),
-        ("cooperative_tasks", c_uint64),  # ABI 6 (ABI 4's proven_free_microsteps slot)
+        ("reserved0", c_uint64),  # ABI 4: proven_free_microsteps
     ]
 
     def as_dict(self):
@@ -266,7 +266,6 @@ PROTOTYPES = [
     ("fks_set_segment_steps", c_int32, [c_void_p, c_uint32]),
     ("fks_set_segment_policy", c_int32, [c_void_p, c_uint32, c_uint32]),
     ("fks_set_individual_jacobians", c_int32, [c_void_p, c_int32]),
-    ("fks_set_cooperative", c_int32, [c_void_p, c_int32]),
     ("fks_env_build", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), POINTER(c_void_p)]),
     ("fks_env_build_gpu", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), c_int32,
                                     POINTER(c_void_p), POINTER(EnvBuildStats)]),

@@ -252,7 +252,6 @@ struct fks_context {
     uint32_t heavy_per_step = kHeavyResolverPerStep; /* fks_set_segment_policy */
     uint32_t heavy_priority = 1;
     int32_t individual_jacobians = 0; /* fks_set_individual_jacobians (SPCS:420-423) */
-    int32_t cooperative = 1;          /* fks_set_cooperative */
     bool fk_pair = false;             /* paired FK of free microsteps (fks_set_robot) */
     double* d_seg_state = nullptr;
     uint32_t* d_seg_done = nullptr;
@@ -890,7 +889,6 @@ static fks_status settle(fks_context* ctx) {
     ctx->last.least_squares_rows = c[fksd::kCntLsqRows];
     ctx->last.self_collision_checks = c[fksd::kCntSelfChecks];
     ctx->last.self_corrected_points = c[fksd::kCntSelfPoints];
-    ctx->last.cooperative_tasks = c[fksd::kCoopTasks];
     for (int k = 0; k < FKS_NUM_PHASES; ++k) {
         ctx->phase_last[k] = c[fksd::kPhaseBase + k];
         ctx->phase_total[k] += ctx->phase_last[k];
@@ -909,7 +907,6 @@ static fks_status settle(fks_context* ctx) {
     ctx->total.least_squares_rows += ctx->last.least_squares_rows;
     ctx->total.self_collision_checks += ctx->last.self_collision_checks;
     ctx->total.self_corrected_points += ctx->last.self_corrected_points;
-    ctx->total.cooperative_tasks += ctx->last.cooperative_tasks;
     ctx->total.kernel_ms += ctx->last.kernel_ms;
     ctx->total.call_ms += ctx->last.call_ms;
     ctx->total.calls += 1;
@@ -1035,19 +1032,13 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
         a.tr_step_cap = tr->step_cap;
         a.tr_cfg_cap = tr->cfg_cap;
     }
-    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, fksd::kCounterWords * sizeof(unsigned long long), s));
-    /* cooperative point rounds: the idle waves of a workgroup serve its busy ones; a batch
-     * no larger than the grid and run whole is spread one particle per wave over up to
-     * grid_groups workgroups (wave w of workgroup b: particle w * grid + b) */
-    a.coop = (ctx->cooperative && ctx->waves_per_group > 1) ? 1u : 0u;
-    a.spread = (a.coop && a.nseg == 1 && n <= (uint64_t)ctx->grid_waves) ? 1u : 0u;
-    const uint64_t groups_needed = a.spread ? n : (n + ctx->waves_per_group - 1) / ctx->waves_per_group;
-    const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? (groups_needed > 0 ? groups_needed : 1)
-                                                                                  : ctx->grid_groups);
-    a.self = static_cast<const fksd::SimArgs*>(ctx->d_args);
     /* the previous call has settled, so the pinned staging copy is free */
     *ctx->h_args = a;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, fksd::kCounterWords * sizeof(unsigned long long), s));
+    const uint64_t groups_needed = (n + ctx->waves_per_group - 1) / ctx->waves_per_group;
+    const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? (groups_needed > 0 ? groups_needed : 1)
+                                                                                  : ctx->grid_groups);
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
     hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type) : kernel_for(ctx->R.type, ctx->individual_jacobians != 0),
                        dim3(grid),
@@ -1501,12 +1492,6 @@ fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_
 fks_status fks_set_individual_jacobians(fks_context* ctx, int32_t simulate_with_individual_jacobians) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
     ctx->individual_jacobians = simulate_with_individual_jacobians ? 1 : 0;
-    return FKS_OK;
-}
-
-fks_status fks_set_cooperative(fks_context* ctx, int32_t enable) {
-    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
-    ctx->cooperative = enable ? 1 : 0;
     return FKS_OK;
 }
 

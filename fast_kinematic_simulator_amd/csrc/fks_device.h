@@ -123,15 +123,8 @@ struct RobotDev {
  * `shared_total` doubles); every other offset is relative to the wave's own block of
  * `total` doubles that follows. */
 constexpr int kWavesPerGroup = 4;
-/* cooperative point rounds (fks_kernels.hip "cooperative point rounds"): a 16-double
- * header (u32 words: idle mask, task word, leadership, two completion counters, task
- * kind, leader wave, transform offsets, flags, skip mask; then err / self count / bytes
- * per participant) and 2 doubles per 64-point round (mask, bytes of the round, bytes up
- * to its first colliding point) */
-constexpr uint32_t kCoopHeader = 16;
-constexpr uint32_t kCoopRound = 2;
 struct LdsLayout {
-    uint32_t joints, ctrl, base, dofj, gbox, gpairs, rounds, coop, shared_total;
+    uint32_t joints, ctrl, base, dofj, gbox, gpairs, rounds, shared_total;
     uint32_t rstate, noise, noise_err, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u,
         ustep, x, real, axis_w, orig_w, colsq, hcoef, box, misc, ints, jm2, total;
     uint32_t fk_pair; /* 1: the free-motion microsteps pair their FK chains (jm2 allocated) */
@@ -160,8 +153,6 @@ inline
     o = (o + 1u) & ~1u;
     l.rounds = o; /* per 64-point round r < 64: (double)link, radius (RoundDev) */
     o += 2u * (uint32_t)(NR < 1 ? 1 : (NR > 64 ? 64 : NR));
-    l.coop = o; /* cooperative point rounds (CoopWords): header, per-participant and per-round results */
-    o += kCoopHeader + kCoopRound * (uint32_t)(NR < 1 ? 1 : (NR > 64 ? 64 : NR));
     l.shared_total = o;
     /* per wave */
     o = 0;
@@ -243,7 +234,7 @@ inline
 
 /* per-wave scratch layout (doubles) */
 struct ScratchLayout {
-    uint64_t J, b, keys, corr, flag, cand, list, cellw, dense, cstage, total;
+    uint64_t J, b, keys, corr, flag, cand, list, cellw, dense, total;
 };
 inline
 #if defined(__HIPCC__)
@@ -270,8 +261,6 @@ inline
     o += 2u * kMaxGeoms + 4u * kMaxGeoms;
     l.dense = o;
     o += (G > 1) ? self_dense_words(G) : 8;
-    l.cstage = o; /* cooperative corrections: per point its correction and world position (6) */
-    o += 6ull * (uint64_t)P;
     l.total = (o + 7) & ~7ull;
     return l;
 }
@@ -330,11 +319,11 @@ struct SimArgs {
     uint32_t seg_stride;          /* doubles per particle in seg_state */
     uint32_t seg_heavy_resolver;  /* resolver iterations that mark a segment contact-heavy (0: off) */
     uint32_t seg_heavy_prio;      /* waves carrying a heavy particle raise their issue priority */
-    uint32_t coop;                /* idle waves of a workgroup evaluate a busy sibling's point rounds (fks_set_cooperative) */
+    uint32_t seg_pad;
     double* scratch;
     uint64_t scratch_per_wave; /* doubles */
     uint32_t row_cap;          /* 3 * P */
-    uint32_t spread;           /* batch <= grid waves, one segment: wave w of workgroup b runs particle w * grid + b */
+    uint32_t pad2;
     LdsLayout L;               /* per-wave LDS carve-out */
     ScratchLayout SL;          /* per-wave scratch carve-out */
     double self_res;           /* batched CheckConfigCollision: extended-cell size (SPCS:1404) */
@@ -350,11 +339,6 @@ struct SimArgs {
     int32_t kin_mode;
     int32_t kin_pad;
     double* kin_out;
-    /* this block's own device address: the cooperative helpers' out-of-line loop reads the
-     * arguments through it, so the kernel's restrict argument pointer is never passed to a
-     * call that the optimiser cannot prove leaves it uncaptured (the kernel's argument
-     * reads would otherwise stop being scalar loads) */
-    const SimArgs* self;
 };
 
 enum {
@@ -381,8 +365,7 @@ enum {
  * particle queue in the counter buffer; order = FKS_PHASE_* in fks_capi.h */
 enum {
     kPhaseBase = kNumCounters + 2,
-    kCoopTasks = kPhaseBase + FKS_NUM_PHASES, /* cooperative point-round tasks handed to helpers */
-    kCounterWords = kCoopTasks + 1
+    kCounterWords = kPhaseBase + FKS_NUM_PHASES
 };
 
 }  // namespace fksd

@@ -1090,124 +1090,6 @@ __device__ __forceinline__ void round_update(Sim& s, int r, const double* T, dou
     }
 }
 
-/* ---------------- cooperative point rounds ----------------
- * A wave whose particle is done and that finds the ticket queue drained (or, in a batch
- * smaller than the grid, a wave that got no particle) does not leave: it sets its bit in
- * the workgroup's idle mask and serves as a helper.  A sibling wave still running a
- * particle (the leader) hands a share of the 64-point rounds of its environment check and
- * of its correction pass to the idle waves, so a contact-heavy particle's point rounds run
- * on up to four waves; everything else (FK chain, least squares, control) stays on the
- * leader.  Every round is evaluated with exactly the single-wave arithmetic and the
- * results are merged in round order, so outputs and counted bytes are bit-identical.
- *
- * Protocol (u32 words of A.L.coop, workgroup-scope atomics in LDS): leadership is a CAS
- * on kCoopLead; the leader writes the task, then the task word (seq << 8 | participant
- * mask) with release; a participant acquires the word, runs its share, writes its
- * results and adds 1 to kCoopDone with release; the leader waits for participants - 1.
- * Helpers wait only for a task or for the end (every wave of the workgroup idle); a
- * leader waits only for helpers that were idle when it posted, and idle bits are never
- * cleared, so every wait ends. */
-enum {
-    kCoopIdle = 0, /* bit w: wave w serves as a helper */
-    kCoopWord,     /* task word: seq << 8 | participant mask */
-    kCoopLead,     /* 0, or 1 + the wave that holds the helpers */
-    kCoopDoneA,    /* participants past phase A (corrections) */
-    kCoopDone,     /* helpers finished */
-    kCoopKind,
-    kCoopLeader,
-    kCoopTc,       /* LDS offsets (doubles from the workgroup's LDS base) */
-    kCoopTp,
-    kCoopFlags,    /* bit 0: the self-collision map is non-empty */
-    kCoopSkipLo,
-    kCoopSkipHi,
-    kCoopCfg,
-    kCoopPart = 16 /* per participant rank: err, self-corrected points, bytes (u64) */
-};
-enum { kCoopTaskEnv = 1, kCoopTaskCorr = 2 };
-#ifndef FKS_COOP_SERVE
-#define FKS_COOP_SERVE 1
-#endif
-#ifndef FKS_COOP_ENV
-#define FKS_COOP_ENV 1
-#endif
-#ifndef FKS_COOP_CORR
-#define FKS_COOP_CORR 1
-#endif
-constexpr uint32_t kCoopDeclined = 0xffffffffu;
-#ifndef FKS_COOP_LEAD_ATTR
-#define FKS_COOP_LEAD_ATTR __noinline__
-#endif
-constexpr int kCoopMinEnvRounds = 3;  /* one wave evaluates two rounds at a time */
-constexpr int kCoopMinCorrRounds = 2; /* the single-wave correction pass takes one round at a time */
-constexpr int kCoopMinHelpers = 2;    /* the leader only waits: one helper would just move its work */
-struct CoopEnvResult {
-    uint32_t hit; /* kCoopDeclined: no helpers taken, run the rounds alone */
-    uint32_t pad;
-    uint64_t bytes;
-};
-struct CoopCorrResult {
-    uint32_t rows; /* kCoopDeclined as above */
-    uint32_t err;
-    uint64_t bytes;
-};
-
-__device__ __forceinline__ uint32_t* coop_words(const SimArgs& A, double* shared) {
-    return reinterpret_cast<uint32_t*>(shared + A.L.coop);
-}
-__device__ __forceinline__ uint32_t lds_acquire(uint32_t* p) {
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-__device__ __forceinline__ void lds_release(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void coop_wait(uint32_t* p, uint32_t target) {
-    while (lds_acquire(p) != target) __builtin_amdgcn_s_sleep(1);
-}
-/* the wave's index in its workgroup (misc + 6 of its LDS block, set once) */
-__device__ __forceinline__ uint32_t& coop_self(const SimArgs& A, double* lds) {
-    return reinterpret_cast<uint32_t*>(lds + A.L.misc)[12];
-}
-/* cooperative tasks this wave handed out (misc + 7 of its LDS block, flushed at the end) */
-__device__ __forceinline__ uint64_t& coop_tasks(const SimArgs& A, double* lds) { return reinterpret_cast<uint64_t*>(lds + A.L.misc)[7]; }
-/* idle siblings that could take rounds now */
-__device__ __forceinline__ uint32_t coop_helpers(const Sim& s) {
-    uint32_t* w = coop_words(*s.A, s.shared);
-    const uint32_t me = (uint32_t)__builtin_amdgcn_readfirstlane((int)coop_self(*s.A, s.lds));
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(w + kCoopIdle, __ATOMIC_RELAXED,
-                                                                         __HIP_MEMORY_SCOPE_WORKGROUP)) &
-           ~(1u << me);
-}
-/* the k-th set bit of `rounds` belongs to participant k mod np */
-__device__ __forceinline__ uint64_t coop_share(uint64_t rounds, int rank, int np) {
-    uint64_t mine = 0;
-    int k = 0;
-    while (rounds) {
-        const int r = __ffsll((unsigned long long)rounds) - 1;
-        rounds &= rounds - 1ull;
-        if (k == rank) mine |= 1ull << r;
-        k = (k + 1 == np) ? 0 : k + 1;
-    }
-    return mine;
-}
-__device__ __forceinline__ uint64_t coop_all_rounds(int nrounds) {
-    return (nrounds >= kWave) ? ~0ull : ((1ull << nrounds) - 1ull);
-}
-/* round_update for a round of the leader's skip-proof cache (rstate of its LDS block) */
-__device__ __forceinline__ void coop_round_update(const SimArgs& A, const double* shared, double* rstate, int ln, int r, const double* T,
-                                                  double S, double G, double C) {
-    if (!A.skip_enabled || r >= kWave || r >= A.R.nrounds) return;
-    const int link = (int)shared[A.L.rounds + 2 * r];
-    if (link < 0) return;
-    const double smin = wave_min(S), gmin = wave_min(G), cmin = wave_min(C);
-    double* st = rstate + kRoundState * r;
-    if (ln < 12) st[ln] = T[12 * link + ln];
-    if (ln == 0) {
-        st[12] = smin;
-        st[13] = gmin;
-        st[14] = cmin;
-    }
-}
-
 /* EstimateMaxControlInputWorkspaceMotion over two transform sets (SPCS:1492-1527).
  * The result is the exact max over all points; rounds whose rigid-motion bound
  * cannot reach the max of the round with the largest bound are not evaluated. */
@@ -1299,122 +1181,6 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
     return false;
 }
 
-/* round r's entry of the cooperative results: colliding-lane mask, then the bytes of the
- * whole round (low word) and up to and including its first colliding point (high word) */
-__device__ __forceinline__ void coop_round_result(double* res, int r, int ln, bool c, uint64_t b) {
-    const uint64_t m = __ballot(c);
-    const int first = m ? __ffsll((unsigned long long)m) - 1 : kWave - 1;
-    const uint64_t all = wave_sum_u64(b), upto = wave_sum_u64(ln <= first ? b : 0ull);
-    if (ln == 0) {
-        uint64_t* q = reinterpret_cast<uint64_t*>(res + kCoopRound * r);
-        q[0] = m;
-        q[1] = (upto << 32) | all;
-    }
-}
-
-/* a participant's share of a cooperative environment check: the rounds not proven free,
- * dealt round-robin over the participants, two at a time so their gathers overlap; the
- * leader's skip-proof cache is updated for every round evaluated */
-__device__ __forceinline__ void coop_env_work(const SimArgs& A, double* shared, double* lead, int ln, const double* T, uint64_t skip,
-                                              int rank, int np) {
-    double* res = shared + A.L.coop + kCoopHeader;
-    uint64_t mine = coop_share(~skip & coop_all_rounds(A.R.nrounds), rank, np);
-    while (mine) {
-        const int r0 = __ffsll((unsigned long long)mine) - 1;
-        mine &= mine - 1ull;
-        int r1 = -1;
-        if (mine) {
-            r1 = __ffsll((unsigned long long)mine) - 1;
-            mine &= mine - 1ull;
-        }
-        uint64_t b0 = 0, b1 = 0;
-        double S0 = __builtin_huge_val(), S1 = __builtin_huge_val(), G0 = __builtin_huge_val(), G1 = __builtin_huge_val();
-        double C0 = __builtin_huge_val(), C1 = __builtin_huge_val();
-        const bool c0 = env_point(A, T, kWave * r0 + ln, &b0, &S0, &G0, &C0);
-        bool c1 = false;
-        if (r1 >= 0) c1 = env_point(A, T, kWave * r1 + ln, &b1, &S1, &G1, &C1);
-        coop_round_update(A, shared, lead + A.L.rstate, ln, r0, T, S0, G0, C0);
-        coop_round_result(res, r0, ln, c0, b0);
-        if (r1 >= 0) {
-            coop_round_update(A, shared, lead + A.L.rstate, ln, r1, T, S1, G1, C1);
-            coop_round_result(res, r1, ln, c1, b1);
-        }
-    }
-}
-
-/* take the workgroup's helpers (one leader at a time); false if a sibling holds them */
-__device__ __forceinline__ bool coop_lead_acquire(uint32_t* w, uint32_t me, int ln) {
-    uint32_t got = 0;
-    if (ln == 0) {
-        uint32_t expect = 0;
-        got = __hip_atomic_compare_exchange_strong(w + kCoopLead, &expect, 1u + me, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP)
-                  ? 1u
-                  : 0u;
-    }
-    return __builtin_amdgcn_readlane((int)got, 0) != 0;
-}
-
-/* post a task to the helpers in `mask` (lane 0 has written its arguments) */
-__device__ __forceinline__ void coop_post(uint32_t* w, uint32_t kind, uint32_t me, uint32_t mask, int ln) {
-    if (ln == 0) {
-        w[kCoopDone] = 0;
-        w[kCoopDoneA] = 0;
-        w[kCoopKind] = kind;
-        w[kCoopLeader] = me;
-        const uint32_t word = w[kCoopWord];
-        lds_release(w + kCoopWord, (((word >> 8) + 1u) << 8) | mask);
-    }
-}
-
-/* CheckEnvironmentCollision on the helpers: they evaluate every round not proven free
- * while the leader waits, then the single-wave outcome is read off in round order: the
- * first round with a colliding point decides, and the bytes are those of the rounds before
- * it (4 B per point of a proven-free round) plus its own up to that point.  The leader
- * takes no share itself, so this stays a few LDS operations inside its hot loop (no call). */
-__device__ FKS_COOP_LEAD_ATTR CoopEnvResult coop_env_lead(const SimArgs* __restrict__ Ap, double* shared, double* lds, int ln,
-                                                         const double* T, uint64_t skip) {
-    const SimArgs& A = *Ap;
-    const RobotDev& R = A.R;
-    uint32_t* w = coop_words(A, shared);
-    const uint32_t me = (uint32_t)__builtin_amdgcn_readfirstlane((int)coop_self(A, lds));
-    CoopEnvResult out{kCoopDeclined, 0u, 0ull};
-    if (!coop_lead_acquire(w, me, ln)) return out;
-    const uint32_t mask = lds_acquire(w + kCoopIdle);
-    if (ln == 0) {
-        w[kCoopTc] = (uint32_t)(T - shared);
-        w[kCoopSkipLo] = (uint32_t)skip;
-        w[kCoopSkipHi] = (uint32_t)(skip >> 32);
-    }
-    coop_post(w, kCoopTaskEnv, me, mask, ln);
-    coop_wait(w + kCoopDone, (uint32_t)__popc(mask));
-    const double* res = shared + A.L.coop + kCoopHeader;
-    uint64_t all = 0, upto = 0, m = 0;
-    bool ev = false;
-    if (ln < R.nrounds) {
-        if ((skip >> ln) & 1ull) {
-            const int left = R.P - kWave * ln;
-            all = 4ull * (uint64_t)(left < kWave ? left : kWave);
-        } else {
-            const uint64_t* q = reinterpret_cast<const uint64_t*>(res + kCoopRound * ln);
-            m = q[0];
-            all = q[1] & 0xffffffffull;
-            upto = q[1] >> 32;
-            ev = true;
-        }
-    }
-    const uint64_t hits = __ballot(ev && m != 0ull);
-    const int rc = hits ? __ffsll((unsigned long long)hits) - 1 : kWave;
-    out.bytes = wave_sum_u64(ln < rc ? all : (ln == rc ? upto : 0ull));
-    out.hit = hits ? 1u : 0u;
-    wsync();
-    if (ln == 0) {
-        lds_release(w + kCoopLead, 0u);
-        coop_tasks(A, lds)++;
-    }
-    return out;
-}
-
 /* CheckEnvironmentCollision (SPCS:921-981) with threshold 0: two 64-point rounds are
  * evaluated together (their loads overlap), stopping after the pair holding the first
  * colliding point; algorithmic bytes are counted up to that point, as the reference
@@ -1433,16 +1199,6 @@ __device__ FKS_HOT_ATTR bool env_collision(Sim& s, const double* T) {
             if (s.lane < R.P) s.lane_bytes += 4ull * (uint64_t)((R.P - s.lane + kWave - 1) / kWave);
             count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (uint64_t)R.nrounds);
             return false;
-        }
-        if (FKS_COOP_ENV && !FULL && A.coop && __popcll(~skip & all) >= kCoopMinEnvRounds) {
-            /* idle sibling waves take a share of the rounds (cooperative point rounds) */
-            if (__popc(coop_helpers(s)) >= kCoopMinHelpers) {
-                const CoopEnvResult r = coop_env_lead(A.self, s.shared, s.lds, s.lane, T, skip);
-                if (r.hit != kCoopDeclined) {
-                    if (s.lane == 0) s.lane_bytes += r.bytes;
-                    return r.hit != 0u;
-                }
-            }
         }
     }
     for (int base = 0, r = 0; base < R.P; base += 2 * kWave, r += 2) {
@@ -1951,174 +1707,19 @@ __device__ void joint_frames(Sim& s, const double* Tc) {
     wsync();
 }
 
-/* one point of CollectPointCorrectionsAndJacobians (SPCS:1836-1925): the point's world
- * position, its correction (self-collision from the scratch tables, then the environment's
- * EstimateDistance + surface normal) and whether it has one.  A round proven free of
- * corrections (skr) counts its EstimateDistance bytes without reading them. */
-__device__ __forceinline__ bool point_correction(const SimArgs& A, const double* Tp, const double* Tc, const FKS_GLOBAL double* corr,
-                                                 const FKS_GLOBAL double* flag, bool self_nonempty, bool skr, int i,
-                                                 uint64_t* bytes, uint32_t* err, D3* pc, D4* xcp, int* linkp) {
-    const RobotDev& R = A.R;
-    bool has = false;
-    D3 pcorr{0.0, 0.0, 0.0};
-    D4 xc{0.0, 0.0, 0.0, 0.0};
-    int link = 0;
-    if (i < R.P) {
-        const D4 p = load_point(R, i);
-        link = gp(R.point_link)[i];
-        xc = xform4(Tc + 12 * link, p);
-        const bool has_self = self_nonempty && flag[i] != 0.0;
-        bool inb = false;
-        double est = 0.0;
-        if (skr)
-            *bytes += 28;
-        else
-            est = estimate_distance(A, xc, &inb, bytes);
-        const bool has_env = (est < 0.0) && inb;
-        D3 ecorr{0.0, 0.0, 0.0};
-        if (has_env) {
-            const D4 xp = xform4(Tp + 12 * link, p);
-            const D4 motion{xc.x - xp.x, xc.y - xp.y, xc.z - xp.z, xc.w - xp.w};
-            const D4 nm = safe_normal4(motion);
-            D3 raw;
-            const bool ok = lookup_normal(A, xc, nm, &raw, err, bytes);
-            if (!ok) *err |= FKS_PARTICLE_ERR_NORMAL_OOB;
-            const D3 g = safe_normal3(raw);
-            const double pen = dabs(0.0 - est);
-            ecorr = D3{g.x * pen, g.y * pen, g.z * pen};
-        }
-        has = has_self || has_env;
-        if (has_self) pcorr = D3{pcorr.x + corr[3 * i], pcorr.y + corr[3 * i + 1], pcorr.z + corr[3 * i + 2]};
-        if (has_env) pcorr = D3{pcorr.x + ecorr.x, pcorr.y + ecorr.y, pcorr.z + ecorr.z};
-    }
-    *pc = pcorr;
-    *xcp = xc;
-    *linkp = link;
-    return has;
-}
-
-/* the three stacked rows of one corrected point (SPCS:1926-1935): b = its correction,
- * J = ComputeLinkPointTranslationJacobian at its world position */
-template <int RT>
-__device__ __forceinline__ void write_point_rows(const SimArgs& A, const JointDev* joints, const int32_t* dofj, const double* axw,
-                                                 const double* orw, const double* cfg, FKS_GLOBAL double* J, FKS_GLOBAL double* bv,
-                                                 uint32_t row, const D3& pcorr, const D4& xc, int link) {
-    const RobotDev& R = A.R;
-    const uint32_t rc = A.row_cap;
-    const int D = R.D;
-    bv[row + 0] = pcorr.x;
-    bv[row + 1] = pcorr.y;
-    bv[row + 2] = pcorr.z;
-    if constexpr (RT == FKS_ROBOT_LINKED) {
-        const uint64_t mask = gp(R.link_dof_mask)[link];
-        for (int d = 0; d < D; ++d) {
-            D3 col{0.0, 0.0, 0.0};
-            if ((mask >> d) & 1ull) {
-                const D3 aw{axw[3 * d], axw[3 * d + 1], axw[3 * d + 2]};
-                const int jt = joints[dofj[d]].type;
-                if (jt == FKS_JOINT_PRISMATIC) {
-                    col = aw;
-                } else {
-                    col = cross(aw, D3{xc.x - orw[3 * d], xc.y - orw[3 * d + 1], xc.z - orw[3 * d + 2]});
-                }
-                col = D3{0.0 + col.x, 0.0 + col.y, 0.0 + col.z};
-            }
-            J[(uint64_t)d * rc + row + 0] = col.x;
-            J[(uint64_t)d * rc + row + 1] = col.y;
-            J[(uint64_t)d * rc + row + 2] = col.z;
-        }
-    } else if constexpr (RT == FKS_ROBOT_SE2) {
-        J[0 * rc + row + 0] = 0.0 + 1.0;
-        J[0 * rc + row + 1] = 0.0;
-        J[0 * rc + row + 2] = 0.0;
-        J[1 * rc + row + 0] = 0.0;
-        J[1 * rc + row + 1] = 0.0 + 1.0;
-        J[1 * rc + row + 2] = 0.0;
-        const D3 c2 = cross(D3{0.0, 0.0, 1.0}, D3{xc.x - cfg[0], xc.y - cfg[1], xc.z - 0.0});
-        J[2 * rc + row + 0] = 0.0 + c2.x;
-        J[2 * rc + row + 1] = 0.0 + c2.y;
-        J[2 * rc + row + 2] = 0.0 + c2.z;
-    } else {
-        const D3 d{xc.x - cfg[3], xc.y - cfg[7], xc.z - cfg[11]};
-        for (int a = 0; a < 3; ++a) {
-            const D3 axis{cfg[a], cfg[4 + a], cfg[8 + a]};
-            J[(uint64_t)a * rc + row + 0] = 0.0 + axis.x;
-            J[(uint64_t)a * rc + row + 1] = 0.0 + axis.y;
-            J[(uint64_t)a * rc + row + 2] = 0.0 + axis.z;
-            const D3 c = cross(axis, d);
-            J[(uint64_t)(3 + a) * rc + row + 0] = 0.0 + c.x;
-            J[(uint64_t)(3 + a) * rc + row + 1] = 0.0 + c.y;
-            J[(uint64_t)(3 + a) * rc + row + 2] = 0.0 + c.z;
-        }
-    }
-}
-
-
-/* CollectPointCorrectionsAndJacobians on the helpers (see coop_corr_work) while the
- * leader waits: returns the row count, or kCoopDeclined if a sibling holds the helpers */
-__device__ FKS_COOP_LEAD_ATTR CoopCorrResult coop_corr_lead(const SimArgs* __restrict__ Ap, double* shared, double* lds, int ln,
-                                                           const double* Tp, const double* Tc, const double* cfg, uint64_t skip,
-                                                           bool self_nonempty) {
-    const SimArgs& A = *Ap;
-    const RobotDev& R = A.R;
-    uint32_t* w = coop_words(A, shared);
-    const uint32_t me = (uint32_t)__builtin_amdgcn_readfirstlane((int)coop_self(A, lds));
-    CoopCorrResult out{kCoopDeclined, 0u, 0ull};
-    if (!coop_lead_acquire(w, me, ln)) return out;
-    const uint32_t mask = lds_acquire(w + kCoopIdle);
-    const int np = __popc(mask);
-    if (ln == 0) {
-        w[kCoopTc] = (uint32_t)(Tc - shared);
-        w[kCoopTp] = (uint32_t)(Tp - shared);
-        w[kCoopCfg] = (uint32_t)(cfg - shared);
-        w[kCoopFlags] = self_nonempty ? 1u : 0u;
-        w[kCoopSkipLo] = (uint32_t)skip;
-        w[kCoopSkipHi] = (uint32_t)(skip >> 32);
-    }
-    coop_post(w, kCoopTaskCorr, me, mask, ln);
-    coop_wait(w + kCoopDone, (uint32_t)np);
-    const double* res = shared + A.L.coop + kCoopHeader;
-    const uint64_t work = self_nonempty ? coop_all_rounds(R.nrounds) : (~skip & coop_all_rounds(R.nrounds));
-    uint64_t rows = 0, bytes = 0;
-    if (ln < R.nrounds) {
-        if ((work >> ln) & 1ull) {
-            rows = (uint64_t)__popcll(reinterpret_cast<const uint64_t*>(res + kCoopRound * ln)[0]);
-        } else {
-            const int left = R.P - kWave * ln;
-            bytes = 28ull * (uint64_t)(left < kWave ? left : kWave); /* proven free: counted, not read */
-        }
-    }
-    uint32_t err = 0, selfk = 0;
-    if (ln < np) {
-        const uint32_t* slot = w + kCoopPart + 4 * ln;
-        err = slot[0];
-        selfk = slot[1];
-        bytes += *reinterpret_cast<const uint64_t*>(slot + 2);
-    }
-    out.rows = 3u * (uint32_t)wave_sum_u64(rows);
-    out.bytes = wave_sum_u64(bytes);
-    out.err = wave_or(err);
-    const uint32_t k = (uint32_t)wave_sum_u64(selfk);
-    if (self_nonempty && ln == 0) reinterpret_cast<uint64_t*>(lds + A.L.misc + 28)[1] += k;
-    wsync();
-    if (ln == 0) {
-        lds_release(w + kCoopLead, 0u);
-        coop_tasks(A, lds)++;
-    }
-    return out;
-}
-
 /* CollectPointCorrectionsAndJacobians (SPCS:1818-1939): rows written to scratch, returns R */
 template <int RT>
 __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* Tc, const double* cfg) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const int ln = s.lane;
+    const int D = R.D;
     const ScratchLayout& SL = A.SL;
     FKS_GLOBAL double* J = gpw(s.scratch) + SL.J;
     FKS_GLOBAL double* bv = gpw(s.scratch) + SL.b;
     const FKS_GLOBAL double* corr = gp(s.scratch) + SL.corr;
     const FKS_GLOBAL double* flag = gp(s.scratch) + SL.flag;
+    const uint32_t rc = A.row_cap;
     joint_frames<RT>(s, Tc);
     const double* axw = s.lds + s.A->L.axis_w;
     const double* orw = s.lds + s.A->L.orig_w;
@@ -2126,23 +1727,6 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
     /* rounds that provably hold no corrected point: their EstimateDistance reads are
      * counted (28 B per point, in bounds) but not made */
     const uint64_t skip = skippable_rounds(s, Tc, kSkipCorrections);
-    if (FKS_COOP_CORR && A.coop && R.nrounds <= kWave) {
-        /* idle sibling waves take a share of the rounds (cooperative point rounds) */
-        const uint64_t all = (R.nrounds == kWave) ? ~0ull : ((1ull << R.nrounds) - 1ull);
-        const uint64_t work = s.self_nonempty ? all : (~skip & all);
-        if (__popcll(work) >= kCoopMinCorrRounds) {
-            if (__popc(coop_helpers(s)) >= kCoopMinHelpers) {
-                const CoopCorrResult r = coop_corr_lead(A.self, s.shared, s.lds, ln, Tp, Tc, cfg, skip, s.self_nonempty);
-                if (r.rows != kCoopDeclined) {
-                    if (ln == 0) {
-                        s.lane_bytes += r.bytes;
-                        s.err |= r.err;
-                    }
-                    return r.rows;
-                }
-            }
-        }
-    }
     for (int base = 0; base < R.P; base += kWave) {
         const int i = base + ln;
         const int r = base / kWave;
@@ -2152,10 +1736,38 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
             if (i < R.P) s.lane_bytes += 28;
             continue;
         }
-        D3 pcorr;
-        D4 xc;
-        int link;
-        const bool has = point_correction(A, Tp, Tc, corr, flag, s.self_nonempty, skr, i, &s.lane_bytes, &s.err, &pcorr, &xc, &link);
+        bool has = false;
+        D3 pcorr{0.0, 0.0, 0.0};
+        D4 xc{0.0, 0.0, 0.0, 0.0};
+        int link = 0;
+        if (i < R.P) {
+            const D4 p = load_point(R, i);
+            link = gp(R.point_link)[i];
+            xc = xform4(Tc + 12 * link, p);
+            const bool has_self = s.self_nonempty && flag[i] != 0.0;
+            bool inb = false;
+            double est = 0.0;
+            if (skr)
+                s.lane_bytes += 28;
+            else
+                est = estimate_distance(A, xc, &inb, &s.lane_bytes);
+            const bool has_env = (est < 0.0) && inb;
+            D3 ecorr{0.0, 0.0, 0.0};
+            if (has_env) {
+                const D4 xp = xform4(Tp + 12 * link, p);
+                const D4 motion{xc.x - xp.x, xc.y - xp.y, xc.z - xp.z, xc.w - xp.w};
+                const D4 nm = safe_normal4(motion);
+                D3 raw;
+                const bool ok = lookup_normal(A, xc, nm, &raw, &s.err, &s.lane_bytes);
+                if (!ok) s.err |= FKS_PARTICLE_ERR_NORMAL_OOB;
+                const D3 g = safe_normal3(raw);
+                const double pen = dabs(0.0 - est);
+                ecorr = D3{g.x * pen, g.y * pen, g.z * pen};
+            }
+            has = has_self || has_env;
+            if (has_self) pcorr = D3{pcorr.x + corr[3 * i], pcorr.y + corr[3 * i + 1], pcorr.z + corr[3 * i + 2]};
+            if (has_env) pcorr = D3{pcorr.x + ecorr.x, pcorr.y + ecorr.y, pcorr.z + ecorr.z};
+        }
         const uint64_t m = __ballot(has);
         if (s.self_nonempty) {
             const uint64_t k = (uint64_t)__popcll(__ballot(has && flag[i] != 0.0));
@@ -2163,137 +1775,56 @@ __device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* 
         }
         if (has) {
             const uint32_t row = (rows + (uint32_t)__popcll(m & ((1ull << ln) - 1ull))) * 3u;
-            write_point_rows<RT>(A, s.joints, s.dofj, axw, orw, cfg, J, bv, row, pcorr, xc, link);
+            bv[row + 0] = pcorr.x;
+            bv[row + 1] = pcorr.y;
+            bv[row + 2] = pcorr.z;
+            if constexpr (RT == FKS_ROBOT_LINKED) {
+                const uint64_t mask = gp(R.link_dof_mask)[link];
+                for (int d = 0; d < D; ++d) {
+                    D3 col{0.0, 0.0, 0.0};
+                    if ((mask >> d) & 1ull) {
+                        const D3 aw{axw[3 * d], axw[3 * d + 1], axw[3 * d + 2]};
+                        const int jt = s.joints[s.dofj[d]].type;
+                        if (jt == FKS_JOINT_PRISMATIC) {
+                            col = aw;
+                        } else {
+                            col = cross(aw, D3{xc.x - orw[3 * d], xc.y - orw[3 * d + 1], xc.z - orw[3 * d + 2]});
+                        }
+                        col = D3{0.0 + col.x, 0.0 + col.y, 0.0 + col.z};
+                    }
+                    J[(uint64_t)d * rc + row + 0] = col.x;
+                    J[(uint64_t)d * rc + row + 1] = col.y;
+                    J[(uint64_t)d * rc + row + 2] = col.z;
+                }
+            } else if constexpr (RT == FKS_ROBOT_SE2) {
+                J[0 * rc + row + 0] = 0.0 + 1.0;
+                J[0 * rc + row + 1] = 0.0;
+                J[0 * rc + row + 2] = 0.0;
+                J[1 * rc + row + 0] = 0.0;
+                J[1 * rc + row + 1] = 0.0 + 1.0;
+                J[1 * rc + row + 2] = 0.0;
+                const D3 c2 = cross(D3{0.0, 0.0, 1.0}, D3{xc.x - cfg[0], xc.y - cfg[1], xc.z - 0.0});
+                J[2 * rc + row + 0] = 0.0 + c2.x;
+                J[2 * rc + row + 1] = 0.0 + c2.y;
+                J[2 * rc + row + 2] = 0.0 + c2.z;
+            } else {
+                const D3 d{xc.x - cfg[3], xc.y - cfg[7], xc.z - cfg[11]};
+                for (int a = 0; a < 3; ++a) {
+                    const D3 axis{cfg[a], cfg[4 + a], cfg[8 + a]};
+                    J[(uint64_t)a * rc + row + 0] = 0.0 + axis.x;
+                    J[(uint64_t)a * rc + row + 1] = 0.0 + axis.y;
+                    J[(uint64_t)a * rc + row + 2] = 0.0 + axis.z;
+                    const D3 c = cross(axis, d);
+                    J[(uint64_t)(3 + a) * rc + row + 0] = 0.0 + c.x;
+                    J[(uint64_t)(3 + a) * rc + row + 1] = 0.0 + c.y;
+                    J[(uint64_t)(3 + a) * rc + row + 2] = 0.0 + c.z;
+                }
+            }
         }
         rows += (uint32_t)__popcll(m);
     }
     wsync();
     return rows * 3u;
-}
-
-/* a participant's share of a cooperative correction pass.  Phase A: for each of its
- * rounds, every point's correction (point_correction), the round's mask of corrected
- * points into the results, the corrections and world positions of those points into the
- * leader's staging area.  After all participants have finished phase A, phase B: a
- * round's first row is 3 x the corrected points of the rounds before it (point order, as
- * the single-wave pass compacts them), and each corrected point's rows are written from
- * its staged values.  Its bytes, error bits and self-corrected count go to its slot. */
-template <int RT>
-__device__ __forceinline__ void coop_corr_work(const SimArgs& A, double* shared, double* lead, double* lscratch, int ln, const double* Tp,
-                                               const double* Tc, const double* cfg, uint64_t skip, bool self_nonempty, int rank,
-                                               int np) {
-    const RobotDev& R = A.R;
-    const ScratchLayout& SL = A.SL;
-    uint32_t* w = coop_words(A, shared);
-    double* res = shared + A.L.coop + kCoopHeader;
-    FKS_GLOBAL double* stage = gpw(lscratch) + SL.cstage;
-    const FKS_GLOBAL double* corr = gp(lscratch) + SL.corr;
-    const FKS_GLOBAL double* flag = gp(lscratch) + SL.flag;
-    const uint64_t work = self_nonempty ? coop_all_rounds(R.nrounds) : (~skip & coop_all_rounds(R.nrounds));
-    const uint64_t mine = coop_share(work, rank, np);
-    uint64_t bytes = 0;
-    uint32_t err = 0, selfk = 0;
-    for (uint64_t mm = mine; mm; mm &= mm - 1ull) {
-        const int r = __ffsll((unsigned long long)mm) - 1;
-        const int i = kWave * r + ln;
-        const bool skr = (skip >> r) & 1ull;
-        D3 pc;
-        D4 xc;
-        int link;
-        const bool has = point_correction(A, Tp, Tc, corr, flag, self_nonempty, skr, i, &bytes, &err, &pc, &xc, &link);
-        const uint64_t m = __ballot(has);
-        if (self_nonempty) selfk += (uint32_t)__popcll(__ballot(has && flag[i] != 0.0));
-        if (ln == 0) reinterpret_cast<uint64_t*>(res + kCoopRound * r)[0] = m;
-        if (has) {
-            FKS_GLOBAL double* st = stage + 6ull * (uint64_t)i;
-            st[0] = pc.x;
-            st[1] = pc.y;
-            st[2] = pc.z;
-            st[3] = xc.x;
-            st[4] = xc.y;
-            st[5] = xc.z;
-        }
-    }
-    wsync();
-    if (ln == 0) __hip_atomic_fetch_add(w + kCoopDoneA, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    coop_wait(w + kCoopDoneA, (uint32_t)np);
-    uint64_t cnt = 0;
-    if (ln < R.nrounds && ((work >> ln) & 1ull)) cnt = (uint64_t)__popcll(reinterpret_cast<const uint64_t*>(res + kCoopRound * ln)[0]);
-    FKS_GLOBAL double* J = gpw(lscratch) + SL.J;
-    FKS_GLOBAL double* bv = gpw(lscratch) + SL.b;
-    const JointDev* joints = reinterpret_cast<const JointDev*>(shared + A.L.joints);
-    const int32_t* dofj = reinterpret_cast<const int32_t*>(shared + A.L.dofj);
-    for (uint64_t mm = mine; mm; mm &= mm - 1ull) {
-        const int r = __ffsll((unsigned long long)mm) - 1;
-        const uint64_t m = reinterpret_cast<const uint64_t*>(res + kCoopRound * r)[0];
-        const uint32_t base = (uint32_t)wave_sum_u64(ln < r ? cnt : 0ull);
-        if (m == 0ull) continue;
-        if ((m >> ln) & 1ull) {
-            const int i = kWave * r + ln;
-            const FKS_GLOBAL double* st = stage + 6ull * (uint64_t)i;
-            const D3 pc{st[0], st[1], st[2]};
-            const D4 xc{st[3], st[4], st[5], 1.0};
-            const uint32_t row = (base + (uint32_t)__popcll(m & ((1ull << ln) - 1ull))) * 3u;
-            write_point_rows<RT>(A, joints, dofj, lead + A.L.axis_w, lead + A.L.orig_w, cfg, J, bv, row, pc, xc,
-                                 (int)gp(R.point_link)[i]);
-        }
-    }
-    const uint64_t tb = wave_sum_u64(bytes);
-    err = wave_or(err);
-    if (ln == 0) {
-        uint32_t* slot = w + kCoopPart + 4 * rank;
-        slot[0] = err;
-        slot[1] = selfk;
-        *reinterpret_cast<uint64_t*>(slot + 2) = tb;
-    }
-    wsync();
-}
-
-/* a helper's life: serve tasks until every wave of the workgroup is idle.  Out of line,
- * and it writes only through its pointer arguments (the workgroup's LDS and scratch):
- * a callee that writes through a pointer it loaded would count as a possible write to
- * the argument block, and the kernel's argument reads would turn from scalar into vector
- * loads */
-template <int RT>
-__device__ __noinline__ void coop_serve(const SimArgs* __restrict__ Ap, double* shared, double* wg_scratch, uint32_t wave) {
-    const SimArgs& A = *Ap;
-    const int ln = lane_id();
-    uint32_t* w = coop_words(A, shared);
-    const uint32_t full = (1u << (blockDim.x >> 6)) - 1u;
-    uint32_t seen = lds_acquire(w + kCoopWord);
-    if (ln == 0) __hip_atomic_fetch_or(w + kCoopIdle, 1u << wave, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    for (;;) {
-        const uint32_t word = lds_acquire(w + kCoopWord);
-        if (word != seen) {
-            seen = word;
-            const uint32_t mask = word & 0xffu;
-            if ((mask >> wave) & 1u) {
-                __builtin_amdgcn_s_setprio(2);
-                const int np = __popc(mask), rank = __popc(mask & ((1u << wave) - 1u));
-                const uint32_t leader = (uint32_t)__builtin_amdgcn_readfirstlane((int)w[kCoopLeader]);
-                const uint32_t kind = (uint32_t)__builtin_amdgcn_readfirstlane((int)w[kCoopKind]);
-                const uint64_t skip = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)w[kCoopSkipLo]) |
-                                      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)w[kCoopSkipHi]) << 32);
-                double* lead = shared + A.L.shared_total + (uint64_t)leader * A.L.total;
-                const double* Tc = shared + (uint32_t)__builtin_amdgcn_readfirstlane((int)w[kCoopTc]);
-                if (kind == kCoopTaskEnv) {
-                    coop_env_work(A, shared, lead, ln, Tc, skip, rank, np);
-                } else {
-                    const double* Tp = shared + (uint32_t)__builtin_amdgcn_readfirstlane((int)w[kCoopTp]);
-                    const double* cfg = shared + (uint32_t)__builtin_amdgcn_readfirstlane((int)w[kCoopCfg]);
-                    const bool self_nonempty = (__builtin_amdgcn_readfirstlane((int)w[kCoopFlags]) & 1) != 0;
-                    double* lscratch = wg_scratch + (uint64_t)leader * A.scratch_per_wave;
-                    coop_corr_work<RT>(A, shared, lead, lscratch, ln, Tp, Tc, cfg, skip, self_nonempty, rank, np);
-                }
-                wsync();
-                if (ln == 0) __hip_atomic_fetch_add(w + kCoopDone, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __builtin_amdgcn_s_setprio(0);
-                continue;
-            }
-        }
-        if (lds_acquire(w + kCoopIdle) == full) break;
-        __builtin_amdgcn_s_sleep(2);
-    }
 }
 
 /* value of column `k` (wave-uniform, runtime) of this lane's register row */
@@ -3446,7 +2977,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             shared[A.L.rounds + 2 * t] = (double)rd.link;
             shared[A.L.rounds + 2 * t + 1] = rd.radius;
         }
-        if (t < 2 * (int)kCoopHeader) reinterpret_cast<uint32_t*>(shared + A.L.coop)[t] = 0u; /* cooperative rounds: nobody idle */
         __syncthreads(); /* the only workgroup barrier: waves run independently afterwards */
     }
     Sim s;
@@ -3464,10 +2994,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     s.base = shared + A.L.base;
     /* skip-proof cache of the first 64 rounds (the skip masks are 64-bit; later rounds are always read) */
     if (s.lane < R.nrounds) s.lds[A.L.rstate + kRoundState * s.lane + 12] = kInvalidRound;
-    if (s.lane == 0) {
-        coop_self(A, s.lds) = (uint32_t)wave;
-        coop_tasks(A, s.lds) = 0;
-    }
     wsync();
     const int ln = s.lane;
     const int W = R.W, D = R.D;
@@ -3479,10 +3005,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     const uint64_t t_resident = __builtin_amdgcn_s_memrealtime();
     const uint32_t nseg = A.nseg;
     uint64_t carry = kNoTicket; /* the next segment of the particle just run, claimed by this wave */
-    /* a batch no larger than the grid, run whole (A.spread): wave w of workgroup b takes
-     * particle w * grid + b, so the particles spread over the workgroups and the waves left
-     * without one serve their siblings' point rounds from the start */
-    bool spread_first = A.spread != 0;
     bool carry_heavy = false;   /* ... and whether the segment just run was contact-heavy */
     /* call counters are summed per wave and flushed once when the queue is drained
      * (per-segment device atomics on a handful of shared addresses would serialise) */
@@ -3508,14 +3030,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
              * longest particles finish sooner, the batch's tail shrinks */
             prio = carry_heavy ? 2u : (A.seg_heavy_prio > 1u ? 1u : 0u);
         } else {
-            if (A.spread) {
-                /* one particle per wave at most, no queue */
-                if (ln == 0) {
-                    *next_particle = spread_first ? (uint64_t)wave * gridDim.x + blockIdx.x : A.n;
-                    *seg_seen = 1u;
-                }
-                spread_first = false;
-            } else if (ln == 0) {
+            if (ln == 0) {
                 const uint64_t t = __hip_atomic_fetch_add(A.queue, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint64_t sg = (A.n > 0) ? t / A.n : (uint64_t)nseg;
                 uint32_t run = 1;
@@ -3553,8 +3068,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                     if (sc[1]) atomicAdd(A.counters + kCntSelfPoints, (unsigned long long)sc[1]);
                     for (int k = 0; k < FKS_NUM_PHASES; ++k)
                         if (s.phase[k]) atomicAdd(A.counters + kPhaseBase + k, (unsigned long long)s.phase[k]);
-                    const uint64_t ct = coop_tasks(A, s.lds);
-                    if (ct) atomicAdd(A.counters + kCoopTasks, (unsigned long long)ct);
                 }
                 break;
             }
@@ -3753,15 +3266,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             }
         }
         wsync();
-    }
-    /* the queue is drained: stay as a helper of the siblings still running particles (after
-     * the loop, so the call cannot count as a write between the loop's argument reads) */
-    if (FKS_COOP_SERVE && A.coop) {
-        /* opaque, so the optimiser does not fold the argument back into a load of A.scratch
-         * inside the callee */
-        double* wg_scratch = A.scratch + (uint64_t)blockIdx.x * (blockDim.x >> 6) * A.scratch_per_wave;
-        asm volatile("" : "+v"(wg_scratch));
-        coop_serve<RT>(A.self, shared, wg_scratch, (uint32_t)wave);
     }
 }
 

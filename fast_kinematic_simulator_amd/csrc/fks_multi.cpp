@@ -219,7 +219,6 @@ fks_status fks_multi_forward_simulate(fks_multi_context* m, const double* starts
         m->last.least_squares_rows += c.least_squares_rows;
         m->last.self_collision_checks += c.self_collision_checks;
         m->last.self_corrected_points += c.self_corrected_points;
-        m->last.cooperative_tasks += c.cooperative_tasks;
         m->last.kernel_ms = std::max(m->last.kernel_ms, c.kernel_ms);
     }
     m->last.calls = 1;

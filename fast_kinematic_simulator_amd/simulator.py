@@ -164,12 +164,6 @@ class HipParticleContactSimulator:
         _capi.check(self._lib.fks_set_individual_jacobians(self._ctx, 1 if simulate_with_individual_jacobians else 0), self._ctx,
                     "individual jacobians")
 
-    def set_cooperative(self, enable: bool):
-        """Cooperative point rounds (fks_set_cooperative, on by default): waves left without
-        a particle evaluate a share of the point rounds of their workgroup's busy waves.
-        Results do not depend on it."""
-        _capi.check(self._lib.fks_set_cooperative(self._ctx, 1 if enable else 0), self._ctx, "cooperative")
-
     def launch_geometry(self) -> dict:
         """Resident waves of the persistent simulation grid and LDS bytes per workgroup
         (fks_get_launch_geometry) for the robot set last."""

@@ -44,9 +44,8 @@ extern "C" {
 #endif
 
 /* 5: the opt-in joint-space proof (ABI 4: fks_set_joint_proof, fks_call_counters.
- * proven_free_microsteps) removed: it broke even on the headline.
- * 6: fks_set_cooperative (idle waves of a workgroup serve a sibling's point rounds) */
-#define FKS_ABI_VERSION 6
+ * proven_free_microsteps) removed: it broke even on the headline */
+#define FKS_ABI_VERSION 5
 
 typedef enum {
     FKS_OK = 0,
@@ -220,8 +219,7 @@ typedef struct {
                                        non-empty, i.e. ExtractSelfCollidingPoints produced corrections (SPCS:1264-1271) */
     uint64_t self_corrected_points; /* sum over resolver iterations of the points whose correction holds a
                                        self-collision term (SPCS:1846-1853, 1909-1916) */
-    uint64_t cooperative_tasks;     /* ABI 6: point-round tasks handed to idle sibling waves
-                                       (fks_set_cooperative); ABI 4's proven_free_microsteps slot */
+    uint64_t reserved0;             /* ABI 4's proven_free_microsteps (removed in ABI 5); always 0 */
 } fks_call_counters;
 
 typedef struct fks_context fks_context;
@@ -438,13 +436,6 @@ fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_
  * FKS.cpp:22,45,68 hard-wire, the default), 1 = ComputeResolverCorrectionStepIndividualJacobians
  * (SPCS:1966-1988: one ColPivHouseholderQR solve per corrected point, summed in point order). */
 fks_status fks_set_individual_jacobians(fks_context* ctx, int32_t simulate_with_individual_jacobians);
-/* Cooperative point rounds (ABI 6; no reference counterpart, results are identical either
- * way): 1 (default) = a wave left without a particle (the queue drained, or a batch smaller
- * than the grid) evaluates a share of the 64-point rounds of the environment checks and
- * correction passes of the particles its workgroup's other waves are still running, so the
- * batch's contact-heavy tail runs on up to four waves per particle; a batch no larger than
- * the grid is spread one particle per wave over the workgroups; 0 = one wave per particle. */
-fks_status fks_set_cooperative(fks_context* ctx, int32_t enable);
 
 /* sums over every call since fks_create / fks_reset_total_counters */
 fks_status fks_get_total_counters(const fks_context* ctx, fks_call_counters* out);

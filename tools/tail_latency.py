@@ -21,7 +21,7 @@ from fast_kinematic_simulator_amd import workloads as W  # noqa: E402
 from fast_kinematic_simulator_amd.simulator import make_linked_simulator  # noqa: E402
 
 
-COUNTS = ("env_rounds_skipped", "env_rounds_evaluated", "corr_rounds_skipped", "corr_rounds_evaluated", "cooperative_tasks")
+COUNTS = ("env_rounds_skipped", "env_rounds_evaluated", "corr_rounds_skipped", "corr_rounds_evaluated")
 
 
 def run(sim, wl, starts, first_id, dev):
@@ -36,7 +36,7 @@ def run(sim, wl, starts, first_id, dev):
                                 d_out_microsteps=micro.data_ptr(), d_out_resolver_iterations=res.data_ptr(), synchronize=True)
     c = sim.last_call_counters()
     ph = sim.phase_cycles(total=False)
-    return micro.cpu().numpy(), res.cpu().numpy(), c["kernel_ms"], dict(ph, cooperative_tasks=c["cooperative_tasks"])
+    return micro.cpu().numpy(), res.cpu().numpy(), c["kernel_ms"], ph
 
 
 def main():
@@ -44,14 +44,11 @@ def main():
     ap.add_argument("--workload", default="cfg3")
     ap.add_argument("--top", type=int, default=3)
     ap.add_argument("--json", default="")
-    ap.add_argument("--no-coop", action="store_true", help="fks_set_cooperative(0): one wave per particle")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     wl = W.WORKLOADS[a.workload]()
     sim = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
     sim.set_robot(wl.robot)
-    if a.no_coop:
-        sim.set_cooperative(False)
     run(sim, wl, wl.starts[:256], 0, dev)
     m, it, kms, ph = run(sim, wl, wl.starts, 0, dev)
     out = {"workload": a.workload, "batch_kernel_ms": kms, "particles": int(m.size), "alone": [],
