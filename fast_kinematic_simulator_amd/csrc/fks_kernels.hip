@@ -396,6 +396,9 @@ __device__ double sampled_pick(uint32_t k0, uint32_t k1, uint64_t particle, uint
 #ifndef FKS_QR_ATTR
 #define FKS_QR_ATTR __noinline__
 #endif
+#ifndef FKS_QR_TILE
+#define FKS_QR_TILE 1
+#endif
 #ifndef FKS_HOT_ATTR
 #define FKS_HOT_ATTR
 #endif
@@ -609,6 +612,10 @@ __device__ bool lookup_normal(const SimArgs& A, const D4& loc, const D4& dir, D3
         return true;
     }
     const double ux = dir.x / direction_norm, uy = dir.y / direction_norm, uz = dir.z / direction_norm;
+    /* the first entry is read whole (direction and normal in one round trip): nearly every
+     * surface cell has exactly one, whose normal is then the answer without a second load */
+    const FKS_GLOBAL double* e0 = gp(A.nent) + 6ull * begin;
+    const double n0 = e0[3], n1 = e0[4], n2 = e0[5];
     int64_t best = -1;
     double best_dot = -__builtin_huge_val();
     for (uint32_t e = begin; e < end; ++e) {
@@ -624,8 +631,12 @@ __device__ bool lookup_normal(const SimArgs& A, const D4& loc, const D4& dir, D3
         *err |= FKS_PARTICLE_ERR_ZERO_DIRECTION;
         return true;
     }
-    const FKS_GLOBAL double* ent = gp(A.nent) + 6ull * (uint64_t)best;
-    *out = D3{ent[3], ent[4], ent[5]};
+    if (best == (int64_t)begin) {
+        *out = D3{n0, n1, n2};
+    } else {
+        const FKS_GLOBAL double* ent = gp(A.nent) + 6ull * (uint64_t)best;
+        *out = D3{ent[3], ent[4], ent[5]};
+    }
     return true;
 }
 
@@ -2047,6 +2058,227 @@ __device__ __forceinline__ int wave_first_argmax(double val, int ln, int first, 
     return __ffsll((unsigned long long)__ballot(part && val == m)) - 1;
 }
 
+/* ---------------- ColPivHouseholderQR on a lane tile ----------------
+ * Small stacked systems (<= 16 rows; the right-hand side as column D) with one element per
+ * lane: CW = 8 columns (D <= 7: every linked arm of <= 7 dofs, SE(2), SE(3)) of RB = 8 rows,
+ * or CW = 16 columns (D <= 15) of RB = 4 rows; lane RB*c + r holds row RB*q + r of column c
+ * in register q (NQ register blocks).  A reduction over the rows of a column is then two or
+ * three in-register DPP steps inside the column's RB lanes plus a tree over the NQ blocks,
+ * which together are exactly the canonical tree of lane_tree_sum (xor 1: rows (0,1), (2,3)
+ * ...; xor 2: pairs of pairs; row_half_mirror: halves of 8), so the arithmetic is that of
+ * qr_solve_cols bit for bit; an update of every column is one instruction per block instead
+ * of one per row, and a Householder step costs about a third of the column-per-lane one. */
+template <int RB>
+__device__ __forceinline__ double col_tree(double v) {
+    v = v + dpp_f64<kDppXor1>(v);
+    v = v + dpp_f64<kDppXor2>(v);
+    if constexpr (RB == 8) v = v + dpp_f64<kDppHalfMirror>(v);
+    return v;
+}
+/* lane_tree_sum<RB * NQ> over the rows of the lane's column (in every lane of the column) */
+template <int RB, int NQ>
+__device__ __forceinline__ double col_sum(const double (&p)[NQ]) {
+    static_assert(NQ == 1 || NQ == 2 || NQ == 4, "1, 2 or 4 row blocks");
+    if constexpr (NQ == 1) {
+        return col_tree<RB>(p[0]) + 0.0;
+    } else if constexpr (NQ == 2) {
+        return (col_tree<RB>(p[0]) + col_tree<RB>(p[1])) + 0.0;
+    } else {
+        return ((col_tree<RB>(p[0]) + col_tree<RB>(p[1])) + (col_tree<RB>(p[2]) + col_tree<RB>(p[3]))) + 0.0;
+    }
+}
+__device__ __forceinline__ double shfl_f64(double v, int src) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)b, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(b >> 32), src, 64);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+template <int CW, int NQ>
+__device__ __forceinline__ void qr_solve_tile(const FKS_GLOBAL double* Jm, const FKS_GLOBAL double* bv, int32_t* perm, int D, uint32_t rc,
+                                              int ln, uint32_t Rn, double* x) {
+    constexpr int RB = kWave / CW; /* rows per register block */
+    constexpr int RM = RB * NQ;    /* rows held */
+    int32_t* transp = perm + kMaxDofs;
+    const int c = ln / RB, r = ln % RB;
+    const bool isc = c < D, isb = c == D;
+    double a[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const uint32_t row = (uint32_t)(RB * q + r);
+        a[q] = (row < Rn) ? (isc ? Jm[(uint64_t)c * rc + row] : (isb ? bv[row] : 0.0)) : 0.0;
+    }
+    if (ln < D) x[ln] = 0.0;
+    if (D == 0) {
+        wsync();
+        return;
+    }
+    /* squared column norms (every lane of column c holds column c's) */
+    double cs;
+    {
+        double p[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) p[q] = ((uint32_t)(RB * q + r) < Rn) ? 0.0 + a[q] * a[q] : 0.0;
+        cs = col_sum<RB, NQ>(p);
+    }
+    /* maxsq = colsq[0]; for k: if (colsq[k] > maxsq) maxsq = colsq[k] (sums of squares have no
+     * -0, so the maximum of the non-NaN values does not depend on the order it is taken in) */
+    double maxsq;
+    {
+        const double c0 = readlane_f64(cs, 0);
+        double m = -__builtin_huge_val();
+        for (int cc = 1; cc < D; ++cc) {
+            const double v = readlane_f64(cs, RB * cc);
+            if (!__builtin_isnan(v) && v > m) m = v;
+        }
+        maxsq = (__builtin_isnan(c0) || !(m > c0)) ? c0 : m;
+    }
+    const double eps = 2.220446049250313e-16;
+    const double threshold_helper = maxsq * (eps * eps) / (double)Rn;
+    const int size = ((int)Rn < D) ? (int)Rn : D;
+    int nz = size;
+#pragma unroll
+    for (int k = 0; k < RM; ++k) {
+        if (k >= size) break;
+        const int kq = k / RB, kr = k % RB;
+        /* wave_first_argmax over columns k..D-1: the first column holding the maximum of the
+         * non-NaN norms right of k, or k if its own is NaN or already the maximum */
+        int biggest = k;
+        {
+            const double vf = readlane_f64(cs, RB * k);
+            double m = -__builtin_huge_val();
+            int at = k;
+            for (int cc = k + 1; cc < D; ++cc) {
+                const double v = readlane_f64(cs, RB * cc);
+                if (!__builtin_isnan(v) && v > m) {
+                    m = v;
+                    at = cc;
+                }
+            }
+            if (!(__builtin_isnan(vf) || !(m > vf))) biggest = at;
+        }
+        double bsq;
+        {
+            double p[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int row = RB * q + r;
+                p[q] = ((uint32_t)row < Rn && row >= k) ? 0.0 + a[q] * a[q] : 0.0;
+            }
+            bsq = readlane_f64(col_sum<RB, NQ>(p), RB * biggest);
+        }
+        if (nz == size && bsq < threshold_helper * (double)(Rn - (uint32_t)k)) nz = k;
+        if (ln == 0) transp[k] = biggest;
+        if (c == biggest) cs = bsq;
+        if (k != biggest) {
+            /* columns k and biggest trade places (with their squared norms) */
+            const int src = RB * ((c == k) ? biggest : ((c == biggest) ? k : c)) + r;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) a[q] = shfl_f64(a[q], src);
+            cs = shfl_f64(cs, src);
+        }
+        /* Householder vector of column k */
+        const double c0 = readlane_f64(a[kq], RB * k + kr);
+        double tail = 0.0;
+        if (Rn - (uint32_t)k != 1u) {
+            double p[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int row = RB * q + r;
+                p[q] = ((uint32_t)row < Rn && row > k) ? 0.0 + a[q] * a[q] : 0.0;
+            }
+            tail = readlane_f64(col_sum<RB, NQ>(p), RB * k);
+        }
+        double tau, beta;
+        if (tail <= 2.2250738585072014e-308) {
+            tau = 0.0;
+            beta = c0;
+            if (c == k) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q)
+                    if (RB * q + r > k) a[q] = 0.0;
+            }
+        } else {
+            beta = dsqrt(c0 * c0 + tail);
+            if (c0 >= 0.0) beta = -beta;
+            const double denom = c0 - beta;
+            if (c == k) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q)
+                    if (RB * q + r > k && (uint32_t)(RB * q + r) < Rn) a[q] = a[q] / denom;
+            }
+            tau = (beta - c0) / beta;
+        }
+        if (c == k && r == kr) a[kq] = beta;
+        /* the reflector (rows k+1..Rn-1 of column k), along every row */
+        double v[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int row = RB * q + r;
+            const double vk = shfl_f64(a[q], RB * k + r);
+            v[q] = (row > k && (uint32_t)row < Rn) ? vk : 0.0;
+        }
+        /* apply H_k to the columns right of k (and, while the rank holds, to the rhs) */
+        const bool upd = (isc && c > k) || (isb && k < nz);
+        double akk = shfl_f64(a[kq], RB * c + kr); /* row k of the lane's column */
+        if (Rn - (uint32_t)k == 1u) {
+            akk = akk * (1.0 - tau);
+        } else if (tau != 0.0) {
+            double p[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int row = RB * q + r;
+                p[q] = (row > k && (uint32_t)row < Rn) ? 0.0 + v[q] * a[q] : 0.0;
+            }
+            const double t = col_sum<RB, NQ>(p) + akk;
+            akk = akk - tau * t;
+            if (upd) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const int row = RB * q + r;
+                    if (row > k && (uint32_t)row < Rn) a[q] = a[q] - (tau * v[q]) * t;
+                }
+            }
+        }
+        if (upd) {
+            if (r == kr) a[kq] = akk;
+            /* colsq downdate with the updated row k */
+            if (isc) cs = cs - akk * akk;
+        }
+    }
+    if (ln == 0) {
+        for (int i = 0; i < D; ++i) perm[i] = i;
+        for (int k = 0; k < size; ++k) {
+            const int t = perm[k];
+            perm[k] = perm[transp[k]];
+            perm[transp[k]] = t;
+        }
+    }
+    wsync();
+    if (nz == 0) return;
+    /* column-oriented back substitution on the nz x nz upper triangle (uniform values) */
+    double bu[RM];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) bu[i] = ((uint32_t)i < Rn) ? readlane_f64(a[i / RB], RB * D + i % RB) : 0.0;
+#pragma unroll
+    for (int ii = RM - 1; ii >= 0; --ii) {
+        if (ii >= nz) continue;
+        const double ci = bu[ii];
+        if (ci != 0.0) {
+            const double vq = ci / readlane_f64(a[ii / RB], RB * ii + ii % RB);
+            bu[ii] = vq;
+#pragma unroll
+            for (int i = 0; i < ii; ++i) bu[i] = bu[i] - vq * readlane_f64(a[i / RB], RB * ii + i % RB);
+        }
+    }
+    double mine = 0.0;
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+        if (i == ln) mine = bu[i];
+    if (ln < nz) x[perm[ln]] = mine;
+    wsync();
+}
+
 /* ColPivHouseholderQR::solve for Rn <= RM rows with one COLUMN per lane (lane c < D
  * holds column c, lane D the right-hand side): every reduction over rows is then a
  * short in-lane tree (lane_tree_sum, the same canonical order as bfly_sum) instead
@@ -2229,6 +2461,19 @@ __device__ __forceinline__ void qr_solve_cols_body(const SimArgs* __restrict__ A
 template <int RM>
 __device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
                                            uint32_t Rn, double* x, uint32_t row0 = 0) {
+    if (FKS_QR_TILE && Ap->R.D <= 7) {
+        /* <= 7 columns: the 8 x 8 tile (qr_solve_tile), same arithmetic */
+        const FKS_GLOBAL double* Jm = gp(scratch) + Ap->SL.J + row0;
+        const FKS_GLOBAL double* bv = gp(scratch) + Ap->SL.b + row0;
+        int32_t* perm = reinterpret_cast<int32_t*>(lds + Ap->L.ints);
+        if constexpr (RM <= 8)
+            qr_solve_tile<8, 1>(Jm, bv, perm, Ap->R.D, Ap->row_cap, ln, Rn, x);
+        else
+            qr_solve_tile<8, 2>(Jm, bv, perm, Ap->R.D, Ap->row_cap, ln, Rn, x);
+        return;
+    }
+    /* (16 columns of 4-row blocks for 8-15 dofs measured 2-3 % slower on cfg5, 14 dofs, than
+     * the column-per-lane body below: profiles/r03h_ab_cfg5.log) */
     if constexpr (RM == 8) {
         if (Rn <= 4u) {
             qr_solve_cols_body<4>(Ap, lds, scratch, ln, Rn, x, row0);
@@ -2947,6 +3192,10 @@ __device__ __forceinline__ void kinematics(const SimArgs* __restrict__ args, dou
     }
 }
 
+/* diagnostic build (tools/finish_probe.py): per-particle end and first heavy-carry times */
+#ifndef FKS_FINISH_PROBE
+#define FKS_FINISH_PROBE 0
+#endif
 template <int RT, bool TR, bool IND = false>
 __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ args, double* lds_mem) {
     const SimArgs& A = *args;
@@ -3221,8 +3470,14 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         if (ln == 0) {
             if (ended) {
                 if (A.out_collided) A.out_collided[local] = collided ? 1 : 0;
+#if FKS_FINISH_PROBE
+                /* diagnostic build (tools/finish_probe.py): when the particle ended, and when it
+                 * was first carried as contact-heavy, in 100 MHz s_memrealtime ticks */
+                if (A.out_micro) A.out_micro[local] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#else
                 if (A.out_micro) A.out_micro[local] = (uint32_t)micro_total;
                 if (A.out_resolver) A.out_resolver[local] = (uint32_t)resolver_total;
+#endif
                 if (A.out_err) A.out_err[local] = s.err;
                 if constexpr (TR) {
                     A.tr_nsteps[local] = s.tr_steps;
@@ -3263,6 +3518,13 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             if (cont) {
                 carry = (seg + 1) * A.n + local;
                 carry_heavy = cont == 2u;
+#if FKS_FINISH_PROBE
+                if (carry_heavy && ln == 0 && A.out_resolver) {
+                    uint32_t z = 0;
+                    __hip_atomic_compare_exchange_strong(A.out_resolver + local, &z, (uint32_t)__builtin_amdgcn_s_memrealtime(),
+                                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+#endif
             }
         }
         wsync();
