@@ -158,7 +158,10 @@ def load_traffic():
     try:
         with open(path) as f:
             d = json.load(f)
-        return float(d["hbm_bytes_per_launch"]), d.get("l2_hit_rate"), d.get("source", "profiles/latest_pmc.json")
+        src = d.get("source", "profiles/latest_pmc.json")
+        if d.get("note"):
+            src = src + "; " + d["note"]
+        return float(d["hbm_bytes_per_launch"]), d.get("l2_hit_rate"), src
     except Exception:
         return None, None, None
 
