@@ -35,6 +35,9 @@ extern "C" __global__ void fks_simulate_se3_indiv(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_traced(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se2_traced(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se3_traced(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_linked_lean(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_linked_lean_indiv(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_linked_lean_traced(const fksd::SimArgs* args);
 extern "C" __global__ void fks_check_configs_linked(const fksd::SimArgs* args);
 extern "C" __global__ void fks_check_configs_se2(const fksd::SimArgs* args);
 extern "C" __global__ void fks_check_configs_se3(const fksd::SimArgs* args);
@@ -57,19 +60,22 @@ sim_kernel_t check_kernel_for(int robot_type) {
 }
 
 /* the simulation kernel compiled for one robot family (FKS.cpp:4-71 factories) */
-sim_kernel_t traced_kernel_for(int robot_type) {
+/* lean: the robot runs a lean LDS block (linked robots only, fks_set_robot) */
+sim_kernel_t traced_kernel_for(int robot_type, bool lean = false) {
     switch (robot_type) {
         case FKS_ROBOT_SE2: return fks_simulate_se2_traced;
         case FKS_ROBOT_SE3: return fks_simulate_se3_traced;
-        default: return fks_simulate_linked_traced;
+        default: return lean ? fks_simulate_linked_lean_traced : fks_simulate_linked_traced;
     }
 }
 
-sim_kernel_t kernel_for(int robot_type, bool individual_jacobians = false) {
+sim_kernel_t kernel_for(int robot_type, bool individual_jacobians = false, bool lean = false) {
     switch (robot_type) {
         case FKS_ROBOT_SE2: return individual_jacobians ? fks_simulate_se2_indiv : fks_simulate_se2;
         case FKS_ROBOT_SE3: return individual_jacobians ? fks_simulate_se3_indiv : fks_simulate_se3;
-        default: return individual_jacobians ? fks_simulate_linked_indiv : fks_simulate_linked;
+        default:
+            if (lean) return individual_jacobians ? fks_simulate_linked_lean_indiv : fks_simulate_linked_lean;
+            return individual_jacobians ? fks_simulate_linked_indiv : fks_simulate_linked;
     }
 }
 
@@ -253,6 +259,7 @@ struct fks_context {
     uint32_t heavy_priority = 1;
     int32_t individual_jacobians = 0; /* fks_set_individual_jacobians (SPCS:420-423) */
     bool fk_pair = false;             /* paired FK of free microsteps (fks_set_robot) */
+    bool lean = false;                /* lean LDS block + lean kernels (fks_set_robot) */
     double* d_seg_state = nullptr;
     uint32_t* d_seg_done = nullptr;
     size_t cap_seg_state = 0, cap_seg_done = 0;
@@ -498,8 +505,10 @@ int32_t fks_config_width(const fks_context* ctx) { return (ctx && ctx->has_robot
  * workspace.  Computed into locals and committed to ctx only when all of it succeeds. */
 static fks_status launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
     const int P = R.P, G = R.G;
-    auto blocks = [&](const fksd::LdsLayout& l, uint32_t* wpg, size_t* bytes) -> int {
-        uint32_t w = fksd::kWavesPerGroup;
+    /* resident waves per CU of a layout at the largest workgroup (<= wmax waves) whose
+     * blocks fit the CU's 160 KiB */
+    auto blocks = [&](const fksd::LdsLayout& l, uint32_t wmax, uint32_t* wpg, size_t* bytes) -> int {
+        uint32_t w = wmax;
         size_t b = 0;
         for (;;) {
             b = ((size_t)l.shared_total + (size_t)w * l.total) * sizeof(double);
@@ -510,22 +519,40 @@ static fks_status launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
         *bytes = b;
         if (b > 160 * 1024) return 0;
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kernel_for(R.type)), 64 * (int)w, b) !=
-            hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kernel_for(R.type, false, l.lean != 0)),
+                                                         64 * (int)w, b) != hipSuccess)
             return 0;
         return n * (int)w; /* resident waves per CU */
     };
     uint32_t wpg = 0;
     size_t bytes = 0;
     const bool linked_pairable = R.type == FKS_ROBOT_LINKED && R.J >= 1 && R.J <= 32;
-    const int w0 = blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds), &wpg, &bytes);
+    const int w0 = blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds), fksd::kWavesPerGroup, &wpg, &bytes);
     bool pair = false;
     if (linked_pairable && w0 > 0) {
         uint32_t w = 0;
         size_t b = 0;
-        pair = blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, true), &w, &b) >= w0;
+        pair = blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, true), fksd::kWavesPerGroup, &w, &b) >= w0;
     }
-    const int waves_per_cu = blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, pair), &wpg, &bytes);
+    int waves_per_cu = blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, pair), fksd::kWavesPerGroup, &wpg, &bytes);
+    /* a linked robot whose LDS block caps the resident waves below the register limit may run
+     * lean blocks (the skip-proof cache in scratch) in workgroups of up to 8 waves, if that
+     * keeps more waves resident (cfg5's 14-dof arm: 12 -> 16 per CU) */
+    bool lean = false;
+    if (R.type == FKS_ROBOT_LINKED) {
+        for (uint32_t wmax : {(uint32_t)fksd::kMaxWavesPerGroup, (uint32_t)fksd::kWavesPerGroup}) {
+            uint32_t w = 0;
+            size_t b = 0;
+            const int n = blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, false, true), wmax, &w, &b);
+            if (n > waves_per_cu) {
+                waves_per_cu = n;
+                wpg = w;
+                bytes = b;
+                lean = true;
+                pair = false;
+            }
+        }
+    }
     if (waves_per_cu < 1)
         return fail(ctx, FKS_ERR_UNSUPPORTED,
                     "robot too large: one wave's LDS block (" + std::to_string(bytes) + " bytes) does not fit a CU");
@@ -551,6 +578,7 @@ static fks_status launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
         ctx->cap_scratch = words;
     }
     ctx->fk_pair = pair;
+    ctx->lean = lean;
     ctx->waves_per_group = wpg;
     ctx->lds_bytes = bytes;
     ctx->grid_groups = grid_groups;
@@ -988,7 +1016,7 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair, ctx->lean);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     /* controller-step segments: automatically only when the batch outnumbers the
      * resident waves (otherwise every particle has a wave from the start), always
@@ -1040,7 +1068,7 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? (groups_needed > 0 ? groups_needed : 1)
                                                                                   : ctx->grid_groups);
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
-    hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type) : kernel_for(ctx->R.type, ctx->individual_jacobians != 0),
+    hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type, ctx->lean) : kernel_for(ctx->R.type, ctx->individual_jacobians != 0, ctx->lean),
                        dim3(grid),
                        dim3(64 * ctx->waves_per_group), ctx->lds_bytes, s, static_cast<const fksd::SimArgs*>(ctx->d_args));
     HIP_TRY(ctx, hipGetLastError());
@@ -1105,7 +1133,7 @@ fks_status fks_check_config_collision_device(fks_context* ctx, const double* d_c
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair, ctx->lean);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     *ctx->h_args = a;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_args, ctx->h_args, sizeof(a), hipMemcpyHostToDevice, s));
@@ -1388,7 +1416,7 @@ fks_status fks_kinematics(fks_context* ctx, int32_t mode, const double* configs,
     a.scratch = ctx->d_scratch;
     a.scratch_per_wave = ctx->scratch_per_wave;
     a.row_cap = 3u * (uint32_t)ctx->R.P;
-    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair);
+    a.L = fksd::make_lds_layout(ctx->R.L, ctx->R.J, ctx->R.D, ctx->R.W, ctx->R.G, ctx->R.nrounds, ctx->fk_pair, ctx->lean);
     a.SL = fksd::make_scratch_layout(a.row_cap, ctx->R.D, ctx->R.P, ctx->R.G);
     a.kin_mode = mode;
     a.kin_out = d_out;

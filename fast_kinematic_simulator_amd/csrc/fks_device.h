@@ -123,18 +123,22 @@ struct RobotDev {
  * `shared_total` doubles); every other offset is relative to the wave's own block of
  * `total` doubles that follows. */
 constexpr int kWavesPerGroup = 4;
+/* an LDS-bound robot may run a lean block (its round skip-proof cache in the wave's scratch,
+ * fks_simulate_*_lean kernels) at up to 8 waves per workgroup */
+constexpr int kMaxWavesPerGroup = 8;
 struct LdsLayout {
     uint32_t joints, ctrl, base, dofj, gbox, gpairs, rounds, shared_total;
     uint32_t rstate, noise, noise_err, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u,
         ustep, x, real, axis_w, orig_w, colsq, hcoef, box, misc, ints, jm2, total;
     uint32_t fk_pair; /* 1: the free-motion microsteps pair their FK chains (jm2 allocated) */
+    uint32_t lean;    /* 1: no rstate here: the skip-proof cache is ScratchLayout.rstate (lean kernels) */
 };
 
 inline
 #if defined(__HIPCC__)
     __host__ __device__
 #endif
-    LdsLayout make_lds_layout(int L, int J, int D, int W, int G, int NR, bool fk_pair = false) {
+    LdsLayout make_lds_layout(int L, int J, int D, int W, int G, int NR, bool fk_pair = false, bool lean = false) {
     LdsLayout l;
     uint32_t o = 0;
     /* shared: the robot tables the hot loops read (filled once per workgroup) */
@@ -156,8 +160,11 @@ inline
     l.shared_total = o;
     /* per wave */
     o = 0;
-    l.rstate = o; /* kRoundState per round r < 64 (the 64-bit skip masks), persists across the wave's particles */
-    o += (uint32_t)kRoundState * (uint32_t)(NR < 1 ? 1 : (NR > 64 ? 64 : NR));
+    /* kRoundState per round r < 64 (the 64-bit skip masks), persists across the wave's
+     * particles; a lean block keeps it in the wave's scratch instead (ScratchLayout.rstate) */
+    l.lean = lean ? 1u : 0u;
+    l.rstate = o;
+    if (!lean) o += (uint32_t)kRoundState * (uint32_t)(NR < 1 ? 1 : (NR > 64 ? 64 : NR));
     l.noise = o; /* actuator noise samples of the next floor(64/D) microsteps, [micro][dof] */
     o += 64;
     l.noise_err = o; /* their error bits, 64 x u32 */
@@ -234,7 +241,7 @@ inline
 
 /* per-wave scratch layout (doubles) */
 struct ScratchLayout {
-    uint64_t J, b, keys, corr, flag, cand, list, cellw, dense, total;
+    uint64_t J, b, keys, corr, flag, cand, list, cellw, dense, rstate, total;
 };
 inline
 #if defined(__HIPCC__)
@@ -261,6 +268,8 @@ inline
     o += 2u * kMaxGeoms + 4u * kMaxGeoms;
     l.dense = o;
     o += (G > 1) ? self_dense_words(G) : 8;
+    l.rstate = o; /* the round skip-proof cache of a lean LDS block (kRoundState per round r < 64) */
+    o += (uint64_t)kRoundState * 64u;
     l.total = (o + 7) & ~7ull;
     return l;
 }

@@ -456,6 +456,7 @@ struct Sim {
     const int32_t* dofj;             /* LDS copy of R.dof_joint */
     const double* base;              /* LDS copy of R.base */
     double pid_integral, pid_last; /* DOF lanes */
+    double* rstate;  /* the round skip-proof cache: LDS block, or scratch in the lean kernels */
     bool self_nonempty;
     bool tcur_valid; /* Tcur == FK(particle configuration) from the end of the last step */
     uint64_t local;            /* particle index within the call (traced kernels) */
@@ -1061,7 +1062,7 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
     const int ln = s.lane;
     if (ln < R.nrounds) {
         const RoundDev rd = lds_round(s, ln);
-        const double* st = s.lds + A.L.rstate + kRoundState * ln;
+        const double* st = s.rstate + kRoundState * ln;
         if (rd.link >= 0 && st[12] > kInvalidRound) {
             const double b = rigid_motion_bound(T + 12 * rd.link, st, rd.radius) * A.sdf_g.inv_res; /* cells */
             const double K = 1.7320508075688773 * b + 3.0;
@@ -1092,7 +1093,7 @@ __device__ __forceinline__ void round_update(Sim& s, int r, const double* T, dou
     const RoundDev rd = lds_round(s, r);
     if (rd.link < 0) return;
     const double smin = wave_min(S), gmin = wave_min(G), cmin = wave_min(C);
-    double* st = s.lds + A.L.rstate + kRoundState * r;
+    double* st = s.rstate + kRoundState * r;
     if (s.lane < 12) st[s.lane] = T[12 * rd.link + s.lane];
     if (s.lane == 0) {
         st[12] = smin;
@@ -2984,6 +2985,7 @@ __device__ __forceinline__ void setup_wave(const SimArgs* __restrict__ args, dou
     s.ctrl = reinterpret_cast<const fks_dof_controller*>(shared + A.L.ctrl);
     s.dofj = reinterpret_cast<const int32_t*>(shared + A.L.dofj);
     s.base = shared + A.L.base;
+    s.rstate = s.lds + A.L.rstate; /* (the check / kinematics kernels keep no skip-proof cache) */
     s.err = 0;
     s.lane_bytes = 0;
     s.self_nonempty = false;
@@ -3196,7 +3198,7 @@ __device__ __forceinline__ void kinematics(const SimArgs* __restrict__ args, dou
 #ifndef FKS_FINISH_PROBE
 #define FKS_FINISH_PROBE 0
 #endif
-template <int RT, bool TR, bool IND = false>
+template <int RT, bool TR, bool IND = false, bool LEAN = false>
 __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ args, double* lds_mem) {
     const SimArgs& A = *args;
     const RobotDev& R = A.R;
@@ -3241,8 +3243,11 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     s.ctrl = reinterpret_cast<const fks_dof_controller*>(shared + A.L.ctrl);
     s.dofj = reinterpret_cast<const int32_t*>(shared + A.L.dofj);
     s.base = shared + A.L.base;
-    /* skip-proof cache of the first 64 rounds (the skip masks are 64-bit; later rounds are always read) */
-    if (s.lane < R.nrounds) s.lds[A.L.rstate + kRoundState * s.lane + 12] = kInvalidRound;
+    /* skip-proof cache of the first 64 rounds (the skip masks are 64-bit; later rounds are always
+     * read): in the wave's LDS block, or in its scratch for a lean block (fixed per kernel, so
+     * each instantiation addresses it with one kind of load) */
+    s.rstate = LEAN ? s.scratch + A.SL.rstate : s.lds + A.L.rstate;
+    if (s.lane < R.nrounds) s.rstate[kRoundState * s.lane + 12] = kInvalidRound;
     wsync();
     const int ln = s.lane;
     const int W = R.W, D = R.D;
@@ -3385,7 +3390,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             resolver_before = load_coherent_u64(sw + 2);
             /* the particle's own skip-proof cache (the rounds' last full evaluations) */
             const int nrc = kRoundState * (R.nrounds < kWave ? R.nrounds : kWave);
-            for (int e = ln; e < nrc; e += kWave) s.lds[A.L.rstate + e] = load_coherent(st + 2 * D + 4 + e);
+            for (int e = ln; e < nrc; e += kWave) s.rstate[e] = load_coherent(st + 2 * D + 4 + e);
         }
         wsync();
         double* Tcur = s.lds + s.A->L.Tcur;
@@ -3456,7 +3461,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                 store_coherent_u64(sw + 2, resolver_total);
             }
             const int nrc = kRoundState * (R.nrounds < kWave ? R.nrounds : kWave);
-            for (int e = ln; e < nrc; e += kWave) store_coherent(st + 2 * D + 4 + e, s.lds[A.L.rstate + e]);
+            for (int e = ln; e < nrc; e += kWave) store_coherent(st + 2 * D + 4 + e, s.rstate[e]);
         }
         w_steps += s.step_count;
         w_micro += s.micro_count;
@@ -3537,7 +3542,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
 #ifndef FKS_WAVES_PER_EU
 #define FKS_WAVES_PER_EU 5
 #endif
-#define FKS_KERNEL_ATTRS __launch_bounds__(64 * kWavesPerGroup) __attribute__((amdgpu_waves_per_eu(FKS_WAVES_PER_EU)))
+#define FKS_KERNEL_ATTRS __launch_bounds__(64 * kMaxWavesPerGroup) __attribute__((amdgpu_waves_per_eu(FKS_WAVES_PER_EU)))
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
     simulate_particles<FKS_ROBOT_LINKED, false>(args, lds_mem);
@@ -3577,6 +3582,21 @@ extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se2_traced(const SimArg
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se3_traced(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
     simulate_particles<FKS_ROBOT_SE3, true>(args, lds_mem);
+}
+
+/* lean LDS blocks (LdsLayout.lean: the round skip-proof cache in the wave's scratch), chosen by
+ * fks_set_robot for linked robots whose LDS block limits the resident waves (14-dof cfg5) */
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked_lean(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_LINKED, false, false, true>(args, lds_mem);
+}
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked_lean_indiv(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_LINKED, false, true, true>(args, lds_mem);
+}
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked_lean_traced(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_LINKED, true, false, true>(args, lds_mem);
 }
 
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_check_configs_linked(const SimArgs* __restrict__ args) {

@@ -128,3 +128,26 @@ def test_mutable_robot_controller_state(fks_lib, oracle_lib, name, scale):
     plain = oracle.forward_simulate(wl.environment(), wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts, wl.targets,
                                     True, call_index=6)
     assert np.array_equal(z["positions"], plain["positions"])
+
+
+@pytest.mark.gpu
+def test_lean_block_cfg5(fks_lib, oracle_lib):
+    """cfg5's 14-dof arm is LDS-bound: fks_set_robot gives it a lean block (the round
+    skip-proof cache in the wave's scratch) in 8-wave workgroups, 16 resident waves per CU
+    instead of 12; results stay bit-identical to the oracle, segmented or whole."""
+    from fast_kinematic_simulator_amd import make_linked_simulator
+
+    wl = W.cfg5(48 / 1048576)
+    sim = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
+    sim.set_robot(wl.robot)
+    geo = sim.launch_geometry()
+    import torch
+
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert geo["resident_waves"] == 16 * cus, geo
+    for seg in (None, 7):
+        sim.reset_statistics()  # GetStatistics accumulates over calls (SPCS:488-512)
+        g, o = run_both(wl, sim=sim, segment_steps=seg)
+        assert_identical(g, o)
+        assert_counters_identical(g, o)
+    sim.close()
