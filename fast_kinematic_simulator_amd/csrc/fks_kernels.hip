@@ -982,6 +982,10 @@ __device__ double config_distance(Sim& s, const double* cfg, const double* targe
  * one that keeps them above 0.5 + 1.5*lplus cannot produce a correction.  Skipped
  * points are still counted in the algorithmic bytes the reference reads (their
  * grid margin guarantees they are in bounds). */
+/* an upper bound of sqrt(x) for the proofs (never for results): the hardware v_sqrt_f64 is
+ * within 2^29 ulp (2^-23 relative) of the root, so one instruction scaled by 1 + 2^-20
+ * replaces the correctly rounded sequence (a dozen dependent instructions) */
+__device__ __forceinline__ double sqrt_upper(double x) { return __builtin_amdgcn_sqrt(x) * (1.0 + 0x1p-20); }
 __device__ __forceinline__ double rigid_motion_bound(const double* T, const double* Tref, double radius) {
     const double dt0 = T[3] - Tref[3], dt1 = T[7] - Tref[7], dt2 = T[11] - Tref[11];
     double f = 0.0;
@@ -992,7 +996,7 @@ __device__ __forceinline__ double rigid_motion_bound(const double* T, const doub
             const double d = T[4 * r + c] - Tref[4 * r + c];
             f = f + d * d;
         }
-    const double b = dsqrt((dt0 * dt0 + dt1 * dt1) + dt2 * dt2) + dsqrt(f) * radius;
+    const double b = sqrt_upper((dt0 * dt0 + dt1 * dt1) + dt2 * dt2) + sqrt_upper(f) * radius;
     return b * (1.0 + 1e-9) + 1e-12;
 }
 __device__ __forceinline__ double wave_min(double v) {
