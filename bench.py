@@ -3,11 +3,14 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-A "step" is one ForwardSimulateRobots batch (SPCS:788) of the headline workload
-cfg3 (7-DOF arm, 256^3 SDF @ 1 cm, 65,536 particles x 200 controller steps) per GPU,
-inputs already resident in HBM, followed by the RCCL gather of every particle's
-outcome (reached configuration, collided flag, microstep / resolver counts, error
-bits) to rank 0.  value = particle-microsteps executed by all ranks / max-over-ranks
+`--gpus N` (N > 1) without a launcher starts the N rank processes itself (spawn_ranks);
+under a launcher WORLD_SIZE must equal N.  A "step" is one ForwardSimulateRobots batch
+(SPCS:788) of the headline workload cfg3 (7-DOF arm, 256^3 SDF @ 1 cm, 65,536 particles
+x 200 controller steps) per GPU, inputs already resident in HBM, followed (with more than
+one rank, or under a launcher) by the RCCL gather of every particle's outcome (reached
+configuration, collided flag, microstep / resolver counts, error bits) to rank 0; a
+single process without a launcher skips the gather and its line says so.
+value = particle-microsteps executed by all ranks / max-over-ranks
 wall time of the K timed steps (weak scaling: each GPU owns 65,536 particles; RNG
 streams are keyed by global particle id so shards are independent).
 
@@ -178,17 +181,32 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config-check", action="store_true", help="skip the batched CheckConfigCollision line")
     ap.add_argument("--segment-steps", type=int, default=-1, help="A/B: fks_set_segment_steps (default: automatic)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rendezvous / shard / gather check without a GPU (gloo): no simulation, value null")
     args = ap.parse_args()
-
+    if args.gpus < 1:
+        log("--gpus must be >= 1")
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no external launcher: start one rank process per GPU before anything touches a GPU
+        return spawn_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
     import torch
 
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    if torch.cuda.device_count() <= local_rank:
+        log(f"[rank {rank}] needs GPU {local_rank}, {torch.cuda.device_count()} visible")
+        return 1
     torch.cuda.set_device(local_rank)
     dist = None
-    # under torchrun (RANK/MASTER_ADDR set) the RCCL process group is used even at
+    # under a launcher (RANK/MASTER_ADDR set) the RCCL process group is used even at
     # world size 1, so the launched path is the one the multi-GPU runs take
     if world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ):
         import torch.distributed as dist
@@ -332,8 +350,10 @@ def main():
             "dtype": "f64",
             "data": f"synthetic (seeded {args.workload} scene and start perturbations, workloads.py)",
             "config": {
-                "workload": f"{workload_desc}, {n_local} particles per GPU, allow_contacts, RCCL gather of outcomes "
-                            f"to rank 0",
+                "workload": f"{workload_desc}, {n_local} particles per GPU, allow_contacts"
+                            + (f", RCCL gather of outcomes to rank 0 over {world} ranks" if dist is not None else
+                               ", one process (no gather: outcomes stay on this GPU)"),
+                "outcome_gather": "rccl" if dist is not None else None,
                 "particles_per_gpu": n_local,
                 "particles_total": n_local * world,
                 "controller_steps": wl.steps,
@@ -381,7 +401,78 @@ def main():
     if dist is not None:
         dist.barrier()  # rank 0 ran the CPU baseline and the config-check line after the timed region
         dist.destroy_process_group()
+    return 0
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: N child processes of this script, rank r on
+    GPU r (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT), the same
+    RCCL path torch.distributed.run gives.  No GPU is touched here; only rank 0 prints the
+    line.  Any failed rank fails the run (the others are stopped by PID)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    log(f"started {n} rank processes (MASTER_PORT {port})")
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                log(f"rank process {procs.index(p)} exited with {code}: stopping the others")
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def dry_run(args, world: int, rank: int) -> int:
+    """The multi-process plumbing without a GPU (CPU tests): gloo process group, this rank's
+    shard of the batch, the outcome gather to rank 0 (each row carries its global particle id,
+    so rank 0 checks that the concatenation is the whole batch in order), max-over-ranks
+    timing.  Nothing is simulated: the line says so and its value is null."""
+    import torch
+    import torch.distributed as dist
+
+    from fast_kinematic_simulator_amd.sharding import OUTCOME_EXTRA, gather_outcomes, shard_bounds
+
+    base, per_gpu, workload_desc = WORKLOADS[args.workload]
+    n_total = (args.particles or per_gpu) * world
+    lo, hi = shard_bounds(n_total, world, rank)
+    dist.init_process_group("gloo")
+    log(f"[rank {rank}] joined the gloo process group (world size {world}, dry run)")
+    W = 7
+    packed = torch.zeros((hi - lo, W + OUTCOME_EXTRA), dtype=torch.float64)
+    packed[:, 0] = torch.arange(lo, hi, dtype=torch.float64)
+    dist.barrier()
+    t0 = time.perf_counter()
+    full = gather_outcomes(packed, dist, n_total, world, rank)
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ok = True
+    if rank == 0:
+        ok = full.shape[0] == n_total and bool(torch.equal(full[:, 0], torch.arange(n_total, dtype=torch.float64)))
+        print(json.dumps({"metric": METRIC, "value": None, "unit": UNIT, "n_gpus": world, "steps": 0, "warmup": 0,
+                          "dry_run": True, "gather_verified": ok, "gather_ms": float(t.item()) * 1e3,
+                          "config": {"workload": f"{workload_desc}: dry run, nothing simulated",
+                                     "particles_per_gpu": hi - lo, "particles_total": n_total,
+                                     "parallelism": f"dp{world} (particle shards)", "outcome_gather": "gloo"}}), flush=True)
+    dist.destroy_process_group()
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -82,6 +82,15 @@ def _load(path):
                                       POINTER(c_double)]
     L.oracle_counter_truncated_normal.restype = c_double
     L.oracle_counter_truncated_normal.argtypes = [c_uint64, c_uint64, c_uint64, c_uint32, c_uint32, c_uint32, POINTER(c_uint32)]
+    L.oracle_qr_info.restype = None
+    L.oracle_qr_info.argtypes = [POINTER(c_double), c_uint64, c_uint64, POINTER(c_double), POINTER(c_double), POINTER(c_uint64),
+                                 POINTER(c_uint64)]
+    L.oracle_capture_systems.restype = None
+    L.oracle_capture_systems.argtypes = [c_uint64, c_uint64, c_uint64]
+    L.oracle_captured_systems.restype = c_uint64
+    L.oracle_captured_systems.argtypes = [POINTER(c_uint64), POINTER(c_uint64)]
+    L.oracle_copy_captured.restype = None
+    L.oracle_copy_captured.argtypes = [POINTER(c_double), POINTER(c_double), POINTER(c_uint64)]
     L.oracle_qr_solve.restype = None
     L.oracle_qr_solve.argtypes = [POINTER(c_double), c_uint64, c_uint64, POINTER(c_double), POINTER(c_double)]
     L.oracle_estimate_distance.restype = None
@@ -231,6 +240,45 @@ def qr_solve(J, b):
     x = np.zeros(J.shape[1])
     lib().oracle_qr_solve(_p(J, c_double), J.shape[0], J.shape[1], _p(b, c_double), _p(x, c_double))
     return x
+
+
+def qr_info(J, b):
+    """The oracle's ColPivHouseholderQR of J (SPCS:1994): (basic solution x, permutation
+    perm with perm[i] = the original column of pivot i, number of nonzero pivots)."""
+    J = np.ascontiguousarray(J, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    D = J.shape[1]
+    x = np.zeros(D)
+    perm = np.zeros(D, dtype=np.uint64)
+    nz = c_uint64(0)
+    lib().oracle_qr_info(_p(J, c_double), J.shape[0], D, _p(b, c_double), _p(x, c_double), _p(perm, c_uint64), ctypes.byref(nz))
+    return x, perm.astype(np.int64), int(nz.value)
+
+
+@contextlib.contextmanager
+def captured_systems(max_systems, stride=1, max_rows=64):
+    """Record the stacked least-squares systems (J, b) the simulator solves inside the block
+    (every `stride`-th with at most `max_rows` rows); yields a list filled on exit."""
+    L = lib()
+    out = []
+    L.oracle_capture_systems(int(max_systems), int(stride), int(max_rows))
+    try:
+        yield out
+    finally:
+        nj, nb = c_uint64(0), c_uint64(0)
+        n = int(L.oracle_captured_systems(ctypes.byref(nj), ctypes.byref(nb)))
+        J = np.zeros(nj.value)
+        b = np.zeros(nb.value)
+        shape = np.zeros(2 * n, dtype=np.uint64)
+        if n:
+            L.oracle_copy_captured(_p(J, c_double), _p(b, c_double), _p(shape, c_uint64))
+        L.oracle_capture_systems(0, 1, 0)
+        oj = ob = 0
+        for k in range(n):
+            r, c = int(shape[2 * k]), int(shape[2 * k + 1])
+            out.append((J[oj:oj + r * c].reshape(r, c).copy(), b[ob:ob + r].copy()))
+            oj += r * c
+            ob += r
 
 
 def estimate_distance(env, points):

@@ -27,6 +27,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -301,8 +302,11 @@ static Dense inverse(const Dense& A) {
  * (tol = DBL_MIN), nonzero pivots by threshold maxColSqNorm*eps^2/R*(R-k), Q^T b
  * applied for k < nonzero pivots, column-oriented back substitution, basic
  * solution (zeros in non-pivot unknowns).  Long sums are canon_sum(). */
-std::vector<double> colpiv_qr_solve(const std::vector<double>& Jrm, size_t R, size_t D, const std::vector<double>& b) {
+std::vector<double> colpiv_qr_solve(const std::vector<double>& Jrm, size_t R, size_t D, const std::vector<double>& b,
+                                    std::vector<size_t>* perm_out = nullptr, size_t* nonzero_out = nullptr) {
     std::vector<double> x(D, 0.0);
+    if (perm_out) perm_out->assign(D, 0);
+    if (nonzero_out) *nonzero_out = 0;
     if (D == 0) return x;
     /* column-major working copy */
     std::vector<double> qr(R * D);
@@ -375,6 +379,8 @@ std::vector<double> colpiv_qr_solve(const std::vector<double>& Jrm, size_t R, si
     std::vector<size_t> perm(D);
     for (size_t i = 0; i < D; ++i) perm[i] = i;
     for (size_t k = 0; k < size; ++k) std::swap(perm[k], perm[transpositions[k]]);
+    if (perm_out) *perm_out = perm;
+    if (nonzero_out) *nonzero_out = nonzero_pivots;
     if (nonzero_pivots == 0) return x;
     std::vector<double> c(b);
     for (size_t k = 0; k < nonzero_pivots; ++k) {
@@ -399,6 +405,28 @@ std::vector<double> colpiv_qr_solve(const std::vector<double>& Jrm, size_t R, si
     for (size_t i = 0; i < nonzero_pivots; ++i) x[perm[i]] = c[i];
     for (size_t i = nonzero_pivots; i < D; ++i) x[perm[i]] = 0.0;
     return x;
+}
+
+/* Capture of the stacked least-squares systems the simulator solves (SPCS:1990-1998),
+ * for the pivot-rule pin against LAPACK dgeqp3 (tests/golden/make_qr_golden.py): every
+ * `stride`-th system with at most `max_rows` rows, up to `max_systems` of them. */
+struct SystemCapture {
+    std::mutex mu;
+    uint64_t max_systems = 0, stride = 1, max_rows = 0, seen = 0;
+    std::vector<double> J, b;
+    std::vector<uint64_t> shape; /* rows, cols per system */
+};
+static SystemCapture g_capture;
+
+static void capture_system(const std::vector<double>& Jrm, size_t R, size_t D, const std::vector<double>& b) {
+    if (g_capture.max_systems == 0) return;
+    std::lock_guard<std::mutex> lock(g_capture.mu);
+    if (g_capture.shape.size() / 2 >= g_capture.max_systems || R == 0 || R > g_capture.max_rows) return;
+    if ((g_capture.seen++ % g_capture.stride) != 0) return;
+    g_capture.J.insert(g_capture.J.end(), Jrm.begin(), Jrm.begin() + (long)(R * D));
+    g_capture.b.insert(g_capture.b.end(), b.begin(), b.begin() + (long)R);
+    g_capture.shape.push_back(R);
+    g_capture.shape.push_back(D);
 }
 
 /* ComputeResolverCorrectionStepIndividualJacobians (SPCS:1966-1988): each corrected
@@ -856,6 +884,7 @@ class Simulator {
                                                         self_collision_map, J, b, rows, pc);
                     pc.lsq_rows += rows;
                     if (pc.error_flags) return ResolveResult{previous_configuration, collided, false, true};
+                    if (!simulate_with_individual_jacobians_) capture_system(J, rows, D, b);
                     /* SPCS:1629: individual (SPCS:1966-1988) or stacked (SPCS:1990-1998) solve */
                     const std::vector<double> raw_correction_step = simulate_with_individual_jacobians_
                                                                         ? individual_jacobians_solve(J, rows, D, b)
@@ -1166,6 +1195,45 @@ double oracle_counter_truncated_normal(uint64_t seed, uint64_t call_index, uint6
 }
 
 /* J row-major R x D */
+/* the column permutation (perm[i] = original column of pivot i) and nonzero-pivot count
+ * of the oracle's ColPivHouseholderQR, with its basic solution */
+void oracle_qr_info(const double* J, uint64_t R, uint64_t D, const double* b, double* x, uint64_t* perm, uint64_t* nonzero) {
+    const std::vector<double> Jv(J, J + R * D), bv(b, b + R);
+    std::vector<size_t> p;
+    size_t nz = 0;
+    const std::vector<double> xv = colpiv_qr_solve(Jv, (size_t)R, (size_t)D, bv, &p, &nz);
+    for (size_t i = 0; i < (size_t)D; ++i) {
+        x[i] = xv[i];
+        perm[i] = p[i];
+    }
+    *nonzero = nz;
+}
+
+void oracle_capture_systems(uint64_t max_systems, uint64_t stride, uint64_t max_rows) {
+    std::lock_guard<std::mutex> lock(g_capture.mu);
+    g_capture.max_systems = max_systems;
+    g_capture.stride = stride ? stride : 1;
+    g_capture.max_rows = max_rows;
+    g_capture.seen = 0;
+    g_capture.J.clear();
+    g_capture.b.clear();
+    g_capture.shape.clear();
+}
+
+uint64_t oracle_captured_systems(uint64_t* nvalues_J, uint64_t* nvalues_b) {
+    std::lock_guard<std::mutex> lock(g_capture.mu);
+    *nvalues_J = g_capture.J.size();
+    *nvalues_b = g_capture.b.size();
+    return g_capture.shape.size() / 2;
+}
+
+void oracle_copy_captured(double* J, double* b, uint64_t* shape) {
+    std::lock_guard<std::mutex> lock(g_capture.mu);
+    std::copy(g_capture.J.begin(), g_capture.J.end(), J);
+    std::copy(g_capture.b.begin(), g_capture.b.end(), b);
+    std::copy(g_capture.shape.begin(), g_capture.shape.end(), shape);
+}
+
 void oracle_qr_solve(const double* J, uint64_t R, uint64_t D, const double* b, double* x) {
     const std::vector<double> Jv(J, J + R * D), bv(b, b + R);
     const std::vector<double> xv = colpiv_qr_solve(Jv, (size_t)R, (size_t)D, bv);

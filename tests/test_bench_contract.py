@@ -30,6 +30,8 @@ def test_bench_json_line():
     assert d["metric"] == metric and d["n_gpus"] == 1 and d["steps"] == 1 and d["warmup"] == 1
     assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak" and d["vs_baseline"] is None
     assert d["dtype"] == "f64" and "workload" in d["config"]
+    # one process, no launcher: no gather ran, and the line does not claim one
+    assert d["config"]["outcome_gather"] is None and "RCCL" not in d["config"]["workload"]
     r = d["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
     f = r["fp64"]
@@ -60,4 +62,64 @@ def test_bench_under_torchrun():
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and d["value"] > 0 and d["config"]["particles_total"] == 2048
+    assert d["config"]["outcome_gather"] == "rccl"
     assert "process group" in p.stderr  # bench.py logs the RCCL group it joined
+
+
+def _run_bench(args, timeout=240, env=None):
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], stdout=subprocess.PIPE,
+                          stderr=subprocess.PIPE, text=True, timeout=timeout, cwd=ROOT, env=env)
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.strip().startswith("{")]
+
+
+def test_bench_spawns_its_own_ranks():
+    """`bench.py --gpus 2` with no launcher starts two rank processes itself (RANK / WORLD_SIZE /
+    MASTER_ADDR), which join one process group, shard the batch and gather the outcomes to
+    rank 0 (gloo here, --dry-run: nothing is simulated without a GPU)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = _run_bench(["--gpus", "2", "--particles", "64", "--no-cpu-baseline", "--dry-run"], env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["dry_run"] is True and d["value"] is None and d["gather_verified"] is True
+    assert d["config"]["particles_total"] == 128 and d["config"]["particles_per_gpu"] == 64
+    assert "started 2 rank processes" in p.stderr
+    assert p.stderr.count("joined the gloo process group (world size 2") == 2
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """--gpus N beyond the visible devices fails (non-zero), it never times fewer GPUs."""
+    import torch
+
+    n = torch.cuda.device_count()
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = _run_bench(["--gpus", str(n + 1), "--particles", "64", "--no-cpu-baseline", "--no-config-check"], env=env)
+    assert p.returncode != 0
+    assert not _json_lines(p.stdout)
+    assert f"needs GPU {n}" in p.stderr
+
+
+def test_bench_refuses_world_size_mismatch():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = _run_bench(["--gpus", "4", "--particles", "64", "--no-cpu-baseline", "--dry-run"], env=env)
+    assert p.returncode == 2 and "WORLD_SIZE=2" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_spawns_ranks_on_gpus():
+    """The real RCCL path of `bench.py --gpus 2` (two GPUs, one rank each)."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = _run_bench(["--gpus", "2", "--particles", "1024", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
+                    "--no-config-check"], timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _json_lines(p.stdout)[0]
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["outcome_gather"] == "rccl"
+    assert d["config"]["particles_total"] == 2048

@@ -107,3 +107,36 @@ def test_multi_device_context_matches_single(fks_lib, oracle_lib, devices):
     o = oracle.forward_simulate(wl.environment(), wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts, wl.targets, True,
                                 call_index=3)
     assert np.array_equal(m["positions"], o["positions"])
+
+
+@pytest.mark.gpu
+def test_multi_device_context_over_every_visible_gpu(fks_lib, oracle_lib):
+    """fks_create_multi over every visible MI355X (one shard per physical device): results
+    bit-identical to one context and to the oracle, statistics summed (skips below 2 GPUs)."""
+    import torch
+
+    import oracle
+    from fast_kinematic_simulator_amd import MultiDeviceSimulator, make_linked_simulator
+    from fast_kinematic_simulator_amd import workloads as W
+
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("needs 2 or more GPUs")
+    wl = W.cfg3((16 * n + 3) / 65536)
+    multi = MultiDeviceSimulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed, list(range(n)))
+    single = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
+    try:
+        assert multi.num_devices() == n
+        multi.set_call_index(5)
+        single.set_call_index(5)
+        m = multi.forward_simulate_arrays(wl.robot, wl.starts, wl.targets, True)
+        s = single.forward_simulate_arrays(wl.robot, wl.starts, wl.targets, True)
+        for k in ("positions", "collided", "microsteps", "resolver_iterations", "error_flags"):
+            assert np.array_equal(m[k], s[k]), k
+        assert multi.get_statistics() == single.get_statistics()
+    finally:
+        multi.close()
+        single.close()
+    o = oracle.forward_simulate(wl.environment(), wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts, wl.targets, True,
+                                call_index=5)
+    assert np.array_equal(m["positions"], o["positions"]) and np.array_equal(m["microsteps"], o["microsteps"])

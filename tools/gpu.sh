@@ -1,0 +1,64 @@
+# One parametrised GPU-box tool (run through gpurun from the repository root).  Each step
+# runs under its own time limit and the chain stops at the first failure.
+#
+# usage: bash tools/gpu.sh <tag> <task> [<task> ...]
+#   suite              pytest -m gpu (whole suite)                  -> <tag>_pytest_gpu.log
+#   smoke              __graft_entry__.smoke()                      -> <tag>_smoke.log
+#   bench[:cfgN]       bench.py (default workload, or --workload cfgN) -> <tag>_bench[_cfgN].json
+#   others             bench lines of cfg1 / cfg2 / cfg4 / cfg5
+#   trace              rocprofv3 --kernel-trace --stats of bench.py -> <tag>_trace/
+#   pmc                FETCH_SIZE / WRITE_SIZE / TCC hit+miss, one --pmc pass each -> <tag>_pmc_*/
+#   valu               VALUBusy / VALUUtilization / SQ issue counters, one pass each -> <tag>_valu/
+#   ab:<wl>:<libs>     interleaved bench.py of comma-separated libraries (each may carry +flag;
+#                      "L" = the product library) on workload <wl>  -> <tag>_ab_<wl>.log
+#   tail:<wl>:<lib>    heaviest particles alone + phase shares (tools/tail_latency.py) -> <tag>_tail_<wl>_<lib>.json
+#   torchrun1          bench.py through torch.distributed.run, world size 1 (RCCL) -> <tag>_torchrun_w1.json
+#   round              suite smoke bench trace pmc others
+set -o pipefail
+TAG=$1
+shift
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+O=gpurun_out
+L=fast_kinematic_simulator_amd/libfks_hip.so
+BP="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
+lib() { [ "$1" = L ] && echo $L || echo "$1"; }
+
+run_task() {
+  case "$1" in
+  suite) timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/${TAG}_pytest_gpu.log 2>&1 ;;
+  smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1 ;;
+  bench) timeout -k 10 400 python bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err ;;
+  bench:*) w=${1#bench:}; timeout -k 10 300 python bench.py --workload $w --no-config-check > $O/${TAG}_bench_$w.json 2> $O/${TAG}_bench_$w.err ;;
+  others) for w in cfg1 cfg2 cfg4 cfg5; do run_task bench:$w || return $?; done ;;
+  trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_trace -o bench -- $BP > $O/${TAG}_bench_under_rocprof.json 2> $O/${TAG}_trace.err ;;
+  pmc)
+    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_fetch -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_fetch.err &&
+    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_write -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_write.err &&
+    timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/${TAG}_pmc_tcc -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_tcc.err ;;
+  valu)
+    B1="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-check"
+    mkdir -p $O/${TAG}_valu
+    timeout -s KILL 180 rocprofv3 --pmc VALUBusy --kernel-trace --output-format csv -d $O/${TAG}_valu/valubusy -o bench -- $B1 > /dev/null 2> $O/${TAG}_valu/valubusy.err &&
+    timeout -s KILL 180 rocprofv3 --pmc VALUUtilization --kernel-trace --output-format csv -d $O/${TAG}_valu/valuutil -o bench -- $B1 > /dev/null 2> $O/${TAG}_valu/valuutil.err &&
+    timeout -s KILL 180 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $O/${TAG}_valu/issue -o bench -- $B1 > /dev/null 2> $O/${TAG}_valu/issue.err ;;
+  ab:*)
+    spec=${1#ab:}; w=${spec%%:*}; libs=${spec#*:}; args=()
+    for x in ${libs//,/ }; do args+=("$(lib ${x%%+*})${x#${x%%+*}}"); done
+    extra=""; [ "$w" != cfg3 ] && extra="--workload $w --no-config-check"
+    timeout -k 10 1000 python tools/variant_bench.py "${args[@]}" $extra > $O/${TAG}_ab_$w.log 2>&1 ;;
+  tail:*)
+    spec=${1#tail:}; w=${spec%%:*}; l=$(lib ${spec#*:}); n=$(basename $l .so)
+    FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1 timeout -k 10 400 python tools/tail_latency.py --workload $w --top 3 --json $O/${TAG}_tail_${w}_$n.json > $O/${TAG}_tail_${w}_$n.log 2>&1 ;;
+  torchrun1) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_torchrun_w1.json 2> $O/${TAG}_torchrun_w1.err ;;
+  round) for t in suite smoke bench trace pmc others; do run_task $t || return $?; done ;;
+  *) echo "unknown task $1" >&2; return 2 ;;
+  esac
+}
+
+for t in "$@"; do
+  echo "[$(date +%T)] $t"
+  run_task "$t" || { rc=$?; echo "task $t failed: $rc"; exit $rc; }
+done
+echo done
