@@ -255,12 +255,18 @@ PROTOTYPES = [
     ("fks_get_call_index", c_uint64, [c_void_p]),
     ("fks_get_statistics", c_int32, [c_void_p, POINTER(Statistics)]),
     ("fks_reset_statistics", c_int32, [c_void_p]),
+    ("fks_set_statistics", c_int32, [c_void_p, POINTER(Statistics)]),
     ("fks_reset_generators", c_int32, [c_void_p, c_uint64]),
     ("fks_get_debug_level", c_int32, [c_void_p]),
     ("fks_set_debug_level", c_int32, [c_void_p, c_int32]),
     ("fks_get_last_call_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
     ("fks_get_total_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
     ("fks_reset_total_counters", c_int32, [c_void_p]),
+    ("fks_set_total_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
+    ("fks_robot_control_action", c_int32, [POINTER(RobotDesc), POINTER(c_double), POINTER(c_double), c_double, POINTER(c_double),
+                                           POINTER(c_double)]),
+    ("fks_robot_apply_control_input", c_int32, [POINTER(RobotDesc), POINTER(c_double), POINTER(c_double), POINTER(c_double),
+                                                POINTER(c_double)]),
     ("fks_get_phase_cycles", c_int32, [c_void_p, c_int32, POINTER(c_uint64)]),
     ("fks_get_launch_geometry", c_int32, [c_void_p, POINTER(c_uint32), POINTER(c_uint64)]),
     ("fks_set_segment_steps", c_int32, [c_void_p, c_uint32]),
@@ -277,6 +283,9 @@ PROTOTYPES = [
     ("fks_create_from_device_env", c_int32, [c_void_p, POINTER(SolverParams), c_double, c_uint64, c_int32, POINTER(c_void_p)]),
     ("fks_env_view", c_int32, [c_void_p, POINTER(Environment)]),
     ("fks_env_occupancy", c_int32, [c_void_p, POINTER(c_uint8), c_uint64]),
+    ("fks_env_discretize_obstacle", c_int32, [POINTER(Obstacle), c_double, POINTER(c_double), c_uint64, POINTER(c_uint64)]),
+    ("fks_env_build_normals", c_int32, [POINTER(Obstacle), c_int32, POINTER(GridGeometry), POINTER(c_float), POINTER(c_void_p)]),
+    ("fks_env_cell_objects", c_int32, [c_void_p, POINTER(c_uint32), c_uint64]),
     ("fks_env_free", None, [c_void_p]),
     ("fks_selftest_math", c_int32, [c_int32, c_uint64, POINTER(c_uint64)]),
     ("fks_shard_bounds", c_int32, [c_uint64, c_int32, c_int32, POINTER(c_uint64), POINTER(c_uint64)]),

@@ -12,8 +12,10 @@ import subprocess
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-SOURCES = ["csrc/fks_kernels.hip", "csrc/fks_capi.cpp", "csrc/fks_multi.cpp", "csrc/fks_env_builder.cpp", "csrc/fks_env_gpu.hip"]
-HEADERS = ["csrc/fks_device.h", "csrc/fks_env_internal.h", "../include/fks_capi.h", "../include/fks_portable_math.h"]
+SOURCES = ["csrc/fks_kernels.hip", "csrc/fks_capi.cpp", "csrc/fks_multi.cpp", "csrc/fks_env_builder.cpp", "csrc/fks_env_gpu.hip",
+           "csrc/fks_robot_control.cpp"]
+HEADERS = ["csrc/fks_device.h", "csrc/fks_env_internal.h", "csrc/fks_se3.h", "../include/fks_capi.h",
+           "../include/fks_portable_math.h"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 
 
@@ -21,9 +23,9 @@ def hipcc() -> str:
     return shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 
-def build_command(output: str, defines=()) -> list:
+def build_command(output: str, defines=(), flags=()) -> list:
     return [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
-            *[f"-D{d}" for d in defines],
+            *[f"-D{d}" for d in defines], *flags,
             f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(PKG, 'csrc')}", "-x", "hip",
             *[os.path.join(PKG, s) for s in SOURCES], "-o", output]
 
@@ -50,11 +52,15 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
     return target
 
 
-def build_variant(output: str, defines) -> str:
-    """Build a tuning variant (e.g. FKS_WAVES_PER_EU=3) to a separate path; load it
-    with FKS_LIB_PATH=<output> (tools/variant_bench.py)."""
+def build_variant(output: str, defines=(), flags=()) -> str:
+    """Build a tuning or diagnostic variant (e.g. FKS_WAVES_PER_EU=3, FKS_PHASE_TIMERS=1, or
+    extra compiler flags) to a separate path; load it with FKS_LIB_PATH=<output> and
+    FKS_VARIANT_LIB=1 (tools/variant_bench.py).  A variant never takes the product's name."""
     output = os.path.abspath(output)
-    proc = subprocess.run(build_command(output, defines), cwd=PKG, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if os.path.basename(output) == "libfks_hip.so":
+        raise ValueError("a build variant must not be named libfks_hip.so (the product library)")
+    proc = subprocess.run(build_command(output, defines, flags), cwd=PKG, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                          text=True)
     if proc.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + proc.stdout[-6000:])
     return output

@@ -1458,6 +1458,13 @@ fks_status fks_reset_statistics(fks_context* ctx) {
     std::memset(&ctx->stats, 0, sizeof(ctx->stats));
     return FKS_OK;
 }
+fks_status fks_set_statistics(fks_context* ctx, const fks_statistics* stats) {
+    if (!ctx || !stats) return FKS_ERR_INVALID_ARGUMENT;
+    fks_status st = settle(ctx);
+    if (st != FKS_OK) return st;
+    ctx->stats = *stats;
+    return FKS_OK;
+}
 fks_status fks_reset_generators(fks_context* ctx, uint64_t prng_seed) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
     ctx->seed = prng_seed;
@@ -1483,6 +1490,13 @@ fks_status fks_get_total_counters(const fks_context* ctx, fks_call_counters* out
     fks_status st = settle(const_cast<fks_context*>(ctx));
     if (st != FKS_OK) return st;
     *out = ctx->total;
+    return FKS_OK;
+}
+fks_status fks_set_total_counters(fks_context* ctx, const fks_call_counters* totals) {
+    if (!ctx || !totals) return FKS_ERR_INVALID_ARGUMENT;
+    fks_status st = settle(ctx);
+    if (st != FKS_OK) return st;
+    ctx->total = *totals;
     return FKS_OK;
 }
 fks_status fks_reset_total_counters(fks_context* ctx) {

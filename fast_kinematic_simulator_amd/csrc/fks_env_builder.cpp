@@ -111,6 +111,72 @@ struct Entry {
     double e[6];
 };
 
+/* BuildSurfaceNormalsGrid (SEB.cpp:258-468) on `sdf` (VoxelGrid order over `grid`): the
+ * obstacles' boundary samples get their exact face / edge / corner entries (last write wins),
+ * every other cell with a negative distance its SDF-gradient entry (pass 1) */
+void build_normals(const fks_obstacle* obstacles, int32_t num_obstacles, const Grid& grid, const float* sdf,
+                   std::vector<uint32_t>* offsets_out, std::vector<double>* entries_out) {
+    const double resolution = grid.res;
+    const double effective_resolution = resolution * 0.5;
+    const size_t total = grid.cells();
+    auto sdf_at = [&](int64_t i, int64_t j, int64_t k) { return sdf[grid.linear(i, j, k)]; };
+    /* pass 2 first into a map (last write wins); pass 1 fills the rest */
+    std::unordered_map<size_t, std::vector<Entry>> surface;
+    for (int32_t o = 0; o < num_obstacles; ++o) {
+        const fks_obstacle& ob = obstacles[o];
+        int32_t nc[3];
+        for (int a = 0; a < 3; ++a) nc[a] = (int32_t)(ob.extents[a] * 2.0 * (1.0 / effective_resolution));
+        for (int32_t xi = 0; xi < nc[0]; ++xi)
+            for (int32_t yi = 0; yi < nc[1]; ++yi)
+                for (int32_t zi = 0; zi < nc[2]; ++zi) {
+                    const int32_t id3[3] = {xi, yi, zi};
+                    bool boundary = false;
+                    for (int a = 0; a < 3; ++a) boundary = boundary || id3[a] == 0 || id3[a] == nc[a] - 1;
+                    if (!boundary) continue;
+                    const double local[3] = {-(ob.extents[0] - effective_resolution) + (effective_resolution * xi),
+                                             -(ob.extents[1] - effective_resolution) + (effective_resolution * yi),
+                                             -(ob.extents[2] - effective_resolution) + (effective_resolution * zi)};
+                    double w[3];
+                    xform3(ob.pose, local, w);
+                    int64_t idx[3];
+                    /* UpdateSurfaceNormalGridCell SEB.cpp:162-187 */
+                    if (!grid.index(w, idx)) continue; /* GetImmutable3d OOB = +inf, then insert fails */
+                    const float distance = sdf_at(idx[0], idx[1], idx[2]);
+                    if (!((double)distance > -(resolution * 1.5))) continue;
+                    std::vector<Entry> list;
+                    for (int a = 0; a < 3; ++a) {
+                        if (id3[a] != 0 && id3[a] != nc[a] - 1) continue;
+                        /* StoredSurfaceNormal: SafeNormal(normal), SafeNormal((entry, 0)) */
+                        Entry E;
+                        fks_env::face_entry(ob.pose, a, id3[a] == 0, E.e);
+                        list.push_back(E);
+                    }
+                    surface[grid.linear(idx[0], idx[1], idx[2])] = list;
+                }
+    }
+    offsets_out->assign(total + 1, 0);
+    uint64_t count = 0;
+    for (int64_t i = 0; i < grid.n[0]; ++i)
+        for (int64_t j = 0; j < grid.n[1]; ++j)
+            for (int64_t k = 0; k < grid.n[2]; ++k) {
+                const size_t c = grid.linear(i, j, k);
+                (*offsets_out)[c] = (uint32_t)count;
+                const auto it = surface.find(c);
+                if (it != surface.end()) {
+                    for (const Entry& E : it->second) entries_out->insert(entries_out->end(), E.e, E.e + 6);
+                    count += it->second.size();
+                } else if (sdf[c] < 0.0f) {
+                    /* pass 1 (SEB.cpp:263-277): SDF gradient (edge gradients enabled), entry 0 */
+                    Entry E;
+                    fks_env::gradient_entry(grid, i, j, k, sdf_at, E.e);
+                    entries_out->insert(entries_out->end(), E.e, E.e + 6);
+                    count += 1;
+                }
+                if (count > 0xffffffffull) throw std::bad_alloc();
+            }
+    (*offsets_out)[total] = (uint32_t)count;
+}
+
 }  // namespace
 
 extern "C" fks_status fks_env_build(const fks_obstacle* obstacles, int32_t num_obstacles, double resolution,
@@ -182,62 +248,8 @@ extern "C" fks_status fks_env_build(const fks_obstacle* obstacles, int32_t num_o
             const double free_distance = fks_math::dsqrt(to_free[c]) * resolution;
             env->sdf[c] = (float)(filled_distance - free_distance);
         }
-        auto sdf_at = [&](int64_t i, int64_t j, int64_t k) { return env->sdf[grid.linear(i, j, k)]; };
-        /* pass 2 first into a map (last write wins); pass 1 fills the rest */
-        std::unordered_map<size_t, std::vector<Entry>> surface;
-        for (int32_t o = 0; o < num_obstacles; ++o) {
-            const fks_obstacle& ob = obstacles[o];
-            int32_t nc[3];
-            for (int a = 0; a < 3; ++a) nc[a] = (int32_t)(ob.extents[a] * 2.0 * (1.0 / effective_resolution));
-            for (int32_t xi = 0; xi < nc[0]; ++xi)
-                for (int32_t yi = 0; yi < nc[1]; ++yi)
-                    for (int32_t zi = 0; zi < nc[2]; ++zi) {
-                        const int32_t id3[3] = {xi, yi, zi};
-                        bool boundary = false;
-                        for (int a = 0; a < 3; ++a) boundary = boundary || id3[a] == 0 || id3[a] == nc[a] - 1;
-                        if (!boundary) continue;
-                        const double local[3] = {-(ob.extents[0] - effective_resolution) + (effective_resolution * xi),
-                                                 -(ob.extents[1] - effective_resolution) + (effective_resolution * yi),
-                                                 -(ob.extents[2] - effective_resolution) + (effective_resolution * zi)};
-                        double w[3];
-                        xform3(ob.pose, local, w);
-                        int64_t idx[3];
-                        /* UpdateSurfaceNormalGridCell SEB.cpp:162-187 */
-                        if (!grid.index(w, idx)) continue; /* GetImmutable3d OOB = +inf, then insert fails */
-                        const float distance = sdf_at(idx[0], idx[1], idx[2]);
-                        if (!((double)distance > -(resolution * 1.5))) continue;
-                        std::vector<Entry> list;
-                        for (int a = 0; a < 3; ++a) {
-                            if (id3[a] != 0 && id3[a] != nc[a] - 1) continue;
-                            /* StoredSurfaceNormal: SafeNormal(normal), SafeNormal((entry, 0)) */
-                            Entry E;
-                            fks_env::face_entry(ob.pose, a, id3[a] == 0, E.e);
-                            list.push_back(E);
-                        }
-                        surface[grid.linear(idx[0], idx[1], idx[2])] = list;
-                    }
-        }
-        env->offsets.assign(total + 1, 0);
-        uint64_t count = 0;
-        for (int64_t i = 0; i < grid.n[0]; ++i)
-            for (int64_t j = 0; j < grid.n[1]; ++j)
-                for (int64_t k = 0; k < grid.n[2]; ++k) {
-                    const size_t c = grid.linear(i, j, k);
-                    env->offsets[c] = (uint32_t)count;
-                    const auto it = surface.find(c);
-                    if (it != surface.end()) {
-                        for (const Entry& E : it->second) env->entries.insert(env->entries.end(), E.e, E.e + 6);
-                        count += it->second.size();
-                    } else if (env->sdf[c] < 0.0f) {
-                        /* pass 1 (SEB.cpp:263-277): SDF gradient (edge gradients enabled), entry 0 */
-                        Entry E;
-                        fks_env::gradient_entry(grid, i, j, k, sdf_at, E.e);
-                        env->entries.insert(env->entries.end(), E.e, E.e + 6);
-                        count += 1;
-                    }
-                    if (count > 0xffffffffull) throw std::bad_alloc();
-                }
-        env->offsets[total] = (uint32_t)count;
+        build_normals(obstacles, num_obstacles, grid, env->sdf.data(), &env->offsets, &env->entries);
+        env->obstacles.assign(obstacles, obstacles + num_obstacles);
     } catch (const std::bad_alloc&) {
         delete env;
         return FKS_ERR_OUT_OF_MEMORY;
@@ -269,3 +281,86 @@ extern "C" fks_status fks_env_occupancy(const fks_env_handle* env, uint8_t* out,
 }
 
 extern "C" void fks_env_free(fks_env_handle* env) { delete env; }
+
+/* DiscretizeObstacle (SEB.cpp:21-46): the world positions of the obstacle's half-resolution
+ * sample lattice, x then y then z (the order BuildEnvironment's SetValue calls take) */
+extern "C" fks_status fks_env_discretize_obstacle(const fks_obstacle* obstacle, double resolution, double* out_xyz,
+                                                  uint64_t capacity, uint64_t* count) {
+    if (!obstacle || !count || !(resolution > 0.0)) return FKS_ERR_INVALID_ARGUMENT;
+    int32_t nc[3];
+    fks_env::obstacle_samples(*obstacle, resolution, nc);
+    const uint64_t n = (nc[0] > 0 && nc[1] > 0 && nc[2] > 0) ? (uint64_t)nc[0] * (uint64_t)nc[1] * (uint64_t)nc[2] : 0;
+    *count = n;
+    if (!out_xyz) return FKS_OK;
+    if (capacity < n) return FKS_ERR_INVALID_ARGUMENT;
+    uint64_t k = 0;
+    for (int32_t xi = 0; xi < nc[0]; ++xi)
+        for (int32_t yi = 0; yi < nc[1]; ++yi)
+            for (int32_t zi = 0; zi < nc[2]; ++zi, ++k)
+                fks_env::obstacle_sample_world(*obstacle, resolution, resolution * 0.5, xi, yi, zi, out_xyz + 3 * k);
+    return FKS_OK;
+}
+
+/* BuildSurfaceNormalsGrid (SEB.cpp:258-468) on a caller's SDF (any SignedDistanceField, e.g.
+ * the planner's own sdf_tools ExtractSignedDistanceField result, SEB.cpp:473-475): a handle
+ * holding only the normal CSR over the SDF's geometry (fks_env_view: sdf_values NULL) */
+extern "C" fks_status fks_env_build_normals(const fks_obstacle* obstacles, int32_t num_obstacles,
+                                            const fks_grid_geometry* sdf_geometry, const float* sdf_values,
+                                            fks_env_handle** out) {
+    if (!out || !sdf_geometry || !sdf_values || num_obstacles < 0 || (num_obstacles > 0 && !obstacles) ||
+        !(sdf_geometry->resolution > 0.0))
+        return FKS_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    Grid grid;
+    grid.res = sdf_geometry->resolution;
+    grid.inv_res = 1.0 / grid.res;
+    std::memcpy(grid.origin, sdf_geometry->origin, sizeof(grid.origin));
+    for (int a = 0; a < 3; ++a) {
+        grid.n[a] = sdf_geometry->num_cells[a];
+        if (grid.n[a] < 1 || grid.n[a] > 4096) return FKS_ERR_INVALID_ARGUMENT;
+    }
+    inverse34(grid.origin, grid.inv_origin);
+    fks_env_handle* env = new (std::nothrow) fks_env_handle();
+    if (!env) return FKS_ERR_OUT_OF_MEMORY;
+    try {
+        build_normals(obstacles, num_obstacles, grid, sdf_values, &env->offsets, &env->entries);
+        env->obstacles.assign(obstacles, obstacles + num_obstacles);
+    } catch (const std::bad_alloc&) {
+        delete env;
+        return FKS_ERR_OUT_OF_MEMORY;
+    }
+    env->geometry = *sdf_geometry;
+    *out = env;
+    return FKS_OK;
+}
+
+/* the object id BuildEnvironment leaves in each cell (SEB.cpp:151-155: every obstacle's
+ * samples SetValue(1.0, object_id) in obstacle order, the last write wins; 0 = free) */
+extern "C" fks_status fks_env_cell_objects(const fks_env_handle* env, uint32_t* out, uint64_t num_cells) {
+    if (!env || (num_cells > 0 && !out)) return FKS_ERR_INVALID_ARGUMENT;
+    Grid grid;
+    grid.res = env->geometry.resolution;
+    grid.inv_res = 1.0 / grid.res;
+    std::memcpy(grid.origin, env->geometry.origin, sizeof(grid.origin));
+    for (int a = 0; a < 3; ++a) grid.n[a] = env->geometry.num_cells[a];
+    if (num_cells != grid.cells()) return FKS_ERR_INVALID_ARGUMENT;
+    if (env->occupancy.size() != num_cells) return FKS_ERR_UNSUPPORTED; /* a normals-only handle */
+    if (env->obstacles.empty())                                          /* a device build's copy */
+        for (uint8_t o : env->occupancy)
+            if (o) return FKS_ERR_UNSUPPORTED;
+    inverse34(grid.origin, grid.inv_origin);
+    std::memset(out, 0, (size_t)num_cells * sizeof(uint32_t));
+    for (const fks_obstacle& ob : env->obstacles) {
+        int32_t nc[3];
+        fks_env::obstacle_samples(ob, grid.res, nc);
+        for (int32_t xi = 0; xi < nc[0]; ++xi)
+            for (int32_t yi = 0; yi < nc[1]; ++yi)
+                for (int32_t zi = 0; zi < nc[2]; ++zi) {
+                    double w[3];
+                    fks_env::obstacle_sample_world(ob, grid.res, grid.res * 0.5, xi, yi, zi, w);
+                    int64_t idx[3];
+                    if (grid.index(w, idx)) out[grid.linear(idx[0], idx[1], idx[2])] = ob.object_id;
+                }
+    }
+    return FKS_OK;
+}

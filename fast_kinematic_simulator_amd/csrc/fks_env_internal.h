@@ -26,6 +26,7 @@ struct fks_env_handle {
     std::vector<uint32_t> offsets;
     std::vector<double> entries;
     std::vector<uint8_t> occupancy;
+    std::vector<fks_obstacle> obstacles; /* what fks_env_build was given (fks_env_cell_objects) */
 };
 
 /* an environment built on the GPU and kept there (fks_env_build_device) */

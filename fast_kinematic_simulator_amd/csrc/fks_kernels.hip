@@ -31,6 +31,7 @@
 #include "fks_capi.h"
 #include "fks_device.h"
 #include "fks_portable_math.h"
+#include "fks_se3.h"
 
 namespace fksd {
 
@@ -116,105 +117,12 @@ __device__ __forceinline__ void angle_axis34(double angle, double a0, double a1,
     M[10] = c1a2 * a2 + c;
 }
 
-/* SE(3) exp/log of body twists: same closed forms as oracle_geometry.h */
-__device__ void se3_coeffs(double theta, double* A, double* B, double* C) {
-    if (theta < 1e-3) {
-        const double t2 = theta * theta;
-        *A = 1.0 - t2 / 6.0 + (t2 * t2) / 120.0;
-        *B = 0.5 - t2 / 24.0 + (t2 * t2) / 720.0;
-        *C = 1.0 / 6.0 - t2 / 120.0 + (t2 * t2) / 5040.0;
-    } else {
-        const double s = fks_math::sin(theta);
-        const double sh = fks_math::sin(0.5 * theta);
-        *A = s / theta;
-        *B = (2.0 * (sh * sh)) / (theta * theta);
-        *C = (theta - s) / ((theta * theta) * theta);
-    }
-}
-__device__ void exp_twist34(const double* tw, double* M) {
-    const D3 v{tw[0], tw[1], tw[2]};
-    const D3 w{tw[3], tw[4], tw[5]};
-    const double theta = dsqrt(sqnorm3(w));
-    double A, B, C;
-    se3_coeffs(theta, &A, &B, &C);
-    const double wv[3] = {w.x, w.y, w.z};
-    const double th2 = (w.x * w.x + w.y * w.y) + w.z * w.z;
-    for (int i = 0; i < 3; ++i) {
-        for (int j = 0; j < 3; ++j) {
-            double Wij = 0.0;
-            if (i == 0 && j == 1) Wij = -w.z;
-            if (i == 0 && j == 2) Wij = w.y;
-            if (i == 1 && j == 0) Wij = w.z;
-            if (i == 1 && j == 2) Wij = -w.x;
-            if (i == 2 && j == 0) Wij = -w.y;
-            if (i == 2 && j == 1) Wij = w.x;
-            const double W2ij = wv[i] * wv[j] - ((i == j) ? th2 : 0.0);
-            M[4 * i + j] = ((i == j) ? 1.0 : 0.0) + A * Wij + B * W2ij;
-        }
-    }
-    const D3 Wv = cross(w, v);
-    const D3 WWv = cross(w, Wv);
-    M[3] = (v.x + B * Wv.x) + C * WWv.x;
-    M[7] = (v.y + B * Wv.y) + C * WWv.y;
-    M[11] = (v.z + B * Wv.z) + C * WWv.z;
-}
-__device__ void log_twist34(const double* T, double* tw) {
-    const double R0 = T[0], R1 = T[1], R2 = T[2], R3 = T[4], R4 = T[5], R5 = T[6], R6 = T[8], R7 = T[9], R8 = T[10];
-    const double cos_arg = (((R0 + R4) + R8) - 1.0) * 0.5;
-    const D3 vee{(R7 - R5) * 0.5, (R2 - R6) * 0.5, (R3 - R1) * 0.5};
-    const double s = dsqrt(sqnorm3(vee));
-    const double theta = fks_math::atan2(s, cos_arg);
-    D3 w;
-    if (theta < 1e-3) {
-        const double f = 1.0 + (theta * theta) / 6.0;
-        w = D3{vee.x * f, vee.y * f, vee.z * f};
-    } else if (s < 1e-6 && cos_arg < 0.0) {
-        const double Rm[9] = {R0, R1, R2, R3, R4, R5, R6, R7, R8};
-        int k = 0;
-        if (Rm[4] > Rm[0]) k = 1;
-        if (Rm[8] > Rm[k * 4]) k = 2;
-        double ax[3];
-        ax[k] = dsqrt((Rm[k * 4] + 1.0) * 0.5);
-        for (int i = 0; i < 3; ++i)
-            if (i != k) ax[i] = (Rm[i * 3 + k] + Rm[k * 3 + i]) / (4.0 * ax[k]);
-        w = D3{ax[0] * theta, ax[1] * theta, ax[2] * theta};
-    } else {
-        const double f = theta / s;
-        w = D3{vee.x * f, vee.y * f, vee.z * f};
-    }
-    const double th = dsqrt(sqnorm3(w));
-    double A, B, C;
-    se3_coeffs(th, &A, &B, &C);
-    double D;
-    if (th < 1e-3) {
-        const double t2 = th * th;
-        D = 1.0 / 12.0 + t2 / 720.0;
-    } else {
-        D = (1.0 - A / (2.0 * B)) / (th * th);
-    }
-    const D3 t{T[3], T[7], T[11]};
-    const D3 Wt = cross(w, t);
-    const D3 WWt = cross(w, Wt);
-    tw[0] = (t.x - 0.5 * Wt.x) + D * WWt.x;
-    tw[1] = (t.y - 0.5 * Wt.y) + D * WWt.y;
-    tw[2] = (t.z - 0.5 * Wt.z) + D * WWt.z;
-    tw[3] = w.x;
-    tw[4] = w.y;
-    tw[5] = w.z;
-}
-/* C = A * B (3x4 row-major), Eigen Transform product order */
-__device__ __forceinline__ void compose34(const double* A, const double* B, double* C) {
-    for (int i = 0; i < 3; ++i) {
-        for (int j = 0; j < 3; ++j)
-            C[4 * i + j] = dot3(A[4 * i + 0], A[4 * i + 1], A[4 * i + 2], B[j], B[4 + j], B[8 + j]);
-        C[4 * i + 3] = dot3(A[4 * i + 0], A[4 * i + 1], A[4 * i + 2], B[3], B[7], B[11]) + A[4 * i + 3];
-    }
-}
-__device__ __forceinline__ void inverse34(const double* T, double* I) {
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) I[4 * i + j] = T[4 * j + i];
-    for (int i = 0; i < 3; ++i) I[4 * i + 3] = -dot3(I[4 * i + 0], I[4 * i + 1], I[4 * i + 2], T[3], T[7], T[11]);
-}
+/* SE(3) exp/log of body twists, 3x4 composition and inverse: fks_se3.h (shared with the
+ * host-side robot control, fks_robot_control.cpp) */
+using fks_se3::compose34;
+using fks_se3::exp_twist34;
+using fks_se3::inverse34;
+using fks_se3::log_twist34;
 
 /* ---------------- wave primitives ---------------- */
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63u); }
@@ -392,27 +300,6 @@ __device__ double sampled_pick(uint32_t k0, uint32_t k1, uint64_t particle, uint
 /* Actuator noise does not depend on the particle state, so the samples of the next
  * floor(64 / D) microsteps are drawn at once, one lane per (microstep, dof), into LDS;
  * noise_sample() consumes them (and their error bits) in the DOF lanes. */
-/* call boundaries of the hot loop (build variants: tools/variant_bench.py) */
-#ifndef FKS_QR_ATTR
-#define FKS_QR_ATTR __noinline__
-#endif
-#ifndef FKS_QR_TILE
-#define FKS_QR_TILE 1
-#endif
-#ifndef FKS_HOT_ATTR
-#define FKS_HOT_ATTR
-#endif
-
-/* Phase-cost profiling builds only (tools/phase_cost.sh): bit b of FKS_PROF_DUP runs
- * phase b of the microstep / resolver loop a second time with identical inputs and
- * outputs, so the difference of SQ_INSTS_* and kernel time against the plain build is
- * that phase's cost.  0 (the product) compiles every repeat away. */
-#ifndef FKS_PROF_DUP
-#define FKS_PROF_DUP 0
-#endif
-enum { kDupFk = 0, kDupInput, kDupEnv, kDupSelf, kDupCorr, kDupSolve, kDupApply, kDupRefill, kDupEnvFull };
-constexpr int prof_reps(int bit) { return 1 + ((FKS_PROF_DUP >> bit) & 1); }
-
 struct Sim;
 __device__ void refill_noise(Sim& s, uint32_t micro0, uint32_t M);
 __device__ __forceinline__ double noise_sample(Sim& s, uint32_t micro);
@@ -529,10 +416,7 @@ __device__ __forceinline__ void count_event(Sim& s, int slot, uint64_t n) {
         if (s.lane == 0) s.phase[slot] += n;
 }
 
-#ifndef FKS_REFILL_ATTR
-#define FKS_REFILL_ATTR __noinline__
-#endif
-__device__ FKS_REFILL_ATTR void refill_noise_lanes(const SimArgs* __restrict__ Ap, double* lds, int ln, uint64_t pid, uint32_t step,
+__device__ __noinline__ void refill_noise_lanes(const SimArgs* __restrict__ Ap, double* lds, int ln, uint64_t pid, uint32_t step,
                                                 uint32_t micro0, uint32_t M) {
     const SimArgs& A = *Ap;
     const int D = A.R.D;
@@ -1202,11 +1086,10 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
  * colliding point; algorithmic bytes are counted up to that point, as the reference
  * reads them (its loop returns at the first colliding point).  Provably-free rounds
  * are not read but still counted (4 B per point, all in bounds). */
-template <bool FULL = false>
-__device__ FKS_HOT_ATTR bool env_collision(Sim& s, const double* T) {
+__device__ bool env_collision(Sim& s, const double* T) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
-    const uint64_t skip = FULL ? 0ull : skippable_rounds(s, T, kSkipCheck);
+    const uint64_t skip = skippable_rounds(s, T, kSkipCheck);
     /* every round proven free (the common microstep): the reference reads 4 bytes per
      * point and finds nothing; account those reads without walking the rounds */
     if (R.nrounds <= kWave) {
@@ -1233,8 +1116,8 @@ __device__ FKS_HOT_ATTR bool env_collision(Sim& s, const double* T) {
             b1 = (i1 < R.P) ? 4 : 0;
         else
             c1 = env_point(A, T, i1, &b1, &S1, &G1, &C1);
-        if (!sk0 && !FULL) round_update(s, r, T, S0, G0, C0);
-        if (!sk1 && !FULL && base + kWave < R.P) round_update(s, r + 1, T, S1, G1, C1);
+        if (!sk0) round_update(s, r, T, S0, G0, C0);
+        if (!sk1 && base + kWave < R.P) round_update(s, r + 1, T, S1, G1, C1);
         count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (sk0 ? 1 : 0) + ((sk1 && base + kWave < R.P) ? 1 : 0));
         count_event(s, FKS_PHASE_ENV_ROUNDS_EVALUATED, (sk0 ? 0 : 1) + ((!sk1 && base + kWave < R.P) ? 1 : 0));
         const uint64_t m0 = __ballot(c0);
@@ -1687,14 +1570,12 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
 template <int RT>
 __device__ bool check_collision(Sim& s, const double* Tp, const double* Tc) {
     uint64_t t0 = tick();
-    bool env = env_collision(s, Tc);
-    for (int k = 1; k < prof_reps(kDupEnv); ++k) env = env_collision(s, Tc);
-    for (int k = 1; k < prof_reps(kDupEnvFull); ++k) env = env_collision<true>(s, Tc) || env;
+    const bool env = env_collision(s, Tc);
     tock(s, FKS_PHASE_ENV_CHECK, t0);
     bool self = false;
     if constexpr (RT == FKS_ROBOT_LINKED) {
         t0 = tick();
-        for (int k = 0; k < prof_reps(kDupSelf); ++k) self = self_collisions(s, Tp, Tc);
+        self = self_collisions(s, Tp, Tc);
         tock(s, FKS_PHASE_SELF_CHECK, t0);
     }
     s.self_nonempty = self;
@@ -1858,7 +1739,7 @@ __device__ __forceinline__ double col_sel(const double (&a)[DM], int k) {
  * with one row per lane), so every long sum is the same canonical reduction and the
  * results equal qr_solve's bit for bit, without touching scratch memory. */
 template <int DM>
-__device__ FKS_QR_ATTR void qr_solve_regs(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
+__device__ __noinline__ void qr_solve_regs(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
                                            uint32_t Rn, double* x) {
     const SimArgs& A = *Ap;
     const int D = A.R.D;
@@ -2464,9 +2345,9 @@ __device__ __forceinline__ void qr_solve_cols_body(const SimArgs* __restrict__ A
  * point (3 rows) runs the 4-row body, same arithmetic (lane_tree_sum<4>) with half the
  * unrolled rows of the 8-row one */
 template <int RM>
-__device__ FKS_QR_ATTR void qr_solve_cols(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
+__device__ __noinline__ void qr_solve_cols(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
                                            uint32_t Rn, double* x, uint32_t row0 = 0) {
-    if (FKS_QR_TILE && Ap->R.D <= 7) {
+    if (Ap->R.D <= 7) {
         /* <= 7 columns: the 8 x 8 tile (qr_solve_tile), same arithmetic */
         const FKS_GLOBAL double* Jm = gp(scratch) + Ap->SL.J + row0;
         const FKS_GLOBAL double* bv = gp(scratch) + Ap->SL.b + row0;
@@ -2697,7 +2578,7 @@ __device__ __noinline__ void individual_jacobians_solve(Sim& s, uint32_t Rn, dou
  * own, so the default stacked-Jacobian kernel does not carry it; the traced kernels
  * (not on the hot path) read the choice at run time. */
 template <int RT, bool TR, bool IND>
-__device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg, bool allow_contacts, bool* out_collided,
+__device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg, bool allow_contacts, bool* out_collided,
                             bool* out_failed, double*& Tcur, double*& Tprev) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
@@ -2790,8 +2671,8 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
             wsync();
         } else {
             if (micro % (uint32_t)(kWave / R.D) == 0u)
-                for (int k = 0; k < prof_reps(kDupRefill); ++k) refill_noise(s, micro, M);
-            for (int k = 0; k < prof_reps(kDupInput); ++k) apply_input<RT>(s, cfg_prev, ustep, cfg, true, micro);
+                refill_noise(s, micro, M);
+            apply_input<RT>(s, cfg_prev, ustep, cfg, true, micro);
         }
         s.err = wave_or(s.err);
         tock(s, FKS_PHASE_MICRO_INPUT, t0);
@@ -2825,12 +2706,12 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
                     apply_input<RT>(s, cfg, ustep, cfg_tmp, true, micro + 1u);
                     pair_err = s.err; /* err_keep is 0 here: errors end the step above */
                     s.err = err_keep;
-                    for (int k = 0; k < prof_reps(kDupFk); ++k) fk_pair(s, cfg, Tcur, cfg_tmp, Ttmp);
+                    fk_pair(s, cfg, Tcur, cfg_tmp, Ttmp);
                     pair_ready = true;
                 }
             }
             if (!pair)
-                for (int k = 0; k < prof_reps(kDupFk); ++k) fk<RT>(s, cfg, Tcur);
+                fk<RT>(s, cfg, Tcur);
         }
         tock(s, FKS_PHASE_MICRO_FK, t0);
         bool in_collision = check_collision<RT>(s, Tprev, Tcur);
@@ -2849,13 +2730,11 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
                 s.resolver_count++;
                 t0 = tick();
                 uint32_t Rn = collect_corrections<RT>(s, Tprev, Tcur, cfg_act);
-                for (int k = 1; k < prof_reps(kDupCorr); ++k) Rn = collect_corrections<RT>(s, Tprev, Tcur, cfg_act);
                 s.lsq_rows += Rn;
                 s.err = wave_or(s.err);
                 tock(s, FKS_PHASE_CORRECTIONS, t0);
                 if (s.err) return 1;
                 t0 = tick();
-                for (int k = 0; k < prof_reps(kDupSolve); ++k)
                 if (IND || (TR && A.individual_jacobians)) {
                     individual_jacobians_solve(s, Rn, x);
                 } else if (Rn <= 8u && R.D < kWave)
@@ -2866,16 +2745,13 @@ __device__ FKS_HOT_ATTR int resolve_step(Sim& s, const double* particle_cfg, dou
                     qr_solve_regs<8>(s.A, s.lds, s.scratch, ln, Rn, x);
                 else if (RT == FKS_ROBOT_LINKED && Rn <= (uint32_t)kWave && R.D <= 16)
                     qr_solve_regs<RT == FKS_ROBOT_LINKED ? 16 : 8>(s.A, s.lds, s.scratch, ln, Rn, x);
-                else if (k == 0) /* factors in place: never repeated */
+                else
                     qr_solve(s.A, s.lds, s.scratch, ln, Rn, x);
                 tock(s, FKS_PHASE_SOLVE, t0);
                 t0 = tick();
-                double est = 0.0;
-                for (int k = 0; k < prof_reps(kDupApply); ++k) {
-                    apply_input<RT>(s, cfg_act, x, cfg_tmp, false, 0);
-                    fk<RT>(s, cfg_tmp, Ttmp);
-                    est = max_point_motion(s, Tcur, Ttmp);
-                }
+                apply_input<RT>(s, cfg_act, x, cfg_tmp, false, 0);
+                fk<RT>(s, cfg_tmp, Ttmp);
+                const double est = max_point_motion(s, Tcur, Ttmp);
                 const double step_fraction = dmax(est / A.allowed_micro, 1.0);
                 if (step_fraction == 1.0 && dabs(scaling) == 1.0) {
                     /* real_correction_step = (x / 1) * 1 == x bit for bit (SPCS:1681-1682): the
@@ -3198,10 +3074,6 @@ __device__ __forceinline__ void kinematics(const SimArgs* __restrict__ args, dou
     }
 }
 
-/* diagnostic build (tools/finish_probe.py): per-particle end and first heavy-carry times */
-#ifndef FKS_FINISH_PROBE
-#define FKS_FINISH_PROBE 0
-#endif
 template <int RT, bool TR, bool IND = false, bool LEAN = false>
 __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ args, double* lds_mem) {
     const SimArgs& A = *args;
@@ -3479,14 +3351,8 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         if (ln == 0) {
             if (ended) {
                 if (A.out_collided) A.out_collided[local] = collided ? 1 : 0;
-#if FKS_FINISH_PROBE
-                /* diagnostic build (tools/finish_probe.py): when the particle ended, and when it
-                 * was first carried as contact-heavy, in 100 MHz s_memrealtime ticks */
-                if (A.out_micro) A.out_micro[local] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-#else
                 if (A.out_micro) A.out_micro[local] = (uint32_t)micro_total;
                 if (A.out_resolver) A.out_resolver[local] = (uint32_t)resolver_total;
-#endif
                 if (A.out_err) A.out_err[local] = s.err;
                 if constexpr (TR) {
                     A.tr_nsteps[local] = s.tr_steps;
@@ -3527,13 +3393,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             if (cont) {
                 carry = (seg + 1) * A.n + local;
                 carry_heavy = cont == 2u;
-#if FKS_FINISH_PROBE
-                if (carry_heavy && ln == 0 && A.out_resolver) {
-                    uint32_t z = 0;
-                    __hip_atomic_compare_exchange_strong(A.out_resolver + local, &z, (uint32_t)__builtin_amdgcn_s_memrealtime(),
-                                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-#endif
             }
         }
         wsync();

@@ -281,13 +281,19 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
                   ctx_.get(), "ForwardSimulateMutableRobot");
         } else {
             /* the trace holds one step record per controller step and every pushed
-             * configuration.  The capacity starts at 16384 configurations; a longer trace is
-             * re-run with the exact size, from the same RNG call index and controller state
-             * (the simulation is deterministic, so the rerun reproduces it) */
+             * configuration.  The capacity starts at TraceCapacityHint() configurations
+             * (16384); a longer trace is re-run with the exact size, from the same RNG call
+             * index and controller state (the simulation is deterministic, so the rerun
+             * reproduces it), and the statistics and call totals the first run added are taken
+             * back, so GetStatistics counts the particle once */
             const uint32_t steps = ForwardSteps();
             const uint64_t call = fks_get_call_index(ctx_.get());
             const std::vector<double> pid0 = pid;
-            uint32_t cap = 16384;
+            fks_statistics stats0{};
+            fks_call_counters totals0{};
+            Check(fks_get_statistics(ctx_.get(), &stats0), ctx_.get(), "fks_get_statistics");
+            Check(fks_get_total_counters(ctx_.get(), &totals0), ctx_.get(), "fks_get_total_counters");
+            uint32_t cap = trace_capacity_hint_;
             for (int attempt = 0;; ++attempt) {
                 std::vector<double> inputs((size_t)steps * 2 * D), configs((size_t)cap * W);
                 std::vector<uint32_t> step_micro(steps), tags((size_t)cap * 3);
@@ -304,6 +310,9 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
                 cap = num_configs;
                 pid = pid0;
                 Check(fks_set_call_index(ctx_.get(), call), ctx_.get(), "fks_set_call_index");
+                Check(fks_set_statistics(ctx_.get(), &stats0), ctx_.get(), "fks_set_statistics");
+                Check(fks_set_total_counters(ctx_.get(), &totals0), ctx_.get(), "fks_set_total_counters");
+                retried_traces_++;
             }
         }
         last_errors_.assign(1, errors);
@@ -329,6 +338,11 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
     const std::vector<uint32_t>& LastMicrosteps() const { return last_micro_; }
     const std::vector<uint32_t>& LastResolverIterations() const { return last_resolver_; }
     fks_context* Context() const { return ctx_.get(); }
+    /* the configuration capacity a traced call starts with (a longer trace is re-run once with
+     * the exact size); RetriedTraces() counts those re-runs */
+    void SetTraceCapacityHint(uint32_t configs) { trace_capacity_hint_ = configs > 0 ? configs : 1; }
+    uint32_t TraceCapacityHint() const { return trace_capacity_hint_; }
+    uint64_t RetriedTraces() const { return retried_traces_; }
 
   private:
     struct Destroy {
@@ -462,6 +476,8 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
     mutable std::shared_ptr<const fks::RobotDescription> robot_key_;
     RNG rng_;
     std::vector<uint32_t> last_errors_, last_micro_, last_resolver_;
+    uint32_t trace_capacity_hint_ = 16384;
+    uint64_t retried_traces_ = 0;
 };
 
 }  // namespace simple_particle_contact_simulator

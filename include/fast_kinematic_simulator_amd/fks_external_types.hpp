@@ -62,6 +62,7 @@ typedef Eigen::VectorXd VectorXd;
 typedef Eigen::Vector3d Vector3d;
 typedef Eigen::Vector4d Vector4d;
 typedef Eigen::Isometry3d Isometry3d;
+typedef Eigen::Quaterniond Quaterniond;
 typedef std_msgs::ColorRGBA ColorRGBA;
 typedef geometry_msgs::Point Point;
 typedef visualization_msgs::Marker Marker;
@@ -76,6 +77,7 @@ typedef fks_standalone::VectorXd VectorXd;
 typedef fks_standalone::Vector3d Vector3d;
 typedef fks_standalone::Vector4d Vector4d;
 typedef fks_standalone::Isometry3d Isometry3d;
+typedef fks_standalone::Quaterniond Quaterniond;
 typedef fks_standalone::ColorRGBA ColorRGBA;
 typedef fks_standalone::Point Point;
 typedef fks_standalone::Marker Marker;

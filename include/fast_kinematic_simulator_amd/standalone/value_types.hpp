@@ -100,6 +100,20 @@ class Isometry3d {
     Matrix4 m_;
 };
 
+/* Eigen::Quaterniond: (w, x, y, z) coefficients, the constructor order of Eigen's */
+class Quaterniond {
+  public:
+    Quaterniond() : w_(1.0), x_(0.0), y_(0.0), z_(0.0) {}
+    Quaterniond(double w, double x, double y, double z) : w_(w), x_(x), y_(y), z_(z) {}
+    double w() const { return w_; }
+    double x() const { return x_; }
+    double y() const { return y_; }
+    double z() const { return z_; }
+
+  private:
+    double w_, x_, y_, z_;
+};
+
 /* Eigen::aligned_allocator: 16-byte aligned storage for fixed-size vectorisable types
  * (the reference stores SE(3) configurations with it, UPC.cpp:131) */
 template <typename T>

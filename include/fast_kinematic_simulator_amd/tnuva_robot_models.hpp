@@ -11,6 +11,14 @@
  * the constructor (HipDescription(), shared by clones and owned through a shared_ptr, so
  * a simulator may keep it as its cache key) and the controller state a mutable robot
  * carries between simulator calls (ResetPosition zeroes it, TNUVA:524-536).
+ * The TnuvaRobot control interface (TNUVA:15-23) steps one robot by hand, as execution
+ * and demonstration code does: GenerateControlAction (the robot's PID controllers and
+ * actuator clamp), ApplyControlInput(u) and ApplyControlInput(u, rng) (the actuators'
+ * truncated-normal noise drawn from the caller's generator, one
+ * std::normal_distribution per actuator as TruncatedNormalDistribution keeps,
+ * UNC:61/77-90), and the virtual ResetControllers.  They run on the host through the
+ * C-ABI (fks_robot_control_action / fks_robot_apply_control_input) with the simulation
+ * kernels' arithmetic.
  */
 #ifndef FAST_KINEMATIC_SIMULATOR_AMD_TNUVA_ROBOT_MODELS_HPP
 #define FAST_KINEMATIC_SIMULATOR_AMD_TNUVA_ROBOT_MODELS_HPP
@@ -19,6 +27,7 @@
 #include <array>
 #include <cmath>
 #include <memory>
+#include <random>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -82,6 +91,8 @@ template <typename Configuration>
 class HipRobotState {
   public:
     virtual ~HipRobotState() {}
+    /* TnuvaRobot (TNUVA:15-23); Generator is the robot class's template argument */
+    virtual const Configuration& ResetPosition(const Configuration& position) = 0;
     const fks::RobotDescription& HipDescription() const { return *desc_; }
     const std::shared_ptr<const fks::RobotDescription>& SharedHipDescription() const { return desc_; }
     const std::vector<double>& ControllerState() const { return pid_; }
@@ -89,6 +100,7 @@ class HipRobotState {
         if (state.size() != pid_.size()) throw std::invalid_argument("controller state has the wrong size");
         pid_ = state;
     }
+    /* TNUVA:145-150, 338-346, 530-536: every controller's integral and last error to zero */
     virtual void ResetControllers() { std::fill(pid_.begin(), pid_.end(), 0.0); }
     bool ControllersAreZero() const {
         for (double v : pid_)
@@ -102,9 +114,51 @@ class HipRobotState {
     void InitState(const std::shared_ptr<const fks::RobotDescription>& desc) {
         desc_ = desc;
         pid_.assign(2 * (size_t)desc->NumDofs(), 0.0);
+        /* TruncatedNormalUncertainVelocityActuator(..., 0.5): TN(0, 0.5) on [-1, 1] (TNUVA:130, 322, 469) */
+        noise_.assign((size_t)desc->NumDofs(), std::normal_distribution<double>(0.0, 1.0));
+    }
+    static void Check(fks_status st, const char* what) {
+        if (st != FKS_OK) throw std::runtime_error(std::string(what) + ": " + fks_status_string(st));
+    }
+    /* GenerateControlAction from the current flat configuration (TNUVA:179-198, 384-412, 598-614) */
+    fks_planner_types::VectorXd ControlAction(const std::vector<double>& current, const std::vector<double>& target,
+                                              double controller_interval) {
+        const fks_robot_desc d = desc_->View();
+        std::vector<double> u((size_t)desc_->NumDofs());
+        Check(fks_robot_control_action(&d, current.data(), target.data(), controller_interval, pid_.data(), u.data()),
+              "GenerateControlAction");
+        return fks_ext::vecx(u);
+    }
+    /* ApplyControlInput: the new flat configuration (TNUVA:152-177, 348-382, 538-596) */
+    std::vector<double> Applied(const std::vector<double>& current, const fks_planner_types::VectorXd& input,
+                                const std::vector<double>* unit_noise) {
+        const std::vector<double> u = fks_ext::vecx_values(input);
+        if (u.size() != (size_t)desc_->NumDofs()) throw std::invalid_argument("ApplyControlInput: one input per dof");
+        const fks_robot_desc d = desc_->View();
+        std::vector<double> out(current.size());
+        Check(fks_robot_apply_control_input(&d, current.data(), u.data(), unit_noise ? unit_noise->data() : nullptr, out.data()),
+              "ApplyControlInput");
+        return out;
+    }
+    /* TruncatedNormalDistribution(0, 0.5, -1, 1) of each actuator, in dof order: the naive
+     * accept-reject of its standardised bounds [-2, 2] over the actuator's own normal draws */
+    template <typename RNG>
+    std::vector<double> DrawNoise(RNG& rng) {
+        std::vector<double> n(noise_.size());
+        for (size_t k = 0; k < noise_.size(); ++k) {
+            for (;;) {
+                const double draw = noise_[k](rng);
+                if ((draw <= 2.0) && (draw >= -2.0)) {
+                    n[k] = 0.0 + 0.5 * draw;
+                    break;
+                }
+            }
+        }
+        return n;
     }
     std::shared_ptr<const fks::RobotDescription> desc_;
     std::vector<double> pid_;
+    std::vector<std::normal_distribution<double>> noise_;
 };
 
 /* ---------------------------------------------------------------- SE(2) (TNUVA:26-199) */
@@ -135,9 +189,20 @@ class TnuvaSE2Robot : public simple_robot_models::PointSphereBasicSE2Robot,
         return new TnuvaSE2Robot(*this);
     }
     /* TNUVA:139-150 */
-    const Configuration& ResetPosition(const Configuration& position) {
+    const Configuration& ResetPosition(const Configuration& position) override {
         this->ResetControllers();
         return SetPosition(position);
+    }
+    /* TnuvaRobot::ApplyControlInput(u), ApplyControlInput(u, rng), GenerateControlAction */
+    void ApplyControlInput(const fks_planner_types::VectorXd& input) {
+        SetPosition(FromFlat(this->Applied(ToFlat(GetPosition()), input, nullptr).data()));
+    }
+    void ApplyControlInput(const fks_planner_types::VectorXd& input, Generator& rng) {
+        const std::vector<double> noise = this->DrawNoise(rng);
+        SetPosition(FromFlat(this->Applied(ToFlat(GetPosition()), input, &noise).data()));
+    }
+    fks_planner_types::VectorXd GenerateControlAction(const Configuration& target, const double controller_interval) {
+        return this->ControlAction(ToFlat(GetPosition()), ToFlat(target), controller_interval);
     }
     std::vector<double> ToFlat(const Configuration& c) const override { return {c(0), c(1), c(2)}; }
     Configuration FromFlat(const double* f) const override { return Configuration(f[0], f[1], f[2]); }
@@ -171,9 +236,21 @@ class TnuvaSE3Robot : public simple_robot_models::PointSphereBasicSE3Robot,
         const override {
         return new TnuvaSE3Robot(*this);
     }
-    const Configuration& ResetPosition(const Configuration& position) {
+    /* TNUVA:332-336 */
+    const Configuration& ResetPosition(const Configuration& position) override {
         this->ResetControllers();
         return SetPosition(position);
+    }
+    /* TnuvaRobot::ApplyControlInput(u), ApplyControlInput(u, rng), GenerateControlAction */
+    void ApplyControlInput(const fks_planner_types::VectorXd& input) {
+        SetPosition(FromFlat(this->Applied(ToFlat(GetPosition()), input, nullptr).data()));
+    }
+    void ApplyControlInput(const fks_planner_types::VectorXd& input, Generator& rng) {
+        const std::vector<double> noise = this->DrawNoise(rng);
+        SetPosition(FromFlat(this->Applied(ToFlat(GetPosition()), input, &noise).data()));
+    }
+    fks_planner_types::VectorXd GenerateControlAction(const Configuration& target, const double controller_interval) {
+        return this->ControlAction(ToFlat(GetPosition()), ToFlat(target), controller_interval);
     }
     /* the 3x4 row-major [R | t] */
     std::vector<double> ToFlat(const Configuration& c) const override {
@@ -261,10 +338,22 @@ class TnuvaLinkedRobot : public simple_robot_models::PointSphereBasicLinkedRobot
         return new TnuvaLinkedRobot(*this);
     }
     /* TNUVA:524-536 */
-    const Configuration& ResetPosition(const Configuration& position) {
+    const Configuration& ResetPosition(const Configuration& position) override {
         this->ResetControllers();
         return SetPosition(position);
     }
+    /* TnuvaRobot::ApplyControlInput(u), ApplyControlInput(u, rng), GenerateControlAction */
+    void ApplyControlInput(const fks_planner_types::VectorXd& input) {
+        SetPosition(FromFlat(this->Applied(ToFlat(GetPosition()), input, nullptr).data()));
+    }
+    void ApplyControlInput(const fks_planner_types::VectorXd& input, Generator& rng) {
+        const std::vector<double> noise = this->DrawNoise(rng);
+        SetPosition(FromFlat(this->Applied(ToFlat(GetPosition()), input, &noise).data()));
+    }
+    fks_planner_types::VectorXd GenerateControlAction(const Configuration& target, const double controller_interval) {
+        return this->ControlAction(ToFlat(GetPosition()), ToFlat(target), controller_interval);
+    }
+
     std::vector<double> ToFlat(const Configuration& c) const override {
         std::vector<double> f;
         for (const auto& j : c) f.push_back(j.GetValue());

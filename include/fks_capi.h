@@ -44,8 +44,11 @@ extern "C" {
 #endif
 
 /* 5: the opt-in joint-space proof (ABI 4: fks_set_joint_proof, fks_call_counters.
- * proven_free_microsteps) removed: it broke even on the headline */
-#define FKS_ABI_VERSION 5
+ * proven_free_microsteps) removed: it broke even on the headline.
+ * 6: host robot control (fks_robot_control_action, fks_robot_apply_control_input), the
+ * environment builder's public steps (fks_env_discretize_obstacle, fks_env_build_normals,
+ * fks_env_cell_objects), fks_set_statistics / fks_set_total_counters */
+#define FKS_ABI_VERSION 6
 
 typedef enum {
     FKS_OK = 0,
@@ -374,6 +377,8 @@ uint64_t fks_get_call_index(const fks_context* ctx);
 
 fks_status fks_get_statistics(const fks_context* ctx, fks_statistics* out);
 fks_status fks_reset_statistics(fks_context* ctx);
+/* overwrite the statistics (a caller that re-runs a call restores what it read before) */
+fks_status fks_set_statistics(fks_context* ctx, const fks_statistics* stats);
 fks_status fks_reset_generators(fks_context* ctx, uint64_t prng_seed);
 int32_t fks_get_debug_level(const fks_context* ctx);
 int32_t fks_set_debug_level(fks_context* ctx, int32_t debug_level);
@@ -440,6 +445,23 @@ fks_status fks_set_individual_jacobians(fks_context* ctx, int32_t simulate_with_
 /* sums over every call since fks_create / fks_reset_total_counters */
 fks_status fks_get_total_counters(const fks_context* ctx, fks_call_counters* out);
 fks_status fks_reset_total_counters(fks_context* ctx);
+fks_status fks_set_total_counters(fks_context* ctx, const fks_call_counters* totals);
+
+/* One robot stepped by hand on the host (the TnuvaRobot control interface, TNUVA:15-23), the
+ * same arithmetic as the simulation kernels:
+ *   fks_robot_control_action       -> GenerateControlAction(target, controller_interval)
+ *                                     (TNUVA:179-198, 384-412, 598-614); pid_state: the robot's
+ *                                     controllers, 2 * num_dofs doubles (error integrals, then
+ *                                     last errors), updated in place; out_control: num_dofs
+ *   fks_robot_apply_control_input  -> ApplyControlInput(u) (TNUVA:152-163, 348-364, 538-566)
+ *                                     with unit_noise NULL; ApplyControlInput(u, rng)
+ *                                     (TNUVA:165-177, 366-382, 568-596) with one truncated-normal
+ *                                     TN(0, 0.5) on [-1, 1] sample per dof drawn by the caller
+ *                                     (UNC:77-90); out_config: the robot's config width */
+fks_status fks_robot_control_action(const fks_robot_desc* robot, const double* config, const double* target,
+                                    double controller_interval, double* pid_state, double* out_control);
+fks_status fks_robot_apply_control_input(const fks_robot_desc* robot, const double* config, const double* input,
+                                         const double* unit_noise, double* out_config);
 
 /* ---- environment preprocessing (CPU; reference SEB.cpp:21-476) ---- */
 /* OBSTACLE_CONFIG (SEB.hpp): pose as 3x4 row-major, half extents, object id > 0 */
@@ -489,6 +511,19 @@ void fks_device_env_free(fks_device_env* env);
 fks_status fks_create_from_device_env(const fks_device_env* env, const fks_solver_params* params,
                                       double simulation_controller_frequency, uint64_t prng_seed,
                                       int32_t debug_level, fks_context** out_ctx);
+/* DiscretizeObstacle (SEB.cpp:21-46): *count = the obstacle's half-resolution samples; with
+ * out_xyz (capacity >= *count triples) their world positions, x then y then z */
+fks_status fks_env_discretize_obstacle(const fks_obstacle* obstacle, double resolution, double* out_xyz, uint64_t capacity,
+                                       uint64_t* count);
+/* BuildSurfaceNormalsGrid (SEB.cpp:258-468) on the caller's SDF (VoxelGrid order over
+ * sdf_geometry, e.g. sdf_tools' ExtractSignedDistanceField result, SEB.cpp:473-475): a handle
+ * with only the surface-normal CSR over that geometry (fks_env_view: sdf_values NULL) */
+fks_status fks_env_build_normals(const fks_obstacle* obstacles, int32_t num_obstacles, const fks_grid_geometry* sdf_geometry,
+                                 const float* sdf_values, fks_env_handle** out);
+/* the object id of each cell of an fks_env_build collision map (BuildEnvironment's
+ * SetValue(1.0, object_id) in obstacle order, the last write wins, SEB.cpp:151-155; 0 = free) */
+fks_status fks_env_cell_objects(const fks_env_handle* env, uint32_t* out, uint64_t num_cells);
+
 /* Fill a view whose pointers stay valid until fks_env_free. */
 fks_status fks_env_view(const fks_env_handle* env, fks_environment* out);
 /* The collision grid (1 = filled cell), z-fastest, num_cells = nx * ny * nz. */

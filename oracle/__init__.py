@@ -30,8 +30,7 @@ def build(force: bool = False) -> str:
 def lib():
     global _LIB
     if _LIB is None:
-        if not os.path.exists(LIB_PATH):
-            build()
+        build()  # make: a no-op when liboracle.so is newer than its sources
         _LIB = _load(LIB_PATH)
     return _LIB
 
@@ -46,8 +45,7 @@ def audit_variant(name):
     global _LIB
     assert name in AUDIT_VARIANTS, name
     path = os.path.join(HERE, "_build", "liboracle_%s.so" % name)
-    if not os.path.exists(path):
-        subprocess.run(["make", "-C", HERE, "audit"], check=True, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    subprocess.run(["make", "-C", HERE, "audit"], check=True, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     saved = lib()
     _LIB = _load(path)
     try:
@@ -100,6 +98,9 @@ def _load(path):
     L.oracle_link_transforms.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), POINTER(c_double)]
     L.oracle_apply_control_input.restype = c_int32
     L.oracle_apply_control_input.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), POINTER(c_double), POINTER(c_double)]
+    L.oracle_robot_steps.restype = c_int32
+    L.oracle_robot_steps.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), POINTER(c_double), c_double, c_uint32, c_uint64,
+                                     c_uint64, POINTER(c_double), POINTER(c_double), POINTER(c_double)]
     L.oracle_point_jacobian.restype = c_int32
     L.oracle_point_jacobian.argtypes = [POINTER(C.RobotDesc), POINTER(c_double), c_int32, POINTER(c_double), POINTER(c_double)]
     L.oracle_se3_exp.restype = None
@@ -308,6 +309,25 @@ def apply_control_input(robot, config, control_input):
     out = np.zeros(robot.config_width)
     lib().oracle_apply_control_input(ctypes.byref(desc), _p(cfg, c_double), _p(u, c_double), _p(out, c_double))
     return out
+
+
+def robot_steps(robot, start, target, controller_interval, steps, seed, noisy_mask=0):
+    """One robot stepped by hand: GenerateControlAction + ApplyControlInput per step (noisy on
+    the steps set in noisy_mask, std::mt19937_64(seed)).  Returns (controls, configs, pid)."""
+    desc, keep = robot.to_c()
+    W, D = robot.config_width, robot.num_dofs
+    s = np.ascontiguousarray(start, dtype=np.float64)
+    t = np.ascontiguousarray(target, dtype=np.float64)
+    u = np.zeros((steps, D))
+    q = np.zeros((steps, W))
+    pid = np.zeros(2 * D)
+    st = lib().oracle_robot_steps(ctypes.byref(desc), _p(s, c_double), _p(t, c_double), float(controller_interval), int(steps),
+                                  c_uint64(int(seed)), c_uint64(int(noisy_mask)), _p(u, c_double), _p(q, c_double),
+                                  _p(pid, c_double))
+    del keep
+    if st != 0:
+        raise RuntimeError(f"oracle_robot_steps failed ({st})")
+    return u, q, pid
 
 
 def point_jacobian(robot, config, geometry, point):

@@ -1277,6 +1277,36 @@ int oracle_apply_control_input(const fks_robot_desc* robot_desc, const double* c
     return 0;
 }
 
+/* One robot stepped by hand (the TnuvaRobot interface, TNUVA:15-23): ResetPosition(start),
+ * then per step u = GenerateControlAction(target, controller_interval) and ApplyControlInput(u)
+ * (clean) or, on the steps whose bit is set in noisy_mask, ApplyControlInput(u, rng) with one
+ * std::mt19937_64(seed) as the generator (reference mode: each actuator's own
+ * std::normal_distribution).  out_controls: steps x D, out_configs: steps x W, out_pid: 2D. */
+int oracle_robot_steps(const fks_robot_desc* robot_desc, const double* start, const double* target, double controller_interval,
+                       uint32_t steps, uint64_t seed, uint64_t noisy_mask, double* out_controls, double* out_configs,
+                       double* out_pid) {
+    std::unique_ptr<RobotModel> robot(make_robot(*robot_desc));
+    if (!robot) return 1;
+    const size_t W = config_width(*robot_desc), D = robot->NumDofs();
+    robot->ResetPosition(Config(start, start + W));
+    const Config tgt(target, target + W);
+    std::mt19937_64 mt(seed);
+    uint32_t err = 0;
+    NoiseContext ctx{RNG_REFERENCE, 0, 0, 0, 0, 0, &mt, &err};
+    for (uint32_t k = 0; k < steps; ++k) {
+        const std::vector<double> u = robot->GenerateControlAction(tgt, controller_interval);
+        for (size_t d = 0; d < D; ++d) out_controls[k * D + d] = u[d];
+        if (k < 64 && ((noisy_mask >> k) & 1ull))
+            robot->ApplyControlInput(u, ctx);
+        else
+            robot->ApplyControlInput(u);
+        const Config& q = robot->GetPosition();
+        std::memcpy(out_configs + k * W, q.data(), W * sizeof(double));
+    }
+    robot->GetControllerState(out_pid);
+    return err ? 2 : 0;
+}
+
 /* point Jacobian (3 x D row-major) of point p (4 doubles) on geometry g */
 int oracle_point_jacobian(const fks_robot_desc* robot_desc, const double* config, int32_t geometry, const double* p, double* out) {
     std::unique_ptr<RobotModel> robot(make_robot(*robot_desc));

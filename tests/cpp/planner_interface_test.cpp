@@ -3,7 +3,7 @@
  * std::shared_ptr<simple_simulator_interface::SimulatorInterface<...>> as the
  * reference's planner does (FKS.hpp:18-22 factories, SPCS:446-1416 virtuals).
  *
- *   planner_interface_test <scene file>
+ *   planner_interface_test <scene file> [--dump | --normals-out <file>]
  *
  * The scene (written by tests/test_planner_interface.py) gives the robot's constructor
  * arguments (TnuvaLinkedRobot TNUVA:486-517, TnuvaSE2Robot 109-132, TnuvaSE3Robot
@@ -13,8 +13,11 @@
  */
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
+#include <cmath>
 #include <iostream>
+#include <map>
 #include <memory>
 #include <sstream>
 #include <string>
@@ -77,6 +80,7 @@ struct Scene {
     bool allow = true;
     fast_kinematic_simulator::SolverParameters solver;
     std::unique_ptr<simulator_environment_builder::EnvironmentComponents> env;
+    std::vector<simulator_environment_builder::OBSTACLE_CONFIG> obstacles;
 };
 
 static Scene read_common(Reader& r) {
@@ -104,7 +108,7 @@ static Scene read_common(Reader& r) {
     const std::vector<double> origin = r.nums(12);
     const int64_t cells[3] = {r.integer(), r.integer(), r.integer()};
     const int64_t nobs = r.integer();
-    std::vector<simulator_environment_builder::OBSTACLE_CONFIG> obstacles;
+    std::vector<simulator_environment_builder::OBSTACLE_CONFIG>& obstacles = s.obstacles;
     for (int64_t k = 0; k < nobs; ++k) {
         const Isometry3d pose = r.iso();
         const Vector3d ext = r.vec3();
@@ -124,6 +128,51 @@ static simple_robot_models::PointSphereGeometry read_points(Reader& r) {
 
 /* --dump: the flattened robot the GPU receives and the flat starts / targets (no GPU needed) */
 static bool g_dump = false;
+
+/* FNV-1a of a byte range (environment fingerprints in --dump) */
+static uint64_t fnv(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+
+/* --dump, environment side (no GPU): the builder's public steps on the scene's obstacles */
+static void dump_environment(const Scene& s, const std::vector<simulator_environment_builder::OBSTACLE_CONFIG>& obstacles) {
+    namespace seb = simulator_environment_builder;
+    const auto& E = *s.env;
+    const auto& N = E.GetSurfaceNormalsGrid();
+    const uint64_t cells = (uint64_t)N.GetNumXCells() * (uint64_t)N.GetNumYCells() * (uint64_t)N.GetNumZCells();
+    const uint32_t* off = N.CsrOffsets();
+    std::printf("env_normals %u %llx %llx\n", off[cells], (unsigned long long)fnv(off, 4 * (size_t)(cells + 1)),
+                (unsigned long long)(off[cells] ? fnv(N.CsrEntries(), 48 * (size_t)off[cells]) : 0ull));
+    /* BuildSurfaceNormalsGrid on the complete environment's SDF gives the same grid */
+    const auto again = seb::BuildSurfaceNormalsGrid(obstacles, E.GetEnvironmentSDF());
+    const uint32_t* off2 = again.CsrOffsets();
+    std::printf("env_normals_again %u %llx %llx\n", off2[cells], (unsigned long long)fnv(off2, 4 * (size_t)(cells + 1)),
+                (unsigned long long)(off2[cells] ? fnv(again.CsrEntries(), 48 * (size_t)off2[cells]) : 0ull));
+    /* object ids of the collision map (SEB.cpp:151-155) */
+    std::map<uint32_t, uint64_t> ids;
+    const auto& G = E.GetEnvironment();
+    for (int64_t x = 0; x < G.GetNumXCells(); ++x)
+        for (int64_t y = 0; y < G.GetNumYCells(); ++y)
+            for (int64_t z = 0; z < G.GetNumZCells(); ++z) {
+                const auto c = G.GetImmutable(x, y, z).first;
+                if (c.occupancy > 0.5f) ids[c.object_id]++;
+            }
+    std::printf("env_ids");
+    for (const auto& kv : ids) std::printf(" %u:%llu", kv.first, (unsigned long long)kv.second);
+    std::printf("\n");
+    /* DiscretizeObstacle of the first obstacle, and OBSTACLE_CONFIG's quaternion constructor */
+    const auto d = seb::DiscretizeObstacle(obstacles.front(), G.GetResolution());
+    std::printf("env_discretize %zu %a %a %a %u\n", d.size(), d.front().first(0), d.front().first(1), d.front().first(2),
+                d.front().second.object_id);
+    const double h = 0.5 * std::sqrt(2.0);
+    const seb::OBSTACLE_CONFIG q(7u, Vector3d(0.1, 0.2, 0.3), fks_planner_types::Quaterniond(h, 0.0, 0.0, h), Vector3d(0.1, 0.2, 0.3));
+    std::printf("env_quat");
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 4; ++c) hex(q.pose.matrix()(r, c));
+    std::printf("\n");
+}
 template <typename Configs, typename Robot>
 static int dump(const Robot& robot, const Configs& starts, const Configs& targets) {
     const fks::RobotDescription& d = robot.HipDescription();
@@ -163,6 +212,83 @@ static int dump(const Robot& robot, const Configs& starts, const Configs& target
     return 0;
 }
 
+/* one robot stepped by hand through the TnuvaRobot interface (TNUVA:15-23), as execution
+ * code does: GenerateControlAction, then ApplyControlInput(u) on even steps and
+ * ApplyControlInput(u, rng) on odd ones (std::mt19937_64(seed + 77)); prints every control
+ * and configuration, then the controllers' state */
+template <typename Robot, typename Config>
+static void step_by_hand(const Scene& s, const Robot& prototype, const Config& start, const Config& target) {
+    std::unique_ptr<Robot> robot(static_cast<Robot*>(prototype.Clone()));
+    robot->ResetPosition(start);
+    upc::PRNG rng(s.seed + 77);
+    for (int k = 0; k < 12; ++k) {
+        const auto u = robot->GenerateControlAction(target, 1.0 / s.frequency);
+        std::printf("hand_u %d", k);
+        for (int64_t d = 0; d < (int64_t)u.size(); ++d) hex(u(d));
+        std::printf("\n");
+        if (k % 2 == 0)
+            robot->ApplyControlInput(u);
+        else
+            robot->ApplyControlInput(u, rng);
+        std::printf("hand_q %d", k);
+        for (double v : robot->ToFlat(robot->GetPosition())) hex(v);
+        std::printf("\n");
+    }
+    std::printf("hand_pid");
+    for (double v : robot->ControllerState()) hex(v);
+    std::printf("\n");
+    robot->ResetControllers();
+    std::printf("hand_reset %d\n", robot->ControllersAreZero() ? 1 : 0);
+}
+
+/* a surface-normal grid made through the SurfaceNormalGrid API (SPCS:138-343) and the
+ * builder's public steps (SEB.hpp:61-70): the built grid's entries re-inserted cell by cell
+ * with InsertSurfaceNormal, then AdjustSurfaceNormalGridForAllFlatSurfaces and one
+ * UpdateSurfaceNormalGridCell; its CSR is written to `path` (offsets then entries, raw) for
+ * the oracle, and a simulator made over it runs the batch (fresh simulator, call index 0) */
+template <typename Robot, typename Configs>
+static void custom_normals(const Scene& s, const std::shared_ptr<Robot>& robot, const Configs& starts, const Configs& targets,
+                           const char* path) {
+    namespace seb = simulator_environment_builder;
+    const auto& E = *s.env;
+    const simple_particle_contact_simulator::SurfaceNormalGrid& built = E.GetSurfaceNormalsGrid();
+    const double res = built.GetResolution();
+    simple_particle_contact_simulator::SurfaceNormalGrid grid(built.GetOriginTransform(), res, ((double)built.GetNumXCells() - 0.5) * res,
+                                                              ((double)built.GetNumYCells() - 0.5) * res,
+                                                              ((double)built.GetNumZCells() - 0.5) * res);
+    std::printf("custom_init %d %d\n", simple_particle_contact_simulator::SurfaceNormalGrid().IsInitialized() ? 1 : 0,
+                grid.IsInitialized() ? 1 : 0);
+    size_t inserted = 0;
+    for (int64_t x = 0; x < built.GetNumXCells(); ++x)
+        for (int64_t y = 0; y < built.GetNumYCells(); ++y)
+            for (int64_t z = 0; z < built.GetNumZCells(); ++z)
+                for (const auto& e : built.GetCellEntries(x, y, z)) {
+                    grid.InsertSurfaceNormal(x, y, z, e.second, Vector3d(e.first(0), e.first(1), e.first(2)));
+                    inserted++;
+                }
+    seb::AdjustSurfaceNormalGridForAllFlatSurfaces(E.GetEnvironmentSDF(), grid);
+    const Vector3d probe(0.3, 0.02, 0.5);
+    seb::UpdateSurfaceNormalGridCell({seb::RawCellSurfaceNormal(Vector3d(0.0, 0.0, 1.0), Vector3d(0.0, 0.0, -1.0))},
+                                     fks_planner_types::Isometry3d::Identity(), probe, E.GetEnvironmentSDF(), grid);
+    const auto look = grid.LookupSurfaceNormal(probe, Vector3d(0.0, 0.0, -1.0));
+    std::printf("custom_lookup %d %a %a %a %zu\n", look.second ? 1 : 0, look.first(0), look.first(1), look.first(2), inserted);
+    const uint64_t cells = (uint64_t)grid.GetNumXCells() * (uint64_t)grid.GetNumYCells() * (uint64_t)grid.GetNumZCells();
+    const uint32_t* off = grid.CsrOffsets();
+    FILE* f = std::fopen(path, "wb");
+    if (!f) throw std::runtime_error("cannot write the normals file");
+    std::fwrite(off, sizeof(uint32_t), (size_t)cells + 1, f);
+    if (off[cells]) std::fwrite(grid.CsrEntries(), sizeof(double), 6 * (size_t)off[cells], f);
+    std::fclose(f);
+    upc::LinkedSimulatorPtr sim = fast_kinematic_simulator::MakeLinkedSimulator(E.GetEnvironment(), E.GetEnvironmentSDF(), grid, s.solver,
+                                                                                s.frequency, s.seed, 0);
+    const auto res_c = sim->ForwardSimulateRobots(robot, starts, targets, s.allow, {});
+    for (size_t i = 0; i < res_c.size(); ++i) {
+        std::printf("custom %zu", i);
+        for (double v : robot->ToFlat(res_c[i].result_config)) hex(v);
+        std::printf(" %d\n", res_c[i].did_contact ? 1 : 0);
+    }
+}
+
 /* the interface calls every family goes through; `to_flat` prints a configuration */
 template <typename Config, typename Alloc, typename Robot>
 static int exercise(const Scene& s, const std::shared_ptr<simple_simulator_interface::SimulatorInterface<Config, upc::PRNG, Alloc>>& sim,
@@ -182,10 +308,18 @@ static int exercise(const Scene& s, const std::shared_ptr<simple_simulator_inter
     /* call index 1: ReverseSimulateRobots (SPCS:806) */
     const auto rev = sim->ReverseSimulateRobots(base, starts, targets, s.allow, {});
     for (size_t i = 0; i < rev.size(); ++i) print("rev", i, rev[i]);
-    /* call index 2: ForwardSimulateRobot with tracing (SPCS:824) of particle 0 */
+    /* call index 2: ForwardSimulateRobot with tracing (SPCS:824) of particle 0, started with a
+     * trace capacity of 8 configurations so the longer trace is re-run at its exact size; the
+     * statistics must count the particle once (reset before, printed after) */
     typename Interface::ForwardSimulationStepTrace trace;
+    auto* hip = dynamic_cast<simple_particle_contact_simulator::HipParticleContactSimulator<Robot, Config, upc::PRNG, Alloc>*>(sim.get());
+    if (!hip) throw std::runtime_error("the factory did not return the HIP simulator");
+    hip->SetTraceCapacityHint(8);
+    sim->ResetStatistics();
     const auto tr = sim->ForwardSimulateRobot(base, starts[0], targets[0], s.allow, trace, true, {});
     print("traced", 0, tr);
+    std::printf("traced_retries %llu\n", (unsigned long long)hip->RetriedTraces());
+    for (const auto& kv : sim->GetStatistics()) std::printf("stat_traced %s %.0f\n", kv.first.c_str(), kv.second);
     size_t configs = 0;
     for (const auto& rs : trace.resolver_steps)
         for (const auto& c : rs.contact_resolver_steps) configs += c.contact_resolution_steps.size();
@@ -222,6 +356,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     g_dump = argc > 2 && std::string(argv[2]) == "--dump";
+    const char* normals_out = (argc > 3 && std::string(argv[2]) == "--normals-out") ? argv[3] : nullptr;
     try {
         Reader r(argv[1]);
         const Scene s = read_common(r);
@@ -280,11 +415,16 @@ int main(int argc, char** argv) {
             };
             const auto starts = read_configs("starts");
             const auto targets = read_configs("targets");
-            if (g_dump) return dump(*robot, starts, targets);
+            if (g_dump) {
+                dump_environment(s, s.obstacles);
+                return dump(*robot, starts, targets);
+            }
             upc::LinkedSimulatorPtr sim = fast_kinematic_simulator::MakeLinkedSimulator(
                 E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
             const int rc = exercise<upc::LinkedConfig, upc::LinkedConfigAlloc>(s, sim, robot, starts, targets);
             if (rc != 0) return rc;
+            step_by_hand(s, *robot, starts[0], targets[0]);
+            if (normals_out) custom_normals(s, robot, starts, targets, normals_out);
             /* Two robots alternating on one simulator, each destroyed before the next is made
              * (call indices 5-8): "other" keeps only the first point of every geometry, "same"
              * is rebuilt from the scene's arguments and must reproduce the oracle's run of the
@@ -341,7 +481,9 @@ int main(int argc, char** argv) {
             if (g_dump) return dump(*robot, starts, targets);
             upc::SE2SimulatorPtr sim = fast_kinematic_simulator::MakeSE2Simulator(
                 E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
-            return exercise<upc::SE2Config, upc::SE2ConfigAlloc>(s, sim, robot, starts, targets);
+            const int rc = exercise<upc::SE2Config, upc::SE2ConfigAlloc>(s, sim, robot, starts, targets);
+            if (rc == 0) step_by_hand(s, *robot, starts[0], targets[0]);
+            return rc;
         }
         typedef tnuva_robot_models::TnuvaSE3Robot<upc::PRNG> Robot;
         auto robot = std::make_shared<Robot>(upc::SE3Config::Identity(), pw, rw, "body", geometry, cfg);
@@ -360,7 +502,9 @@ int main(int argc, char** argv) {
         if (g_dump) return dump(*robot, starts, targets);
         upc::SE3SimulatorPtr sim = fast_kinematic_simulator::MakeSE3Simulator(
             E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
-        return exercise<upc::SE3Config, upc::SE3ConfigAlloc>(s, sim, robot, starts, targets);
+        const int rc = exercise<upc::SE3Config, upc::SE3ConfigAlloc>(s, sim, robot, starts, targets);
+        if (rc == 0) step_by_hand(s, *robot, starts[0], targets[0]);
+        return rc;
     } catch (const fks::SimulatorError& e) {
         std::fprintf(stderr, "%s\n", e.what());
         return e.status() == FKS_ERR_NO_DEVICE ? 3 : 1;

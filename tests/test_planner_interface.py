@@ -10,7 +10,11 @@ constructors and the environment with BuildCompleteEnvironment, and calls:
   ForwardSimulateRobot with tracing for particle 0 (2), CheckConfigCollision of every
   reached configuration, ForwardSimulateMutableRobot (3) then ReverseSimulateMutableRobot
   (4) on one robot that keeps its controllers, Get3dPointForConfig and
-  MakeConfigurationDisplayRep.
+  MakeConfigurationDisplayRep; then it steps one robot by hand through the TnuvaRobot
+  interface (GenerateControlAction, ApplyControlInput with and without the generator) and,
+  for the linked scene, builds a surface-normal grid through the SurfaceNormalGrid API
+  (InsertSurfaceNormal, AdjustSurfaceNormalGridForAllFlatSurfaces, UpdateSurfaceNormalGridCell)
+  and runs a simulator made over it.
 Every number comes back as a hex float and is compared with the oracle bit for bit."""
 import os
 import subprocess
@@ -96,13 +100,18 @@ def _hexrow(row):
     return np.array([float.fromhex(v) for v in row])
 
 
-def _run(name, workspace=False):
+def _run(name, workspace=False, normals=False):
+    """Run the planner program on a scene; with normals=True (linked) it also builds a
+    surface-normal grid through the SurfaceNormalGrid API and returns its CSR as p.normals."""
     family, wl, obstacles, grid = _scene(name)
     exe = build_planner_test(workspace=workspace)
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "scene.txt")
         _write_scene(path, family, wl, obstacles, grid)
-        p = subprocess.run([exe, path], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600)
+        out = os.path.join(d, "normals.bin")
+        p = subprocess.run([exe, path] + (["--normals-out", out] if normals else []), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           text=True, timeout=600)
+        p.normals = open(out, "rb").read() if normals and os.path.exists(out) else None
     return p, family, wl, obstacles, grid
 
 
@@ -169,7 +178,7 @@ def test_planner_program_builds_and_reads_scene(workspace):
 def test_planner_interface_matches_oracle(fks_lib, oracle_lib, name, workspace):
     import oracle
 
-    p, family, wl, obstacles, (res, origin, cells) = _run(name, workspace)
+    p, family, wl, obstacles, (res, origin, cells) = _run(name, workspace, normals=(name == "linked"))
     assert p.returncode == 0, p.stderr
     rows = _parse(p.stdout)
     env = build_complete_environment(obstacles, res, origin=origin, num_cells=cells)
@@ -197,6 +206,11 @@ def test_planner_interface_matches_oracle(fks_lib, oracle_lib, name, workspace):
     t = rows["trace"][0]
     assert (int(t[0]), int(t[1])) == (len(tr.resolver_steps), nconf)
     assert np.array_equal(_hexrow(t[2:]), tr.resolver_steps[0].control_input)
+    # the trace outgrew its starting capacity of 8 configurations and was re-run at its exact
+    # size; GetStatistics (reset before the call) counts the particle once
+    assert rows["traced_retries"][0] == ["1"]
+    once = run(wl.starts[:1], wl.targets[:1], 2)
+    assert {r[0]: float(r[1]) for r in rows["stat_traced"]} == once["statistics"]
     # CheckConfigCollision of the reached configurations
     fwd = run(wl.starts, wl.targets, 0)
     c = oracle.check_config_collision(env, wl.robot, wl.solver, fwd["positions"], 0.5)
@@ -213,7 +227,32 @@ def test_planner_interface_matches_oracle(fks_lib, oracle_lib, name, workspace):
     # display helpers
     mk = rows["markers"][0]
     assert int(mk[0]) == 1 and int(mk[1]) == wl.robot.num_points and mk[2] == "uncertainty_planning_simulator"
+    # one robot stepped by hand (TnuvaRobot interface, TNUVA:15-23): GenerateControlAction, then
+    # ApplyControlInput(u) on even steps and ApplyControlInput(u, rng) on odd ones
+    u_o, q_o, pid_o = oracle.robot_steps(wl.robot, wl.starts[0], wl.targets[0], 1.0 / wl.controller_frequency, 12, wl.seed + 77,
+                                         noisy_mask=sum(1 << k for k in range(1, 12, 2)))
+    assert np.array_equal(np.array([_hexrow(r[1:]) for r in rows["hand_u"]]), u_o)
+    assert np.array_equal(np.array([_hexrow(r[1:]) for r in rows["hand_q"]]), q_o)
+    assert np.array_equal(_hexrow(rows["hand_pid"][0]), pid_o) and np.any(pid_o != 0.0)
+    assert rows["hand_reset"][0] == ["1"]
     if family == "linked":
+        # a normal grid made through InsertSurfaceNormal / AdjustSurfaceNormalGridForAllFlatSurfaces /
+        # UpdateSurfaceNormalGridCell: the simulator over it equals the oracle over the same CSR
+        assert rows["custom_init"][0] == ["0", "1"]
+        assert rows["custom_lookup"][0][0] == "1" and int(rows["custom_lookup"][0][4]) > 0
+        ncell = len(env.normal_offsets) - 1
+        raw = p.normals
+        off = np.frombuffer(raw[:4 * (ncell + 1)], dtype=np.uint32)
+        ent = np.frombuffer(raw[4 * (ncell + 1):], dtype=np.float64)
+        assert len(ent) == 6 * int(off[-1])
+        assert not (np.array_equal(off, env.normal_offsets) and np.array_equal(ent, env.normal_entries))  # really a different grid
+        from fast_kinematic_simulator_amd.environment import SimulatorEnvironment
+        custom = SimulatorEnvironment(env.geometry, env.sdf, off, ent, env.oob_value)
+        oc = oracle.forward_simulate(custom, wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts, wl.targets,
+                                     wl.allow_contacts, call_index=0)
+        got = np.array([_hexrow(r[1:1 + W_]) for r in rows["custom"]])
+        assert np.array_equal(got, oc["positions"])
+        assert [int(r[1 + W_]) for r in rows["custom"]] == [int(v) for v in oc["collided"]]
         # two robots alternating on one simulator, each destroyed before the next is made
         # (planner_interface_test.cpp, call indices 5-8): the rebuilt scene robot reproduces
         # the oracle bit for bit every time, and the one-point robot really was simulated
@@ -254,3 +293,35 @@ def test_standalone_types_collide_with_a_workspace():
         assert ok.returncode == 0, ok.stdout[-3000:]
         bad = subprocess.run(base + ["-DFKS_STANDALONE_PLANNER_TYPES"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         assert bad.returncode != 0 and "redefinition" in bad.stdout
+
+
+@pytest.mark.parametrize("workspace", [False, True], ids=["standalone", "workspace"])
+def test_environment_builder_public_api(workspace):
+    """The builder's public steps (SEB.hpp:39-70) through the planner-side headers, no GPU:
+    BuildSurfaceNormalsGrid on the complete environment's SDF reproduces its normals (in the
+    workspace build that SDF is sdf_tools' own ExtractSignedDistanceField result, SEB.cpp:473-475,
+    and the grids agree with the stand-in build's byte for byte); the collision map carries each
+    obstacle's object id (SEB.cpp:151-155); DiscretizeObstacle gives the half-resolution lattice
+    (SEB.cpp:21-46); OBSTACLE_CONFIG's quaternion constructor is Eigen's toRotationMatrix."""
+    family, wl, obstacles, (res, origin, cells) = _scene("linked")
+    rows = {line.split()[0]: line.split()[1:] for line in _dump("linked", workspace).splitlines()}
+    assert rows["env_normals"] == rows["env_normals_again"] and int(rows["env_normals"][0]) > 0
+    ids = dict(kv.split(":") for kv in rows["env_ids"])
+    assert set(ids) == {str(o.object_id) for o in obstacles} and all(int(v) > 0 for v in ids.values())
+    ext = np.asarray(obstacles[0].extents, dtype=np.float64)
+    nc = [int(e * 2.0 * (1.0 / (res * 0.5))) for e in ext]
+    d = rows["env_discretize"]
+    assert int(d[0]) == nc[0] * nc[1] * nc[2] and d[4] == str(obstacles[0].object_id)
+    pose = np.asarray(obstacles[0].pose, dtype=np.float64).reshape(3, 4)
+    local = np.array([-(ext[a] - res * 0.5) for a in range(3)])
+    first = np.array([(pose[i, 0] * local[0] + pose[i, 1] * local[1]) + pose[i, 2] * local[2] + pose[i, 3] for i in range(3)])
+    assert np.array_equal(_hexrow(d[1:4]), first)
+    h = 0.5 * np.sqrt(2.0)
+    w, x, y, z = h, 0.0, 0.0, h
+    tx, ty, tz = 2.0 * x, 2.0 * y, 2.0 * z
+    twx, twy, twz, txx, txy, txz, tyy, tyz, tzz = tx * w, ty * w, tz * w, tx * x, ty * x, tz * x, ty * y, tz * y, tz * z
+    R = [[1.0 - (tyy + tzz), txy - twz, txz + twy], [txy + twz, 1.0 - (txx + tzz), tyz - twx], [txz - twy, tyz + twx, 1.0 - (txx + tyy)]]
+    want = [R[r][c] if c < 3 else (0.1, 0.2, 0.3)[r] for r in range(3) for c in range(4)]
+    assert np.array_equal(_hexrow(rows["env_quat"]), np.array(want))
+    other = {line.split()[0]: line.split()[1:] for line in _dump("linked", not workspace).splitlines()}
+    assert all(rows[k] == other[k] for k in rows if k.startswith("env_"))
