@@ -518,10 +518,21 @@ static fks_status launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
         *wpg = w;
         *bytes = b;
         if (b > 160 * 1024) return 0;
-        int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kernel_for(R.type, false, l.lean != 0)),
-                                                         64 * (int)w, b) != hipSuccess)
-            return 0;
+        /* every kernel launched with this layout (plain, individual-Jacobian and traced
+         * simulation, configuration check, kinematics) must hold that many groups: the
+         * smallest occupancy of them all */
+        const bool lean_l = l.lean != 0;
+        const sim_kernel_t kernels[] = {kernel_for(R.type, false, lean_l), kernel_for(R.type, true, lean_l),
+                                        traced_kernel_for(R.type, lean_l), check_kernel_for(R.type),
+                                        R.type == FKS_ROBOT_SE2 ? fks_kinematics_se2
+                                                                : (R.type == FKS_ROBOT_SE3 ? fks_kinematics_se3 : fks_kinematics_linked)};
+        int n = 1 << 30;
+        for (sim_kernel_t k : kernels) {
+            int nk = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nk, reinterpret_cast<const void*>(k), 64 * (int)w, b) != hipSuccess)
+                return 0;
+            n = std::min(n, nk);
+        }
         return n * (int)w; /* resident waves per CU */
     };
     uint32_t wpg = 0;

@@ -12,6 +12,8 @@
 #   ab:<wl>:<libs>     interleaved bench.py of comma-separated libraries (each may carry +flag;
 #                      "L" = the product library) on workload <wl>  -> <tag>_ab_<wl>.log
 #   tail:<wl>:<lib>    heaviest particles alone + phase shares (tools/tail_latency.py) -> <tag>_tail_<wl>_<lib>.json
+#   sched:<wl>:<segs>:<heavy>  scheduling sweep (tools/sched_sweep.py; comma lists of segment lengths and
+#                      heavy thresholds, priority 1) -> <tag>_sched_<wl>.json
 #   torchrun1          bench.py through torch.distributed.run, world size 1 (RCCL) -> <tag>_torchrun_w1.json
 #   round              suite smoke bench trace pmc others
 set -o pipefail
@@ -51,6 +53,9 @@ run_task() {
   tail:*)
     spec=${1#tail:}; w=${spec%%:*}; l=$(lib ${spec#*:}); n=$(basename $l .so)
     FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1 timeout -k 10 400 python tools/tail_latency.py --workload $w --top 3 --json $O/${TAG}_tail_${w}_$n.json > $O/${TAG}_tail_${w}_$n.log 2>&1 ;;
+  sched:*)
+    spec=${1#sched:}; w=${spec%%:*}; rest=${spec#*:}; seg=${rest%%:*}; heavy=${rest#*:}
+    timeout -k 10 600 python tools/sched_sweep.py --workload $w --segments $seg --heavy $heavy --prio 1 --json $O/${TAG}_sched_$w.json > $O/${TAG}_sched_$w.log 2>&1 ;;
   torchrun1) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_torchrun_w1.json 2> $O/${TAG}_torchrun_w1.err ;;
   round) for t in suite smoke bench trace pmc others; do run_task $t || return $?; done ;;
   *) echo "unknown task $1" >&2; return 2 ;;
