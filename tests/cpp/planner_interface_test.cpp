@@ -356,6 +356,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     g_dump = argc > 2 && std::string(argv[2]) == "--dump";
+    const bool hand_only = argc > 2 && std::string(argv[2]) == "--hand"; /* TnuvaRobot stepping only: no GPU */
     const char* normals_out = (argc > 3 && std::string(argv[2]) == "--normals-out") ? argv[3] : nullptr;
     try {
         Reader r(argv[1]);
@@ -419,6 +420,10 @@ int main(int argc, char** argv) {
                 dump_environment(s, s.obstacles);
                 return dump(*robot, starts, targets);
             }
+            if (hand_only) {
+                step_by_hand(s, *robot, starts[0], targets[0]);
+                return 0;
+            }
             upc::LinkedSimulatorPtr sim = fast_kinematic_simulator::MakeLinkedSimulator(
                 E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
             const int rc = exercise<upc::LinkedConfig, upc::LinkedConfigAlloc>(s, sim, robot, starts, targets);
@@ -479,6 +484,10 @@ int main(int argc, char** argv) {
             const auto starts = read_configs("starts");
             const auto targets = read_configs("targets");
             if (g_dump) return dump(*robot, starts, targets);
+            if (hand_only) {
+                step_by_hand(s, *robot, starts[0], targets[0]);
+                return 0;
+            }
             upc::SE2SimulatorPtr sim = fast_kinematic_simulator::MakeSE2Simulator(
                 E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
             const int rc = exercise<upc::SE2Config, upc::SE2ConfigAlloc>(s, sim, robot, starts, targets);
@@ -500,6 +509,10 @@ int main(int argc, char** argv) {
         const auto starts = read_configs("starts");
         const auto targets = read_configs("targets");
         if (g_dump) return dump(*robot, starts, targets);
+        if (hand_only) {
+            step_by_hand(s, *robot, starts[0], targets[0]);
+            return 0;
+        }
         upc::SE3SimulatorPtr sim = fast_kinematic_simulator::MakeSE3Simulator(
             E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
         const int rc = exercise<upc::SE3Config, upc::SE3ConfigAlloc>(s, sim, robot, starts, targets);

@@ -325,3 +325,32 @@ def test_environment_builder_public_api(workspace):
     assert np.array_equal(_hexrow(rows["env_quat"]), np.array(want))
     other = {line.split()[0]: line.split()[1:] for line in _dump("linked", not workspace).splitlines()}
     assert all(rows[k] == other[k] for k in rows if k.startswith("env_"))
+
+
+@pytest.mark.parametrize("workspace", [False, True], ids=["standalone", "workspace"])
+@pytest.mark.parametrize("name", ["linked", "se2", "se3"])
+def test_robot_stepped_by_hand_matches_oracle(name, workspace):
+    """The TnuvaRobot control interface (TNUVA:15-23) on the host, no GPU: GenerateControlAction,
+    ApplyControlInput(u) on even steps and ApplyControlInput(u, rng) on odd ones with
+    std::mt19937_64(seed + 77) as the generator, against the oracle's robot stepped the same way
+    (reference-mode actuators: each its own std::normal_distribution), bit for bit; then
+    ResetControllers zeroes the controllers."""
+    import oracle
+
+    family, wl, obstacles, grid = _scene(name)
+    exe = build_planner_test(workspace=workspace)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "scene.txt")
+        _write_scene(path, family, wl, obstacles, grid)
+        p = subprocess.run([exe, path, "--hand"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    rows = _parse(p.stdout)
+    u_o, q_o, pid_o = oracle.robot_steps(wl.robot, wl.starts[0], wl.targets[0], 1.0 / wl.controller_frequency, 12, wl.seed + 77,
+                                         noisy_mask=sum(1 << k for k in range(1, 12, 2)))
+    assert np.array_equal(np.array([_hexrow(r[1:]) for r in rows["hand_u"]]), u_o)
+    assert np.array_equal(np.array([_hexrow(r[1:]) for r in rows["hand_q"]]), q_o)
+    assert np.array_equal(_hexrow(rows["hand_pid"][0]), pid_o) and np.any(pid_o != 0.0)
+    assert rows["hand_reset"][0] == ["1"]
+    # the noisy steps really drew noise: the clean replay of the same controls differs
+    clean = oracle.robot_steps(wl.robot, wl.starts[0], wl.targets[0], 1.0 / wl.controller_frequency, 12, wl.seed + 77)[1]
+    assert not np.array_equal(clean, q_o)
