@@ -271,3 +271,51 @@ def make_linked_robot(base_transform, num_links: int, joints: Sequence[Joint],
 def se3_pose(translation=(0.0, 0.0, 0.0), rotation=None) -> np.ndarray:
     """SE(3) configuration (12 doubles, 3x4 row-major)."""
     return transform34(translation, rotation)
+
+
+class RobotController:
+    """One robot stepped by hand through the TnuvaRobot control interface (TNUVA:15-23), on
+    the host with the simulation kernels' arithmetic (fks_robot_control_action /
+    fks_robot_apply_control_input): the robot's configuration and its controllers' state
+    (per dof the error integral, then per dof the last error; ResetPosition zeroes them,
+    TNUVA:139-150, 332-336, 524-536)."""
+
+    def __init__(self, robot: RobotDescription, position):
+        self.robot = robot
+        self.position = np.ascontiguousarray(position, dtype=np.float64).reshape(robot.config_width).copy()
+        self.controller_state = np.zeros(2 * robot.num_dofs)
+
+    def reset_position(self, position):
+        self.reset_controllers()
+        self.position = np.ascontiguousarray(position, dtype=np.float64).reshape(self.robot.config_width).copy()
+        return self.position
+
+    def reset_controllers(self):
+        self.controller_state[:] = 0.0
+
+    def generate_control_action(self, target, controller_interval: float) -> np.ndarray:
+        """GenerateControlAction(target, controller_interval) (TNUVA:179-198, 384-412, 598-614)."""
+        desc, keep = self.robot.to_c()
+        t = np.ascontiguousarray(target, dtype=np.float64).reshape(self.robot.config_width)
+        u = np.zeros(self.robot.num_dofs)
+        _capi.check(_capi.lib().fks_robot_control_action(ctypes.byref(desc), _capi.as_ptr(self.position, ctypes.c_double),
+                                                         _capi.as_ptr(t, ctypes.c_double), float(controller_interval),
+                                                         _capi.as_ptr(self.controller_state, ctypes.c_double),
+                                                         _capi.as_ptr(u, ctypes.c_double)))
+        del keep
+        return u
+
+    def apply_control_input(self, control_input, unit_noise=None) -> np.ndarray:
+        """ApplyControlInput(u) (TNUVA:152-163, 348-364, 538-566); with unit_noise (one
+        TN(0, 0.5) sample on [-1, 1] per dof) ApplyControlInput(u, rng) (UNC:77-90)."""
+        desc, keep = self.robot.to_c()
+        u = np.ascontiguousarray(control_input, dtype=np.float64).reshape(self.robot.num_dofs)
+        n = None if unit_noise is None else np.ascontiguousarray(unit_noise, dtype=np.float64).reshape(self.robot.num_dofs)
+        out = np.zeros(self.robot.config_width)
+        _capi.check(_capi.lib().fks_robot_apply_control_input(ctypes.byref(desc), _capi.as_ptr(self.position, ctypes.c_double),
+                                                              _capi.as_ptr(u, ctypes.c_double),
+                                                              _capi.as_ptr(n, ctypes.c_double) if n is not None else None,
+                                                              _capi.as_ptr(out, ctypes.c_double)))
+        del keep
+        self.position = out
+        return out
