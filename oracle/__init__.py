@@ -72,7 +72,7 @@ def _load(path):
     L.oracle_forward_simulate_traced.argtypes = [
         POINTER(C.Environment), POINTER(C.SolverParams), c_double, c_uint64, c_uint64, POINTER(C.RobotDesc),
         POINTER(c_double), c_uint64, POINTER(c_double), c_uint64, c_int32, c_int32, POINTER(c_double), POINTER(c_uint8),
-        POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32), POINTER(C.Trace)]
+        POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32), POINTER(C.Trace), c_uint64]
     L.oracle_philox4x32_10.restype = None
     L.oracle_philox4x32_10.argtypes = [POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]
     L.oracle_pid_sequence.restype = None
@@ -156,7 +156,7 @@ def forward_simulate(env, robot, solver, frequency, seed, starts, targets, allow
 
 
 def forward_simulate_traced(env, robot, solver, frequency, seed, starts, targets, allow_contacts=True, call_index=0,
-                            step_capacity=None, config_capacity=4096, threads=0):
+                            step_capacity=None, config_capacity=4096, threads=0, first_particle_id=0):
     """ForwardSimulateRobot with enable_tracing (SPCS:824-829) per particle, counter RNG.
     Returns (result dict, fast_kinematic_simulator_amd.trace.TraceBuffers)."""
     L = lib()
@@ -182,7 +182,7 @@ def forward_simulate_traced(env, robot, solver, frequency, seed, starts, targets
                                           c_uint64(int(call_index)), ctypes.byref(desc), _p(starts, c_double), n,
                                           _p(targets, c_double), targets.shape[0], 1 if allow_contacts else 0, int(threads),
                                           _p(out, c_double), _p(coll, c_uint8), _p(micro, c_uint32), _p(res, c_uint32),
-                                          _p(err, c_uint32), ctypes.byref(tr))
+                                          _p(err, c_uint32), ctypes.byref(tr), c_uint64(int(first_particle_id)))
     del keep_env, keep_robot
     if st != 0:
         raise RuntimeError(f"oracle_forward_simulate_traced failed ({st})")

@@ -1133,9 +1133,10 @@ int oracle_forward_simulate_traced(const fks_environment* env, const fks_solver_
                                    uint64_t seed, uint64_t call_index, const fks_robot_desc* robot_desc, const double* starts,
                                    uint64_t n, const double* targets, uint64_t num_targets, int32_t allow_contacts,
                                    int32_t num_threads, double* out_positions, uint8_t* out_collided, uint32_t* out_microsteps,
-                                   uint32_t* out_resolver_iterations, uint32_t* out_error_flags, const fks_trace* trace) {
+                                   uint32_t* out_resolver_iterations, uint32_t* out_error_flags, const fks_trace* trace,
+                                   uint64_t first_particle_id) {
     if (!trace || !trace->num_steps || !trace->num_configs) return 1;
-    return forward_simulate_impl(env, params, frequency, seed, call_index, robot_desc, starts, n, targets, num_targets, 0,
+    return forward_simulate_impl(env, params, frequency, seed, call_index, robot_desc, starts, n, targets, num_targets, first_particle_id,
                                  allow_contacts, 0, num_threads, out_positions, out_collided, out_microsteps,
                                  out_resolver_iterations, out_error_flags, nullptr, nullptr, trace, 0, nullptr);
 }
