@@ -3,6 +3,7 @@
 #
 # usage: bash tools/gpu.sh <tag> <task> [<task> ...]
 #   suite              pytest -m gpu (whole suite)                  -> <tag>_pytest_gpu.log
+#   suitelib:<lib>     the same suite against a variant library  -> <tag>_pytest_gpu_<lib>.log
 #   smoke              __graft_entry__.smoke()                      -> <tag>_smoke.log
 #   bench[:cfgN]       bench.py (default workload, or --workload cfgN) -> <tag>_bench[_cfgN].json
 #   others             bench lines of cfg1 / cfg2 / cfg4 / cfg5
@@ -12,6 +13,8 @@
 #   ab:<wl>:<libs>     interleaved bench.py of comma-separated libraries (each may carry +flag;
 #                      "L" = the product library) on workload <wl>  -> <tag>_ab_<wl>.log
 #   tail:<wl>:<lib>    heaviest particles alone + phase shares (tools/tail_latency.py) -> <tag>_tail_<wl>_<lib>.json
+#   tailpmc:<wl>:<lib> instruction-mix and wait counters of the batch and the heaviest particle
+#                      alone (three --pmc passes over tools/tail_latency.py --top 1) -> <tag>_tailpmc_<wl>_<lib>/
 #   sched:<wl>:<segs>:<heavy>  scheduling sweep (tools/sched_sweep.py; comma lists of segment lengths and
 #                      heavy thresholds, priority 1) -> <tag>_sched_<wl>.json
 #   torchrun1          bench.py through torch.distributed.run, world size 1 (RCCL) -> <tag>_torchrun_w1.json
@@ -30,6 +33,7 @@ lib() { [ "$1" = L ] && echo $L || echo "$1"; }
 run_task() {
   case "$1" in
   suite) timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/${TAG}_pytest_gpu.log 2>&1 ;;
+  suitelib:*) l=$(lib ${1#suitelib:}); FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/${TAG}_pytest_gpu_$(basename $l .so).log 2>&1 ;;
   smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1 ;;
   bench) timeout -k 10 400 python bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err ;;
   bench:*) w=${1#bench:}; timeout -k 10 300 python bench.py --workload $w --no-config-check > $O/${TAG}_bench_$w.json 2> $O/${TAG}_bench_$w.err ;;
@@ -53,6 +57,14 @@ run_task() {
   tail:*)
     spec=${1#tail:}; w=${spec%%:*}; l=$(lib ${spec#*:}); n=$(basename $l .so)
     FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1 timeout -k 10 400 python tools/tail_latency.py --workload $w --top 3 --json $O/${TAG}_tail_${w}_$n.json > $O/${TAG}_tail_${w}_$n.log 2>&1 ;;
+  tailpmc:*)
+    spec=${1#tailpmc:}; w=${spec%%:*}; l=$(lib ${spec#*:}); n=$(basename $l .so); D=$O/${TAG}_tailpmc_${w}_$n
+    T1="python3 tools/tail_latency.py --workload $w --top 1"
+    export FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1
+    timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES --kernel-trace --output-format csv -d $D/mix -o tail -- $T1 > $D.mix.log 2>&1 &&
+    timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $D/wait -o tail -- $T1 > $D.wait.log 2>&1 &&
+    timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 --kernel-trace --output-format csv -d $D/valu -o tail -- $T1 > $D.valu.log 2>&1
+    rc=$?; unset FKS_LIB_PATH FKS_VARIANT_LIB; return $rc ;;
   sched:*)
     spec=${1#sched:}; w=${spec%%:*}; rest=${spec#*:}; seg=${rest%%:*}; heavy=${rest#*:}
     timeout -k 10 600 python tools/sched_sweep.py --workload $w --segments $seg --heavy $heavy --prio 1 --json $O/${TAG}_sched_$w.json > $O/${TAG}_sched_$w.log 2>&1 ;;
