@@ -181,6 +181,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config-check", action="store_true", help="skip the batched CheckConfigCollision line")
     ap.add_argument("--segment-steps", type=int, default=-1, help="A/B: fks_set_segment_steps (default: automatic)")
+    ap.add_argument("--pipeline-batches", type=int, default=6,
+                    help="one GPU: also time this many batches alternated over two contexts on two streams, so a "
+                         "batch's tail overlaps the next batch's start (reported beside `value`, never as it; 0: off)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous / shard / gather check without a GPU (gloo): no simulation, value null")
     args = ap.parse_args()
@@ -330,6 +333,9 @@ def main():
         host_s = time.perf_counter() - t0
         pcie = {"value": float(np.sum(hr["microsteps"], dtype=np.int64)) / host_s, "unit": UNIT, "ms": host_s * 1e3,
                 "note": "one fks_forward_simulate call with host buffers (H2D starts/targets, kernel, D2H outcomes), rank 0"}
+        pipe = pipelined_batches(sim, denv, wl, dev, starts, targets, n_local, lo, args.pipeline_batches) if world == 1 else None
+        if pipe:
+            log(f"pipelined: {pipe['value']:.4e} {UNIT}, {pipe['ms_per_batch']:.1f} ms per batch, identical={pipe['identical_to_sequential']}")
         cc = None
         if not args.no_config_check and args.workload == "cfg3":
             if not args.no_cpu_baseline:
@@ -389,6 +395,7 @@ def main():
             "cpu_baseline": cpu,
             "config_check": cc,
             "pcie_inclusive": pcie,
+            "pipelined": pipe,
             # share of wave time per phase of the hot path (s_memtime cycle sums, rank 0)
             # (only in profiling builds of the library: -DFKS_PHASE_TIMERS=1, see tools/variant_bench.py)
             "kernel_phases": ({k: (v if k in PHASE_COUNTS else round(v / max(1, phases["particle"]), 4))
@@ -402,6 +409,70 @@ def main():
         dist.barrier()  # rank 0 ran the CPU baseline and the config-check line after the timed region
         dist.destroy_process_group()
     return 0
+
+
+def pipelined_batches(sim, denv, wl, dev, starts, targets, n, first_id, batches):
+    """Consecutive batches alternated over two contexts (each with its own workspace) on two
+    streams: the persistent grid of batch k + 1 takes the wave slots batch k frees during its
+    tail, so the machine stays busy across batches.  Each batch is the full hot path over
+    the same particles with its own RNG call index; the last batch's outcomes are compared
+    bit for bit with a sequential call at that index.  Reported beside `value`, never as it:
+    one batch's latency is still the kernel time of the sequential run."""
+    import torch
+
+    if batches < 2:
+        return None
+    from fast_kinematic_simulator_amd import make_linked_simulator
+
+    sim2 = make_linked_simulator(denv, wl.solver, wl.controller_frequency, wl.seed, device=dev.index)
+    sim2.set_robot(wl.robot)
+    sims = (sim, sim2)
+    streams = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+    W = wl.robot.config_width
+
+    def outs():
+        return (torch.empty((n, W), dtype=torch.float64, device=dev), torch.empty(n, dtype=torch.uint8, device=dev),
+                torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+                torch.empty(n, dtype=torch.int32, device=dev))
+
+    bufs = (outs(), outs())
+    totals = (torch.zeros((), dtype=torch.int64, device=dev), torch.zeros((), dtype=torch.int64, device=dev))
+
+    def launch(k, call_index):
+        j = k % 2
+        q, c, m, r, e = bufs[j]
+        sims[j].set_call_index(call_index)
+        sims[j].forward_simulate_device(wl.robot, starts.data_ptr(), n, targets.data_ptr(), 1, first_id, True, q.data_ptr(),
+                                        c.data_ptr(), m.data_ptr(), r.data_ptr(), e.data_ptr(), stream=streams[j].cuda_stream,
+                                        synchronize=False)
+        with torch.cuda.stream(streams[j]):
+            totals[j].add_(m.sum(dtype=torch.int64))
+
+    for k in range(2):
+        launch(k, 2000 + k)
+    torch.cuda.synchronize()
+    for t in totals:
+        t.zero_()
+    t0 = time.perf_counter()
+    for k in range(batches):
+        launch(k, k)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    micro = int(totals[0].item() + totals[1].item())
+    # the last batch again, alone on the first context: the same outcomes bit for bit
+    last = bufs[(batches - 1) % 2]
+    ref = outs()
+    sim.set_call_index(batches - 1)
+    sim.forward_simulate_device(wl.robot, starts.data_ptr(), n, targets.data_ptr(), 1, first_id, True, ref[0].data_ptr(),
+                                ref[1].data_ptr(), ref[2].data_ptr(), ref[3].data_ptr(), ref[4].data_ptr(),
+                                stream=torch.cuda.current_stream(dev).cuda_stream, synchronize=True)
+    torch.cuda.synchronize()
+    same = all(bool(torch.equal(a, b)) for a, b in zip(last, ref))
+    sim2.close()
+    return {"value": micro / elapsed, "unit": UNIT, "ms_per_batch": elapsed / batches * 1e3, "batches": batches,
+            "contexts": 2, "streams": 2, "identical_to_sequential": same,
+            "note": "throughput of back-to-back batches whose tails overlap the next batch's start (two contexts, two "
+                    "streams, fks_forward_simulate_device without synchronisation); `value` above is the one-stream figure"}
 
 
 def spawn_ranks(n: int) -> int:

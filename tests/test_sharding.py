@@ -140,3 +140,55 @@ def test_multi_device_context_over_every_visible_gpu(fks_lib, oracle_lib):
     o = oracle.forward_simulate(wl.environment(), wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts, wl.targets, True,
                                 call_index=5)
     assert np.array_equal(m["positions"], o["positions"]) and np.array_equal(m["microsteps"], o["microsteps"])
+
+
+@pytest.mark.gpu
+def test_two_contexts_on_two_streams_overlap_without_changing_results(fks_lib, oracle_lib):
+    """Consecutive batches alternated over two contexts on two streams (bench.py's
+    `pipelined` figure): each enqueue returns at once, the batches may run concurrently, and
+    every batch's outcomes equal a sequential call at the same RNG call index bit for bit
+    (and the oracle's for the first)."""
+    import torch
+
+    import oracle
+    from fast_kinematic_simulator_amd import make_linked_simulator
+    from fast_kinematic_simulator_amd import workloads as W
+
+    wl = W.cfg3(3000 / 65536)  # more particles than one wave slot each: segments in play
+    dev = torch.device("cuda", 0)
+    n, Wd = wl.starts.shape[0], wl.robot.config_width
+    sims = [make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed) for _ in range(2)]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    starts = torch.from_numpy(np.ascontiguousarray(wl.starts)).to(dev)
+    targets = torch.from_numpy(np.ascontiguousarray(wl.targets)).to(dev)
+    batches = 4
+    outs = [[torch.empty((n, Wd), dtype=torch.float64, device=dev), torch.empty(n, dtype=torch.uint8, device=dev),
+             torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+             torch.empty(n, dtype=torch.int32, device=dev)] for _ in range(batches)]
+    try:
+        for s in sims:
+            s.set_robot(wl.robot)
+        torch.cuda.synchronize()
+        for k in range(batches):
+            j = k % 2
+            sims[j].set_call_index(k)
+            q, c, m, r, e = outs[k]
+            sims[j].forward_simulate_device(wl.robot, starts.data_ptr(), n, targets.data_ptr(), 1, 0, True, q.data_ptr(),
+                                            c.data_ptr(), m.data_ptr(), r.data_ptr(), e.data_ptr(),
+                                            stream=streams[j].cuda_stream, synchronize=False)
+        torch.cuda.synchronize()
+        for k in range(batches):
+            sims[0].set_call_index(k)
+            ref = sims[0].forward_simulate_arrays(wl.robot, wl.starts, wl.targets, True)
+            got = [t.cpu().numpy() for t in outs[k]]
+            assert np.array_equal(got[0], ref["positions"]), k
+            assert np.array_equal(got[1].astype(bool), ref["collided"]), k
+            assert np.array_equal(got[2].astype(np.uint32), ref["microsteps"]), k
+            assert np.array_equal(got[3].astype(np.uint32), ref["resolver_iterations"]), k
+            assert np.array_equal(got[4].astype(np.uint32), ref["error_flags"]), k
+    finally:
+        for s in sims:
+            s.close()
+    o = oracle.forward_simulate(wl.environment(), wl.robot, wl.solver, wl.controller_frequency, wl.seed, wl.starts[:256],
+                                wl.targets, True, call_index=0)
+    assert np.array_equal(outs[0][0].cpu().numpy()[:256], o["positions"])
