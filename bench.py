@@ -181,6 +181,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config-check", action="store_true", help="skip the batched CheckConfigCollision line")
     ap.add_argument("--segment-steps", type=int, default=-1, help="A/B: fks_set_segment_steps (default: automatic)")
+    ap.add_argument("--no-contacts", action="store_true",
+                    help="A/B only: allow_contacts = false (particles stop at their first contact; no resolver)")
     ap.add_argument("--pipeline-batches", type=int, default=6,
                     help="one GPU: also time this many batches alternated over two contexts on two streams, so a "
                          "batch's tail overlaps the next batch's start (reported beside `value`, never as it; 0: off)")
@@ -258,9 +260,9 @@ def main():
         sim.set_call_index(call_index)
         if timed_events is not None:
             timed_events[0].record(stream)
-        sim.forward_simulate_device(wl.robot, starts.data_ptr(), n_local, targets.data_ptr(), 1, lo, True, out_q.data_ptr(),
-                                    out_coll.data_ptr(), out_micro.data_ptr(), out_res.data_ptr(), out_err.data_ptr(),
-                                    stream=stream.cuda_stream, synchronize=False)
+        sim.forward_simulate_device(wl.robot, starts.data_ptr(), n_local, targets.data_ptr(), 1, lo, not args.no_contacts,
+                                    out_q.data_ptr(), out_coll.data_ptr(), out_micro.data_ptr(), out_res.data_ptr(),
+                                    out_err.data_ptr(), stream=stream.cuda_stream, synchronize=False)
         if timed_events is not None:
             timed_events[1].record(stream)
         micro_total.add_(out_micro.sum(dtype=torch.int64))
@@ -333,7 +335,8 @@ def main():
         host_s = time.perf_counter() - t0
         pcie = {"value": float(np.sum(hr["microsteps"], dtype=np.int64)) / host_s, "unit": UNIT, "ms": host_s * 1e3,
                 "note": "one fks_forward_simulate call with host buffers (H2D starts/targets, kernel, D2H outcomes), rank 0"}
-        pipe = pipelined_batches(sim, denv, wl, dev, starts, targets, n_local, lo, args.pipeline_batches) if world == 1 else None
+        pipe = (pipelined_batches(sim, denv, wl, dev, starts, targets, n_local, lo, args.pipeline_batches)
+                if world == 1 and not args.no_contacts else None)
         if pipe:
             log(f"pipelined: {pipe['value']:.4e} {UNIT}, {pipe['ms_per_batch']:.1f} ms per batch, identical={pipe['identical_to_sequential']}")
         cc = None
@@ -356,7 +359,8 @@ def main():
             "dtype": "f64",
             "data": f"synthetic (seeded {args.workload} scene and start perturbations, workloads.py)",
             "config": {
-                "workload": f"{workload_desc}, {n_local} particles per GPU, allow_contacts"
+                "workload": f"{workload_desc}, {n_local} particles per GPU, "
+                            + ("allow_contacts = false (A/B only)" if args.no_contacts else "allow_contacts")
                             + (f", RCCL gather of outcomes to rank 0 over {world} ranks" if dist is not None else
                                ", one process (no gather: outcomes stay on this GPU)"),
                 "outcome_gather": "rccl" if dist is not None else None,
