@@ -271,6 +271,7 @@ PROTOTYPES = [
     ("fks_get_launch_geometry", c_int32, [c_void_p, POINTER(c_uint32), POINTER(c_uint64)]),
     ("fks_set_segment_steps", c_int32, [c_void_p, c_uint32]),
     ("fks_set_segment_policy", c_int32, [c_void_p, c_uint32, c_uint32]),
+    ("fks_set_small_batch_kernel", c_int32, [c_void_p, c_int32]),
     ("fks_set_individual_jacobians", c_int32, [c_void_p, c_int32]),
     ("fks_env_build", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), POINTER(c_void_p)]),
     ("fks_env_build_gpu", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), c_int32,

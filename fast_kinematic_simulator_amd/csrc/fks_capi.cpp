@@ -35,6 +35,9 @@ extern "C" __global__ void fks_simulate_se3_indiv(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_traced(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se2_traced(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se3_traced(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_linked_small(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_se2_small(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_se3_small(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_lean(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_lean_indiv(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_lean_traced(const fksd::SimArgs* args);
@@ -76,6 +79,15 @@ sim_kernel_t kernel_for(int robot_type, bool individual_jacobians = false, bool 
         default:
             if (lean) return individual_jacobians ? fks_simulate_linked_lean_indiv : fks_simulate_linked_lean;
             return individual_jacobians ? fks_simulate_linked_indiv : fks_simulate_linked;
+    }
+}
+
+/* the low-occupancy instantiation for batches that fit its resident waves */
+sim_kernel_t small_kernel_for(int robot_type) {
+    switch (robot_type) {
+        case FKS_ROBOT_SE2: return fks_simulate_se2_small;
+        case FKS_ROBOT_SE3: return fks_simulate_se3_small;
+        default: return fks_simulate_linked_small;
     }
 }
 
@@ -228,6 +240,7 @@ struct fks_context {
     size_t cap_scratch = 0; /* doubles allocated at d_scratch */
     uint64_t scratch_per_wave = 0;
     uint32_t grid_waves = 0;
+    uint32_t small_grid_waves = 0; /* resident waves of the small-batch kernel (0: none for this layout) */
     uint32_t grid_groups = 0;
     uint32_t waves_per_group = fksd::kWavesPerGroup;
     size_t lds_bytes = 0;
@@ -258,6 +271,7 @@ struct fks_context {
     uint32_t heavy_per_step = kHeavyResolverPerStep; /* fks_set_segment_policy */
     uint32_t heavy_priority = 1;
     int32_t individual_jacobians = 0; /* fks_set_individual_jacobians (SPCS:420-423) */
+    int32_t small_batch = 1;          /* fks_set_small_batch_kernel */
     bool fk_pair = false;             /* paired FK of free microsteps (fks_set_robot) */
     bool lean = false;                /* lean LDS block + lean kernels (fks_set_robot) */
     double* d_seg_state = nullptr;
@@ -594,6 +608,15 @@ static fks_status launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
     ctx->lds_bytes = bytes;
     ctx->grid_groups = grid_groups;
     ctx->grid_waves = grid_groups * wpg;
+    /* the small-batch kernel on the same layout (not for lean blocks) */
+    ctx->small_grid_waves = 0;
+    if (!lean) {
+        int nk = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nk, reinterpret_cast<const void*>(small_kernel_for(R.type)), 64 * (int)wpg,
+                                                         bytes) == hipSuccess &&
+            nk > 0)
+            ctx->small_grid_waves = std::min<uint32_t>((uint32_t)(cus * nk) * wpg, ctx->grid_waves);
+    }
     ctx->scratch_per_wave = scratch_per_wave;
     return FKS_OK;
 }
@@ -1078,8 +1101,13 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     const uint64_t groups_needed = (n + ctx->waves_per_group - 1) / ctx->waves_per_group;
     const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? (groups_needed > 0 ? groups_needed : 1)
                                                                                   : ctx->grid_groups);
+    /* a batch that fits the small-batch kernel's resident waves, whole particles, plain
+     * simulation: that kernel (every particle has its wave from the start either way) */
+    const bool small = ctx->small_batch && !tr && !ctx->individual_jacobians && !ctx->lean && a.nseg == 1 &&
+                       n <= (uint64_t)ctx->small_grid_waves;
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
-    hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type, ctx->lean) : kernel_for(ctx->R.type, ctx->individual_jacobians != 0, ctx->lean),
+    hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type, ctx->lean)
+                          : (small ? small_kernel_for(ctx->R.type) : kernel_for(ctx->R.type, ctx->individual_jacobians != 0, ctx->lean)),
                        dim3(grid),
                        dim3(64 * ctx->waves_per_group), ctx->lds_bytes, s, static_cast<const fksd::SimArgs*>(ctx->d_args));
     HIP_TRY(ctx, hipGetLastError());
@@ -1530,6 +1558,12 @@ fks_status fks_get_phase_cycles(const fks_context* ctx, int which, uint64_t* out
 fks_status fks_set_segment_steps(fks_context* ctx, uint32_t controller_steps) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
     ctx->segment_steps = controller_steps;
+    return FKS_OK;
+}
+
+fks_status fks_set_small_batch_kernel(fks_context* ctx, int32_t enabled) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    ctx->small_batch = enabled ? 1 : 0;
     return FKS_OK;
 }
 

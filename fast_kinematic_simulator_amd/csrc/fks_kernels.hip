@@ -3419,6 +3419,25 @@ extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_se3(const SimArgs* __re
     simulate_particles<FKS_ROBOT_SE3, false>(args, lds_mem);
 }
 
+/* small batches (fks_set_small_batch_kernel): at most two waves per SIMD, so the register
+ * budget holds the whole working set without spills.  One particle per wave and no
+ * segments, chosen only when the batch fits its resident waves: such a batch is the
+ * latency of its slowest particle, not a throughput problem (cfg1: 3.8-3.9 ms against
+ * 4.2-4.35, profiles/r04j_occupancy_ab_cfg1.log). */
+#define FKS_SMALL_KERNEL_ATTRS __launch_bounds__(64 * kMaxWavesPerGroup) __attribute__((amdgpu_waves_per_eu(2)))
+extern "C" __global__ void FKS_SMALL_KERNEL_ATTRS fks_simulate_linked_small(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_LINKED, false>(args, lds_mem);
+}
+extern "C" __global__ void FKS_SMALL_KERNEL_ATTRS fks_simulate_se2_small(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_SE2, false>(args, lds_mem);
+}
+extern "C" __global__ void FKS_SMALL_KERNEL_ATTRS fks_simulate_se3_small(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_SE3, false>(args, lds_mem);
+}
+
 /* simulate_with_individual_jacobians = true (SPCS:420, 1629; fks_set_individual_jacobians) */
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked_indiv(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];

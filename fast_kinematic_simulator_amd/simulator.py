@@ -157,6 +157,11 @@ class HipParticleContactSimulator:
         _capi.check(self._lib.fks_set_segment_policy(self._ctx, int(heavy_resolver_per_step), int(heavy_priority)), self._ctx,
                     "segment policy")
 
+    def set_small_batch_kernel(self, enabled: bool = True):
+        """Batches that fit the low-occupancy instantiation's resident waves run it
+        (fks_set_small_batch_kernel; default on).  Results do not depend on it."""
+        _capi.check(self._lib.fks_set_small_batch_kernel(self._ctx, 1 if enabled else 0), self._ctx, "small batch kernel")
+
     def set_individual_jacobians(self, simulate_with_individual_jacobians: bool):
         """The simulate_with_individual_jacobians constructor flag of the reference class
         (SPCS:420-423, 1629): True selects ComputeResolverCorrectionStepIndividualJacobians

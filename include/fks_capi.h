@@ -47,8 +47,9 @@ extern "C" {
  * proven_free_microsteps) removed: it broke even on the headline.
  * 6: host robot control (fks_robot_control_action, fks_robot_apply_control_input), the
  * environment builder's public steps (fks_env_discretize_obstacle, fks_env_build_normals,
- * fks_env_cell_objects), fks_set_statistics / fks_set_total_counters */
-#define FKS_ABI_VERSION 6
+ * fks_env_cell_objects), fks_set_statistics / fks_set_total_counters.
+ * 7: fks_set_small_batch_kernel */
+#define FKS_ABI_VERSION 7
 
 typedef enum {
     FKS_OK = 0,
@@ -436,6 +437,14 @@ fks_status fks_set_segment_steps(fks_context* ctx, uint32_t controller_steps);
  *     2 = also 1 for particles that fell behind the round-robin).
  * The priority is reset to 0 at the start of every segment a wave claims. */
 fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_step, uint32_t heavy_priority);
+/* Small batches (ABI 7; no reference counterpart, results are bit-identical either way):
+ * with `enabled` (the default) a plain simulation call whose particles all fit the
+ * resident waves of a low-occupancy instantiation (two waves per SIMD, no register
+ * spills; not for lean LDS blocks, traced or individual-Jacobian calls, or explicit
+ * segments) runs that kernel — a batch that small is the latency of its slowest particle
+ * (a planner's typical call: cfg1, 32 particles, 10 % shorter).  0 = always the
+ * throughput kernel. */
+fks_status fks_set_small_batch_kernel(fks_context* ctx, int32_t enabled);
 /* SimpleParticleContactSimulator(..., simulate_with_individual_jacobians, ...) (SPCS:420-423,
  * 1629): 0 = ComputeResolverCorrectionStepStackedJacobian (SPCS:1990-1998; what the factories
  * FKS.cpp:22,45,68 hard-wire, the default), 1 = ComputeResolverCorrectionStepIndividualJacobians

@@ -8,7 +8,7 @@ COUNTER_KEYS = ("microsteps", "resolver_iterations", "controller_steps", "sdf_by
 
 
 def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, first_particle_id=0, sim=None,
-             individual_jacobians=False, segment_steps=None):
+             individual_jacobians=False, segment_steps=None, small_batch_kernel=None):
     import oracle
     from fast_kinematic_simulator_amd import make_linked_simulator
 
@@ -23,6 +23,8 @@ def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, f
         sim.set_individual_jacobians(True)
     if segment_steps is not None:
         sim.set_segment_steps(segment_steps)
+    if small_batch_kernel is not None:
+        sim.set_small_batch_kernel(small_batch_kernel)
     sim.set_call_index(call_index)
     g = sim.forward_simulate_arrays(wl.robot, starts, targets, allow)
     g["statistics"] = sim.get_statistics()

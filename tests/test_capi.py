@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol(fks_lib):
 def test_abi_basics(fks_lib):
     from fast_kinematic_simulator_amd import _capi, get_default_solver_parameters
 
-    assert fks_lib.fks_abi_version() == 6
+    assert fks_lib.fks_abi_version() == 7
     assert fks_lib.fks_status_string(0) == b"ok"
     p = _capi.SolverParams()
     assert fks_lib.fks_default_solver_params(ctypes.byref(p)) == 0
@@ -67,6 +67,7 @@ def test_argument_validation(fks_lib):
     # scheduling knob and grid diagnostics (no reference counterpart)
     assert fks_lib.fks_set_segment_steps(None, 10) == 1
     assert fks_lib.fks_set_segment_policy(None, 2, 1) == 1
+    assert fks_lib.fks_set_small_batch_kernel(None, 1) == 1
     assert fks_lib.fks_set_individual_jacobians(None, 1) == 1
     waves, lds = ctypes.c_uint32(0), ctypes.c_uint64(0)
     assert fks_lib.fks_get_launch_geometry(None, ctypes.byref(waves), ctypes.byref(lds)) == 1

@@ -24,10 +24,13 @@ def test_selftest_math(fks_lib):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("small_batch_kernel", [True, False])
 @pytest.mark.parametrize("name,scale", CASES)
-def test_forward_parity(fks_lib, oracle_lib, name, scale):
+def test_forward_parity(fks_lib, oracle_lib, name, scale, small_batch_kernel):
+    """Batches this small run the low-occupancy instantiation by default
+    (fks_set_small_batch_kernel); both kernels must match the oracle."""
     wl = W.WORKLOADS[name](scale)
-    g, o = run_both(wl)
+    g, o = run_both(wl, small_batch_kernel=small_batch_kernel)
     print(name, mismatch_report(g, o))
     assert_identical(g, o)
     assert_counters_identical(g, o)
