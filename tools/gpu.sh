@@ -27,7 +27,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 O=gpurun_out
 L=fast_kinematic_simulator_amd/libfks_hip.so
-BP="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
+BP="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --pipeline-batches 0"
 lib() { [ "$1" = L ] && echo $L || echo "$1"; }
 
 run_task() {
@@ -44,7 +44,7 @@ run_task() {
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_write -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_write.err &&
     timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/${TAG}_pmc_tcc -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_tcc.err ;;
   valu)
-    B1="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-check"
+    B1="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0"
     mkdir -p $O/${TAG}_valu
     timeout -s KILL 180 rocprofv3 --pmc VALUBusy --kernel-trace --output-format csv -d $O/${TAG}_valu/valubusy -o bench -- $B1 > /dev/null 2> $O/${TAG}_valu/valubusy.err &&
     timeout -s KILL 180 rocprofv3 --pmc VALUUtilization --kernel-trace --output-format csv -d $O/${TAG}_valu/valuutil -o bench -- $B1 > /dev/null 2> $O/${TAG}_valu/valuutil.err &&
