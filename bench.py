@@ -335,9 +335,13 @@ def main():
         host_s = time.perf_counter() - t0
         pcie = {"value": float(np.sum(hr["microsteps"], dtype=np.int64)) / host_s, "unit": UNIT, "ms": host_s * 1e3,
                 "note": "one fks_forward_simulate call with host buffers (H2D starts/targets, kernel, D2H outcomes), rank 0"}
-        pipe = (pipelined_batches(sim, denv, wl, dev, starts, targets, n_local, lo, args.pipeline_batches)
-                if world == 1 and not args.no_contacts else None)
-        if pipe:
+        pipe = None
+        if world == 1 and not args.no_contacts:
+            try:
+                pipe = pipelined_batches(sim, denv, wl, dev, starts, targets, n_local, lo, args.pipeline_batches)
+            except Exception as e:  # a side figure: never costs the headline line
+                pipe = {"value": None, "error": f"{type(e).__name__}: {e}"}
+        if pipe and pipe.get("value"):
             log(f"pipelined: {pipe['value']:.4e} {UNIT}, {pipe['ms_per_batch']:.1f} ms per batch, identical={pipe['identical_to_sequential']}")
         cc = None
         if not args.no_config_check and args.workload == "cfg3":
