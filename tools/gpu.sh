@@ -9,6 +9,7 @@
 #   others             bench lines of cfg1 / cfg2 / cfg4 / cfg5
 #   trace              rocprofv3 --kernel-trace --stats of bench.py -> <tag>_trace/
 #   pmc                FETCH_SIZE / WRITE_SIZE / TCC hit+miss, one --pmc pass each -> <tag>_pmc_*/
+#   pmc:<wl>           the same three passes on another workload  -> <tag>_pmc_<wl>_*/
 #   valu               VALUBusy / VALUUtilization / SQ issue counters, one pass each -> <tag>_valu/
 #   ab:<wl>:<libs>     interleaved bench.py of comma-separated libraries (each may carry +flag;
 #                      "L" = the product library) on workload <wl>  -> <tag>_ab_<wl>.log
@@ -43,6 +44,11 @@ run_task() {
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_fetch -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_fetch.err &&
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_write -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_write.err &&
     timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/${TAG}_pmc_tcc -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_tcc.err ;;
+  pmc:*)
+    w=${1#pmc:}; BW="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0 --workload $w"
+    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_${w}_fetch -o bench -- $BW > /dev/null 2> $O/${TAG}_pmc_${w}_fetch.err &&
+    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_${w}_write -o bench -- $BW > /dev/null 2> $O/${TAG}_pmc_${w}_write.err &&
+    timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/${TAG}_pmc_${w}_tcc -o bench -- $BW > /dev/null 2> $O/${TAG}_pmc_${w}_tcc.err ;;
   valu)
     B1="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0"
     mkdir -p $O/${TAG}_valu

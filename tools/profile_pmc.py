@@ -5,6 +5,10 @@ each its own `rocprofv3 --pmc ... --kernel-trace --output-format csv` run of
 `python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline`):
 
     python tools/profile_pmc.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_tcc r01
+    python tools/profile_pmc.py <fetch> <write> <tcc> r04_cfg5 fks_simulate_linked_lean   # another kernel
+
+Only the headline kernel's summary (no kernel argument) is also written as latest_pmc.json,
+which bench.py reads for `roofline.traffic`.
 
 HBM traffic per launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 bytes, averaged over the
 kernel's dispatches: MI355X_MICROARCH.md §HBM prescribes doubling FETCH_SIZE on gfx950
@@ -21,11 +25,11 @@ import sys
 KERNEL = "fks_simulate_linked"
 
 
-def counters(path):
+def counters(path, kernel=KERNEL):
     vals = {}
     with open(os.path.join(path, "bench_counter_collection.csv")) as f:
         for row in csv.DictReader(f):
-            if row["Kernel_Name"] != KERNEL:
+            if row["Kernel_Name"] != kernel:
                 continue
             vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
     return vals
@@ -33,15 +37,16 @@ def counters(path):
 
 def main():
     fetch_dir, write_dir, tcc_dir, tag = sys.argv[1:5]
-    f = counters(fetch_dir)["FETCH_SIZE"]
-    w = counters(write_dir)["WRITE_SIZE"]
-    t = counters(tcc_dir)
+    kernel = sys.argv[5] if len(sys.argv) > 5 else KERNEL
+    f = counters(fetch_dir, kernel)["FETCH_SIZE"]
+    w = counters(write_dir, kernel)["WRITE_SIZE"]
+    t = counters(tcc_dir, kernel)
     hits, misses = t["TCC_HIT_sum"], t["TCC_MISS_sum"]
     fetch_raw = sum(f) / len(f) * 1024.0
     fetch_b = 2.0 * fetch_raw
     write_b = sum(w) / len(w) * 1024.0
     out = {
-        "kernel": KERNEL,
+        "kernel": kernel,
         "dispatches": len(f),
         "fetch_bytes_per_launch": fetch_b,
         "fetch_size_raw_bytes_per_launch": fetch_raw,
@@ -54,7 +59,7 @@ def main():
                   "bench.py --steps 2 --warmup 1, tools/profile_pmc.py)",
     }
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    for name in (f"{tag}_pmc.json", "latest_pmc.json"):
+    for name in (f"{tag}_pmc.json", "latest_pmc.json") if kernel == KERNEL else (f"{tag}_pmc.json",):
         with open(os.path.join(root, "profiles", name), "w") as fo:
             json.dump(out, fo, indent=1)
     print(json.dumps(out, indent=1))
