@@ -606,7 +606,9 @@ __device__ void fk(Sim& s, const double* cfg, double* T) {
         M[3] = cfg[0];
         M[7] = cfg[1];
         M[11] = 0.0;
-        if (ln < 12) T[ln] = M[ln];
+        if (ln == 0)
+#pragma unroll
+            for (int e = 0; e < 12; ++e) T[e] = M[e]; /* not M[ln]: a lane-indexed private array lives in scratch */
         wsync();
     } else {
         if (ln < 12) T[ln] = cfg[ln];
@@ -765,7 +767,10 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
         double C[12];
         compose34(P, M, C);
         wsync();
-        if (ln < 12) cfg_out[ln] = C[ln];
+        /* lane 0 stores all twelve: indexing the private array by lane would put it in scratch */
+        if (ln == 0)
+#pragma unroll
+            for (int e = 0; e < 12; ++e) cfg_out[e] = C[e];
         wsync();
     }
 }
