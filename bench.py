@@ -171,7 +171,7 @@ def load_traffic():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (ranks); default: WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS),
@@ -186,9 +186,14 @@ def main():
     ap.add_argument("--pipeline-batches", type=int, default=6,
                     help="one GPU: also time this many batches alternated over two contexts on two streams, so a "
                          "batch's tail overlaps the next batch's start (reported beside `value`, never as it; 0: off)")
+    ap.add_argument("--specialize", choices=("on", "off"), default="on",
+                    help="run the robot's shape-specialised kernel (fks_set_specialization: compiled at setup, outside the "
+                         "timed region; results identical) or the generic one")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous / shard / gather check without a GPU (gloo): no simulation, value null")
     args = ap.parse_args()
+    if args.gpus is None:
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus < 1:
         log("--gpus must be >= 1")
         return 2
@@ -241,6 +246,14 @@ def main():
     if args.segment_steps >= 0:
         sim.set_segment_steps(args.segment_steps)
     sim.set_robot(wl.robot)
+    spec = None
+    if args.specialize == "on":
+        t0 = time.perf_counter()
+        sim.set_specialization(True)
+        spec = sim.specialization()
+        log(f"[rank {rank}] shape-specialised kernel {spec['shape']}: "
+            + (f"compiled in {spec['compile_seconds']:.1f}s" if not spec["from_cache"] else "from the kernel cache")
+            + f" ({time.perf_counter() - t0:.1f}s setup)")
     Wd = wl.robot.config_width
     dev = torch.device("cuda", local_rank)
     starts = torch.from_numpy(np.ascontiguousarray(wl.starts[lo:lo + n_local])).to(dev)
@@ -276,6 +289,7 @@ def main():
     torch.cuda.synchronize()
     sim.reset_total_counters()
     micro_total.zero_()
+    spec_before = sim.specialization()["launches"] if spec else 0
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if dist is not None:
         dist.barrier()
@@ -290,6 +304,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     kernel_ms = [a.elapsed_time(b) for a, b in events]
     tot = sim.total_counters()
+    spec_launches = (sim.specialization()["launches"] - spec_before) if spec else 0
     phases = sim.phase_cycles(total=True)
     geom = sim.launch_geometry()
     local_micro = int(micro_total.item())
@@ -387,7 +402,7 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "l2_hit_rate": l2_hit,
-                "kernel": KERNELS[wl.robot.robot_type],
+                "kernel": ("fks_simulate_shaped (" + spec["shape"] + ")") if spec else KERNELS[wl.robot.robot_type],
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 # second entry: the kernel is FP64-VALU- and latency-bound, not HBM-bound
@@ -401,6 +416,11 @@ def main():
             "wave_slots": {"resident_waves": geom["resident_waves"],
                            "busy_fraction": phases["wave_residency"] / 1e5 / max(1e-9, geom["resident_waves"] * sum(kernel_ms))},
             "cpu_baseline": cpu,
+            # the robot-shape-specialised kernel (fks_set_specialization): compiled by hiprtc at
+            # setup, before the warm-up; every timed launch ran it
+            "specialization": ({"shape": spec["shape"], "compile_seconds": spec["compile_seconds"],
+                                "from_cache": bool(spec["from_cache"]), "timed_launches": spec_launches,
+                                "all_timed_launches": spec_launches == args.steps} if spec else None),
             "config_check": cc,
             "pcie_inclusive": pcie,
             "pipelined": pipe,
@@ -434,6 +454,8 @@ def pipelined_batches(sim, denv, wl, dev, starts, targets, n, first_id, batches)
 
     sim2 = make_linked_simulator(denv, wl.solver, wl.controller_frequency, wl.seed, device=dev.index)
     sim2.set_robot(wl.robot)
+    if sim.specialization()["active"]:
+        sim2.set_specialization(True)  # the process cache holds the code object
     sims = (sim, sim2)
     streams = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
     W = wl.robot.config_width

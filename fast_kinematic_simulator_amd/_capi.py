@@ -172,6 +172,24 @@ class CallCounters(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class SpecializationInfo(ctypes.Structure):
+    """fks_specialization_info (ABI 8)"""
+    _fields_ = [
+        ("enabled", c_int32),
+        ("active", c_int32),
+        ("from_cache", c_int32),
+        ("reserved", c_int32),
+        ("compile_seconds", c_double),
+        ("launches", c_uint64),
+        ("shape", ctypes.c_char * 64),
+    ]
+
+    def as_dict(self):
+        d = {name: getattr(self, name) for name, _ in self._fields_ if name not in ("reserved", "shape")}
+        d["shape"] = self.shape.decode()
+        return d
+
+
 class Trace(ctypes.Structure):
     """fks_trace: ForwardSimulationStepTrace flattened per particle (include/fks_capi.h)."""
     _fields_ = [
@@ -272,6 +290,8 @@ PROTOTYPES = [
     ("fks_set_segment_steps", c_int32, [c_void_p, c_uint32]),
     ("fks_set_segment_policy", c_int32, [c_void_p, c_uint32, c_uint32]),
     ("fks_set_small_batch_kernel", c_int32, [c_void_p, c_int32]),
+    ("fks_set_specialization", c_int32, [c_void_p, c_int32]),
+    ("fks_get_specialization", c_int32, [c_void_p, POINTER(SpecializationInfo)]),
     ("fks_set_individual_jacobians", c_int32, [c_void_p, c_int32]),
     ("fks_env_build", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), POINTER(c_void_p)]),
     ("fks_env_build_gpu", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), c_int32,
@@ -307,6 +327,8 @@ PROTOTYPES = [
     ("fks_multi_reset_statistics", c_int32, [c_void_p]),
     ("fks_multi_get_last_call_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
     ("fks_multi_set_call_index", c_int32, [c_void_p, c_uint64]),
+    ("fks_multi_check_config_collision", c_int32, [c_void_p, POINTER(c_double), c_uint64, c_double, POINTER(c_uint8), POINTER(c_uint32)]),
+    ("fks_device_count", c_int32, []),
 ]
 
 _LIB = None

@@ -13,9 +13,14 @@ import subprocess
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 SOURCES = ["csrc/fks_kernels.hip", "csrc/fks_capi.cpp", "csrc/fks_multi.cpp", "csrc/fks_env_builder.cpp", "csrc/fks_env_gpu.hip",
-           "csrc/fks_robot_control.cpp"]
-HEADERS = ["csrc/fks_device.h", "csrc/fks_env_internal.h", "csrc/fks_se3.h", "../include/fks_capi.h",
+           "csrc/fks_robot_control.cpp", "csrc/fks_specialize.cpp"]
+HEADERS = ["csrc/fks_device.h", "csrc/fks_env_internal.h", "csrc/fks_se3.h", "csrc/fks_specialize.h", "../include/fks_capi.h",
            "../include/fks_portable_math.h"]
+# the kernel source and the headers it includes, carried inside the library for the run-time
+# compilation of shape-specialised kernels (fks_specialize.cpp): name as included -> path
+EMBEDDED = [("fks_kernels.hip", "csrc/fks_kernels.hip"), ("fks_device.h", "csrc/fks_device.h"), ("fks_se3.h", "csrc/fks_se3.h"),
+            ("fks_capi.h", "../include/fks_capi.h"), ("fks_portable_math.h", "../include/fks_portable_math.h")]
+GENERATED = os.path.join(ROOT, "build", "generated")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 
 
@@ -23,11 +28,54 @@ def hipcc() -> str:
     return shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 
+def write_embedded_sources(directory: str = GENERATED) -> str:
+    """fks_spec_sources.inc: the EMBEDDED files as byte arrays (cmake/fks_embed_sources.cmake
+    writes the same file for the CMake build)."""
+    os.makedirs(directory, exist_ok=True)
+    lines = ["/* generated from the library's sources by fast_kinematic_simulator_amd/build.py: do not edit */"]
+    entries = []
+    for k, (name, rel) in enumerate(EMBEDDED):
+        data = open(os.path.join(PKG, rel), "rb").read()
+        body = ",".join(f"0x{b:02x}" for b in data)
+        lines.append(f"static const unsigned char kFksSrc{k}[] = {{{body}}};")
+        entries.append(f'{{"{name}", kFksSrc{k}, sizeof(kFksSrc{k})}}')
+    lines.append("struct FksEmbeddedSource {\n    const char* name;\n    const unsigned char* data;\n    unsigned long size;\n};")
+    lines.append("static const FksEmbeddedSource kFksEmbeddedSources[] = {" + ", ".join(entries) + "};")
+    lines.append(f"static const int kFksEmbeddedSourceCount = {len(EMBEDDED)};")
+    out = os.path.join(directory, "fks_spec_sources.inc")
+    text = "\n".join(lines) + "\n"
+    if not os.path.exists(out) or open(out).read() != text:
+        with open(out + ".tmp", "w") as f:
+            f.write(text)
+        os.replace(out + ".tmp", out)
+    return out
+
+
 def build_command(output: str, defines=(), flags=()) -> list:
+    write_embedded_sources()
     return [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
             *[f"-D{d}" for d in defines], *flags,
-            f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(PKG, 'csrc')}", "-x", "hip",
+            f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(PKG, 'csrc')}", f"-I{GENERATED}", "-x", "hip",
             *[os.path.join(PKG, s) for s in SOURCES], "-o", output]
+
+
+SHAPEC = os.path.join(PKG, "fks_shapec")
+
+
+def build_shapec(force: bool = False) -> str:
+    """The compiler process of the shape specialisation (csrc/fks_shapec.cpp): a host program
+    over ROCm's hiprtc, next to libfks_hip.so, carrying the same embedded kernel source."""
+    inc = write_embedded_sources()
+    src = os.path.join(PKG, "csrc", "fks_shapec.cpp")
+    if not force and os.path.exists(SHAPEC) and os.path.getmtime(SHAPEC) >= max(os.path.getmtime(src), os.path.getmtime(inc)):
+        return SHAPEC
+    cmd = ["g++", "-std=c++17", "-O2", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", f"-I{GENERATED}", src, "-o", SHAPEC + ".tmp",
+           "-L/opt/rocm/lib", "-lhiprtc", "-Wl,-rpath,/opt/rocm/lib"]
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError("g++ (fks_shapec) failed:\n" + proc.stdout[-6000:])
+    os.replace(SHAPEC + ".tmp", SHAPEC)
+    return SHAPEC
 
 
 def _stale(target: str) -> bool:
@@ -40,6 +88,7 @@ def _stale(target: str) -> bool:
 
 def build_library(force: bool = False, verbose: bool = False) -> str:
     target = os.path.join(PKG, "libfks_hip.so")
+    build_shapec(force)
     if not force and not _stale(target):
         return target
     tmp = target + ".tmp"

@@ -23,6 +23,7 @@
 
 #include "fks_capi.h"
 #include "fks_env_internal.h"
+#include "fks_specialize.h"
 #include "fks_device.h"
 #include "fks_portable_math.h"
 
@@ -280,6 +281,14 @@ struct fks_context {
     fks_statistics stats;
     fks_call_counters last;
     fks_call_counters total;
+    /* robot-shape specialisation (fks_set_specialization, fks_specialize.cpp) */
+    int32_t specialize = 0;
+    hipModule_t spec_module = nullptr;
+    hipFunction_t spec_fn = nullptr; /* fks_simulate_shaped of the current robot's shape */
+    std::string spec_shape;
+    double spec_seconds = 0.0;
+    int32_t spec_from_cache = 0;
+    uint64_t spec_launches = 0;
 };
 
 template <typename T>
@@ -302,7 +311,10 @@ static fks_status hip_fail(fks_context* ctx, hipError_t e, const char* where) {
         if (_e != hipSuccess) return hip_fail((ctx), _e, #expr); \
     } while (0)
 
+static void spec_release(fks_context* ctx);
+
 static void free_robot(fks_context* ctx) {
+    spec_release(ctx); /* a specialised kernel belongs to one robot shape */
     for (void* p : ctx->robot_allocs) (void)hipFree(p);
     ctx->robot_allocs.clear();
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
@@ -327,6 +339,69 @@ static void free_staging(fks_context* ctx) {
     ctx->d_seg_state = nullptr;
     ctx->d_seg_done = nullptr;
     ctx->cap_seg_state = ctx->cap_seg_done = 0;
+}
+
+static void spec_release(fks_context* ctx) {
+    if (ctx->spec_module) {
+        (void)hipSetDevice(ctx->device);
+        (void)hipModuleUnload(ctx->spec_module);
+    }
+    ctx->spec_module = nullptr;
+    ctx->spec_fn = nullptr;
+    ctx->spec_shape.clear();
+    ctx->spec_seconds = 0.0;
+    ctx->spec_from_cache = 0;
+    ctx->spec_launches = 0;
+}
+
+/* the shape-specialised throughput kernel of the current robot: compiled (or taken from a
+ * cache), loaded on the context's device, and used only if it keeps the generic kernel's
+ * occupancy (the persistent grid is sized for that) */
+static fks_status spec_prepare(fks_context* ctx) {
+    spec_release(ctx);
+    if (!ctx->specialize || !ctx->has_robot) return FKS_OK;
+    fks_spec::Shape sh;
+    sh.type = ctx->R.type;
+    sh.L = ctx->R.L;
+    sh.J = ctx->R.J;
+    sh.D = ctx->R.D;
+    sh.W = ctx->R.W;
+    sh.G = ctx->R.G;
+    sh.P = ctx->R.P;
+    sh.pair = ctx->fk_pair ? 1 : 0;
+    sh.lean = ctx->lean ? 1 : 0;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    std::string log;
+    const std::shared_ptr<const fks_spec::CodeObject> co = fks_spec::code_object(sh, &log);
+    if (!co) return fail(ctx, FKS_ERR_UNSUPPORTED, "shape specialisation: " + log);
+    hipModule_t m = nullptr;
+    hipFunction_t f = nullptr;
+    hipError_t e = hipModuleLoadData(&m, co->bytes.data());
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipModuleLoadData (shape-specialised kernel)");
+    e = hipModuleGetFunction(&f, m, "fks_simulate_shaped");
+    if (e != hipSuccess) {
+        (void)hipModuleUnload(m);
+        return hip_fail(ctx, e, "hipModuleGetFunction(fks_simulate_shaped)");
+    }
+    /* the persistent grid is sized for the generic kernel's occupancy: the specialised kernel
+     * (same launch bounds, same LDS block) is used only if it needs no more registers.  Its
+     * count is read from the code object's metadata (the runtime's attribute query reports a
+     * different quantity for module kernels than for the library's own) */
+    const int shaped_vgpr = fks_spec::metadata_uint(co->bytes, ".vgpr_count") + fks_spec::metadata_uint(co->bytes, ".agpr_count");
+    hipFuncAttributes gen{};
+    if (hipFuncGetAttributes(&gen, reinterpret_cast<const void*>(kernel_for(ctx->R.type, false, ctx->lean))) != hipSuccess ||
+        shaped_vgpr <= 0 || shaped_vgpr > gen.numRegs) {
+        (void)hipModuleUnload(m);
+        return fail(ctx, FKS_ERR_UNSUPPORTED,
+                    "shape specialisation: the specialised kernel needs " + std::to_string(shaped_vgpr) + " VGPRs, the generic " +
+                        std::to_string(gen.numRegs));
+    }
+    ctx->spec_module = m;
+    ctx->spec_fn = f;
+    ctx->spec_shape = fks_spec::shape_key(sh);
+    ctx->spec_seconds = co->compile_seconds;
+    ctx->spec_from_cache = co->compile_seconds > 0.0 ? 0 : 1;
+    return FKS_OK;
 }
 
 extern "C" {
@@ -388,6 +463,10 @@ static fks_status create_impl(const fks_environment* henv, const fks_device_env*
     ctx->frequency = simulation_controller_frequency;
     ctx->seed = prng_seed;
     ctx->debug_level = debug_level;
+    {
+        const char* sp = std::getenv("FKS_SPECIALIZE");
+        ctx->specialize = (sp && std::string(sp) == "1") ? 1 : 0;
+    }
     std::memset(&ctx->stats, 0, sizeof(ctx->stats));
     std::memset(&ctx->last, 0, sizeof(ctx->last));
     std::memset(&ctx->total, 0, sizeof(ctx->total));
@@ -494,6 +573,7 @@ void fks_destroy(fks_context* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->pending && ctx->pending_stream) (void)hipStreamSynchronize(ctx->pending_stream);
     (void)hipDeviceSynchronize();
+    spec_release(ctx);
     free_robot(ctx);
     free_staging(ctx);
     if (ctx->d_sdf) (void)hipFree(ctx->d_sdf);
@@ -915,6 +995,13 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     }
     ctx->R = R;
     ctx->has_robot = true;
+    /* with fks_set_specialization, the new robot's shape-specialised kernel (a failure keeps the
+     * generic kernels and is reported by fks_get_specialization, not by fks_set_robot) */
+    spec_release(ctx);
+    if (ctx->specialize) {
+        const std::string keep = ctx->last_error;
+        if (spec_prepare(ctx) != FKS_OK) ctx->last_error = keep + (keep.empty() ? "" : "; ") + ctx->last_error;
+    }
     return FKS_OK;
 }
 
@@ -1105,11 +1192,20 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
      * simulation: that kernel (every particle has its wave from the start either way) */
     const bool small = ctx->small_batch && !tr && !ctx->individual_jacobians && !ctx->lean && a.nseg == 1 &&
                        n <= (uint64_t)ctx->small_grid_waves;
+    /* the plain throughput path runs the robot's shape-specialised kernel when there is one */
+    const bool shaped = ctx->spec_fn && !tr && !small && !ctx->individual_jacobians;
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
-    hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type, ctx->lean)
-                          : (small ? small_kernel_for(ctx->R.type) : kernel_for(ctx->R.type, ctx->individual_jacobians != 0, ctx->lean)),
-                       dim3(grid),
-                       dim3(64 * ctx->waves_per_group), ctx->lds_bytes, s, static_cast<const fksd::SimArgs*>(ctx->d_args));
+    if (shaped) {
+        const fksd::SimArgs* argp = ctx->d_args;
+        void* params[] = {&argp};
+        HIP_TRY(ctx, hipModuleLaunchKernel(ctx->spec_fn, grid, 1, 1, 64 * ctx->waves_per_group, 1, 1, (unsigned)ctx->lds_bytes, s,
+                                           params, nullptr));
+        ctx->spec_launches++;
+    } else {
+        hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type, ctx->lean)
+                              : (small ? small_kernel_for(ctx->R.type) : kernel_for(ctx->R.type, ctx->individual_jacobians != 0, ctx->lean)),
+                           dim3(grid), dim3(64 * ctx->waves_per_group), ctx->lds_bytes, s, static_cast<const fksd::SimArgs*>(ctx->d_args));
+    }
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_counters, ctx->d_counters, fksd::kCounterWords * sizeof(unsigned long long),
@@ -1579,6 +1675,27 @@ fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_
 fks_status fks_set_individual_jacobians(fks_context* ctx, int32_t simulate_with_individual_jacobians) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
     ctx->individual_jacobians = simulate_with_individual_jacobians ? 1 : 0;
+    return FKS_OK;
+}
+
+fks_status fks_set_specialization(fks_context* ctx, int32_t enabled) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    fks_status st = settle(ctx);
+    if (st != FKS_OK) return st;
+    ctx->specialize = enabled ? 1 : 0;
+    return spec_prepare(ctx);
+}
+
+fks_status fks_get_specialization(const fks_context* ctx, fks_specialization_info* out) {
+    if (!ctx || !out) return FKS_ERR_INVALID_ARGUMENT;
+    std::memset(out, 0, sizeof(*out));
+    out->enabled = ctx->specialize;
+    out->active = ctx->spec_fn ? 1 : 0;
+    out->from_cache = ctx->spec_from_cache;
+    out->compile_seconds = ctx->spec_seconds;
+    out->launches = ctx->spec_launches;
+    std::snprintf(out->shape, sizeof(out->shape), "%s", ctx->spec_shape.c_str());
     return FKS_OK;
 }
 

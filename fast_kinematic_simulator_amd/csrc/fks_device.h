@@ -20,7 +20,9 @@
 #ifndef FKS_DEVICE_H
 #define FKS_DEVICE_H
 
+#if !defined(__HIPCC_RTC__)
 #include <stdint.h>
+#endif
 
 #include "fks_capi.h"
 #include "fks_portable_math.h"
@@ -134,12 +136,12 @@ struct LdsLayout {
     uint32_t lean;    /* 1: no rstate here: the skip-proof cache is ScratchLayout.rstate (lean kernels) */
 };
 
-inline
+constexpr inline
 #if defined(__HIPCC__)
     __host__ __device__
 #endif
     LdsLayout make_lds_layout(int L, int J, int D, int W, int G, int NR, bool fk_pair = false, bool lean = false) {
-    LdsLayout l;
+    LdsLayout l{};
     uint32_t o = 0;
     /* shared: the robot tables the hot loops read (filled once per workgroup) */
     l.joints = o;
@@ -230,7 +232,7 @@ inline
  * others: C, N, M, V, N^T, C^T, M^-1, two products, the Gauss-Jordan tableau (2 rows^2),
  * A^-1, impulses and dv, rows = 3 (n + 1).  The reference's maps are unbounded; so is
  * this (it is sized by the robot, not capped). */
-inline
+constexpr inline
 #if defined(__HIPCC__)
     __host__ __device__
 #endif
@@ -243,12 +245,12 @@ inline
 struct ScratchLayout {
     uint64_t J, b, keys, corr, flag, cand, list, cellw, dense, rstate, total;
 };
-inline
+constexpr inline
 #if defined(__HIPCC__)
     __host__ __device__
 #endif
     ScratchLayout make_scratch_layout(uint32_t row_cap, int D, int P, int G) {
-    ScratchLayout l;
+    ScratchLayout l{};
     uint64_t o = 0;
     l.J = o;
     o += (uint64_t)row_cap * (uint64_t)(D > 0 ? D : 1);

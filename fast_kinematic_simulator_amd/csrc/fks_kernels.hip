@@ -25,8 +25,10 @@
  * transcendentals come from include/fks_portable_math.h, so results are
  * bit-identical to the CPU oracle on the same inputs.
  */
+#if !defined(__HIPCC_RTC__) /* hiprtc (fks_specialize) brings the HIP device API and the integer types itself */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "fks_capi.h"
 #include "fks_device.h"
@@ -40,6 +42,49 @@ using fks_math::dabs;
 using fks_math::dmax;
 using fks_math::dmin;
 using fks_math::dsqrt;
+
+/* ---------------- robot shape ----------------
+ * The generic kernels read the robot's dimensions and the LDS / scratch carve-outs from
+ * SimArgs at run time.  A shape-specialised build (FKS_SHAPE_L defined: fks_specialize.cpp
+ * compiles this file at run time for one robot shape) fixes the carve-outs and the link,
+ * joint, dof, width and geometry counts at compile time: every carve-out offset becomes an
+ * instruction immediate, every per-dof / per-joint loop a fixed trip count, and the kernel
+ * keeps far fewer wave-uniform values live in SGPRs (the SGPR spills of the generic kernel
+ * cost one VALU lane read each).  The point, round and pair counts stay run-time values:
+ * unrolling the point loops made the kernel larger and slower.  Same expression trees,
+ * same results, bit for bit. */
+#if defined(FKS_SHAPE_L)
+struct RobotShape {
+    int L, J, D, W, G;
+};
+constexpr RobotShape kShape{FKS_SHAPE_L, FKS_SHAPE_J, FKS_SHAPE_D, FKS_SHAPE_W, FKS_SHAPE_G};
+constexpr LdsLayout kShapeLayout = make_lds_layout(FKS_SHAPE_L, FKS_SHAPE_J, FKS_SHAPE_D, FKS_SHAPE_W, FKS_SHAPE_G,
+                                                   (FKS_SHAPE_P + 63) / 64, FKS_SHAPE_PAIR != 0, FKS_SHAPE_LEAN != 0);
+constexpr ScratchLayout kShapeScratch = make_scratch_layout(3u * FKS_SHAPE_P, FKS_SHAPE_D, FKS_SHAPE_P, FKS_SHAPE_G);
+#define RDIM(r, f) FKS_RDIM_##f(r)
+#define FKS_RDIM_L(r) (::fksd::kShape.L)
+#define FKS_RDIM_J(r) (::fksd::kShape.J)
+#define FKS_RDIM_D(r) (::fksd::kShape.D)
+#define FKS_RDIM_W(r) (::fksd::kShape.W)
+#define FKS_RDIM_G(r) (::fksd::kShape.G)
+#define FKS_RDIM_P(r) ((r).P)
+#define FKS_RDIM_nrounds(r) ((r).nrounds)
+#define FKS_RDIM_npairs(r) ((r).npairs)
+#define FKS_RDIM_self_possible(r) ((r).self_possible)
+#define LAY(a) (::fksd::kShapeLayout)
+#define SLAY(a) (::fksd::kShapeScratch)
+#define ROWCAP(a) (3u * (uint32_t)FKS_SHAPE_P)
+/* with the per-dof / per-joint loops unrolled, the functions that take the wave's Sim state
+ * grow past the inliner's threshold; an out-of-line one would put Sim in memory and turn
+ * every LDS access into a flat one and every argument read into a vector load */
+#define FKS_SHAPE_INLINE __forceinline__
+#else
+#define FKS_SHAPE_INLINE
+#define RDIM(r, f) ((r).f)
+#define LAY(a) ((a).L)
+#define SLAY(a) ((a).SL)
+#define ROWCAP(a) ((a).row_cap)
+#endif
 
 struct D3 {
     double x, y, z;
@@ -301,7 +346,7 @@ __device__ double sampled_pick(uint32_t k0, uint32_t k1, uint64_t particle, uint
  * floor(64 / D) microsteps are drawn at once, one lane per (microstep, dof), into LDS;
  * noise_sample() consumes them (and their error bits) in the DOF lanes. */
 struct Sim;
-__device__ void refill_noise(Sim& s, uint32_t micro0, uint32_t M);
+__device__ FKS_SHAPE_INLINE void refill_noise(Sim& s, uint32_t micro0, uint32_t M);
 __device__ __forceinline__ double noise_sample(Sim& s, uint32_t micro);
 
 /* ---------------- grids ---------------- */
@@ -361,7 +406,7 @@ __device__ __forceinline__ int opaque_lane(int ln) {
 
 /* wave totals of the self-collision branch (kCntSelfChecks, kCntSelfPoints), kept in the
  * wave's LDS block (misc + 28, + 29) rather than in registers: the branch is rare */
-__device__ __forceinline__ uint64_t* self_counters(const Sim& s) { return reinterpret_cast<uint64_t*>(s.lds + s.A->L.misc + 28); }
+__device__ __forceinline__ uint64_t* self_counters(const Sim& s) { return reinterpret_cast<uint64_t*>(s.lds + LAY(*s.A).misc + 28); }
 
 /* ForwardSimulationStepTrace records (traced kernel instantiations only) */
 template <bool TR>
@@ -371,7 +416,7 @@ __device__ __forceinline__ void trace_config(Sim& s, const double* cfg, uint32_t
         const uint32_t k = s.tr_cfgs++;
         if (k < A.tr_cfg_cap) {
             const uint64_t rec = s.local * (uint64_t)A.tr_cfg_cap + k;
-            if (s.lane < A.R.W) A.tr_cfg[rec * (uint64_t)A.R.W + s.lane] = cfg[s.lane];
+            if (s.lane < RDIM(A.R, W)) A.tr_cfg[rec * (uint64_t)RDIM(A.R, W) + s.lane] = cfg[s.lane];
             if (s.lane == 0) {
                 A.tr_tags[3 * rec] = s.step;
                 A.tr_tags[3 * rec + 1] = micro;
@@ -386,7 +431,7 @@ __device__ __forceinline__ void trace_step(Sim& s, const double* u, const double
         const SimArgs& A = *s.A;
         const uint32_t k = s.tr_steps++;
         if (k < A.tr_step_cap) {
-            const int D = A.R.D;
+            const int D = RDIM(A.R, D);
             const uint64_t rec = s.local * (uint64_t)A.tr_step_cap + k;
             if (s.lane < D) {
                 A.tr_inputs[rec * 2ull * (uint64_t)D + s.lane] = u[s.lane];
@@ -419,10 +464,10 @@ __device__ __forceinline__ void count_event(Sim& s, int slot, uint64_t n) {
 __device__ __noinline__ void refill_noise_lanes(const SimArgs* __restrict__ Ap, double* lds, int ln, uint64_t pid, uint32_t step,
                                                 uint32_t micro0, uint32_t M) {
     const SimArgs& A = *Ap;
-    const int D = A.R.D;
+    const int D = RDIM(A.R, D);
     const int per = kWave / D;
-    double* nz = lds + A.L.noise;
-    uint32_t* ne = reinterpret_cast<uint32_t*>(lds + A.L.noise_err);
+    double* nz = lds + LAY(A).noise;
+    uint32_t* ne = reinterpret_cast<uint32_t*>(lds + LAY(A).noise_err);
     if (ln < per * D) {
         const uint32_t m = micro0 + (uint32_t)(ln / D);
         if (m < M) {
@@ -437,15 +482,15 @@ __device__ __noinline__ void refill_noise_lanes(const SimArgs* __restrict__ Ap, 
     }
     wsync();
 }
-__device__ void refill_noise(Sim& s, uint32_t micro0, uint32_t M) {
+__device__ FKS_SHAPE_INLINE void refill_noise(Sim& s, uint32_t micro0, uint32_t M) {
     refill_noise_lanes(s.A, s.lds, s.lane, s.pid, s.step, micro0, M);
 }
 __device__ __forceinline__ double noise_sample(Sim& s, uint32_t micro) {
     const SimArgs& A = *s.A;
-    const int D = A.R.D;
+    const int D = RDIM(A.R, D);
     const int slot = (int)(micro % (uint32_t)(kWave / D)) * D + s.lane;
-    s.err |= reinterpret_cast<const uint32_t*>(s.lds + A.L.noise_err)[slot];
-    return s.lds[A.L.noise + slot];
+    s.err |= reinterpret_cast<const uint32_t*>(s.lds + LAY(A).noise_err)[slot];
+    return s.lds[LAY(A).noise + slot];
 }
 
 /* sdf_tools EstimateDistance4d (same spec as oracle SDF::EstimateDistance4d) */
@@ -534,13 +579,13 @@ __device__ __forceinline__ D4 load_point(const RobotDev& R, int i) {
 
 /* ---------------- forward kinematics: cfg (LDS) -> link transforms T (LDS) ---------------- */
 template <int RT>
-__device__ void fk(Sim& s, const double* cfg, double* T) {
+__device__ FKS_SHAPE_INLINE void fk(Sim& s, const double* cfg, double* T) {
     const RobotDev& R = s.A->R;
     const int ln = s.lane;
     if constexpr (RT == FKS_ROBOT_LINKED) {
-        double* jm = s.lds + s.A->L.jm;
+        double* jm = s.lds + LAY(*s.A).jm;
         const JointDev* JD = s.joints;
-        if (ln < R.J) {
+        if (ln < RDIM(R, J)) {
             const JointDev& jd = JD[ln];
             if (jd.type == FKS_JOINT_REVOLUTE || jd.type == FKS_JOINT_CONTINUOUS) {
                 double M[12];
@@ -567,7 +612,7 @@ __device__ void fk(Sim& s, const double* cfg, double* T) {
         double p0 = dpp_f64<kDppQuadBcast0>(own), p1 = dpp_f64<kDppQuadBcast1>(own), p2 = dpp_f64<kDppQuadBcast2>(own),
                p3 = dpp_f64<kDppQuadBcast3>(own);
         int last = 0;
-        const int J = R.J;
+        const int J = RDIM(R, J);
         /* the joint's origin / motion columns are read at the top of its iteration (no
          * prefetch registers to rotate: the other waves of the SIMD hide the LDS latency) */
         for (int j = 0; j < J; ++j) {
@@ -620,16 +665,16 @@ __device__ void fk(Sim& s, const double* cfg, double* T) {
  * runs on lanes 0-11 and the chain of cfgB on lanes 16-27 (quads 0-2 and 4-6), their
  * joint motion matrices on lanes j and 32 + j.  Every instruction of the chain serves
  * both, so the pair costs about one FK; each chain is the same arithmetic as fk(). */
-__device__ void fk_pair(Sim& s, const double* cfgA, double* TA, const double* cfgB, double* TB) {
+__device__ FKS_SHAPE_INLINE void fk_pair(Sim& s, const double* cfgA, double* TA, const double* cfgB, double* TB) {
     const RobotDev& R = s.A->R;
     const int ln = s.lane;
-    double* jmA = s.lds + s.A->L.jm;
-    double* jmB = s.lds + s.A->L.jm2;
+    double* jmA = s.lds + LAY(*s.A).jm;
+    double* jmB = s.lds + LAY(*s.A).jm2;
     const JointDev* JD = s.joints;
     {
         const int j = ln & 31;
         const bool second = ln >= 32;
-        if (j < R.J) {
+        if (j < RDIM(R, J)) {
             const JointDev& jd = JD[j];
             const double* cfg = second ? cfgB : cfgA;
             double* jm = second ? jmB : jmA;
@@ -659,7 +704,7 @@ __device__ void fk_pair(Sim& s, const double* cfgA, double* TA, const double* cf
     double p0 = dpp_f64<kDppQuadBcast0>(own), p1 = dpp_f64<kDppQuadBcast1>(own), p2 = dpp_f64<kDppQuadBcast2>(own),
            p3 = dpp_f64<kDppQuadBcast3>(own);
     int last = 0;
-    const int J = R.J;
+    const int J = RDIM(R, J);
     for (int j = 0; j < J; ++j) {
         const int parent = __builtin_amdgcn_readfirstlane(JD[j].parent);
         const int child = __builtin_amdgcn_readfirstlane(JD[j].child);
@@ -716,12 +761,12 @@ __device__ __forceinline__ double actuator_noisy(Sim& s, const fks_dof_controlle
 /* ---------------- robot control-input application (TNUVA ApplyControlInput) ----------------
  * cfg_out = apply(cfg_in, input) with clamp (+ noise if noisy).  Lane d < D owns dof d. */
 template <int RT>
-__device__ void apply_input(Sim& s, const double* cfg_in, const double* input, double* cfg_out, bool noisy, uint32_t micro) {
+__device__ FKS_SHAPE_INLINE void apply_input(Sim& s, const double* cfg_in, const double* input, double* cfg_out, bool noisy, uint32_t micro) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const int ln = s.lane;
     if constexpr (RT == FKS_ROBOT_LINKED) {
-        if (ln < R.D) {
+        if (ln < RDIM(R, D)) {
             const fks_dof_controller& ct = s.ctrl[ln];
             const double vmax = dabs(ct.velocity_limit);
             double real = clamp(input[ln], -vmax, vmax);
@@ -751,7 +796,7 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
         }
         wsync();
     } else {
-        double* tw = s.lds + s.A->L.misc; /* 6 doubles */
+        double* tw = s.lds + LAY(*s.A).misc; /* 6 doubles */
         if (ln < 6) {
             const fks_dof_controller& ct = s.ctrl[ln];
             const double vmax = dabs(ct.velocity_limit);
@@ -777,13 +822,13 @@ __device__ void apply_input(Sim& s, const double* cfg_in, const double* input, d
 
 /* GenerateControlAction (TNUVA:179-198, 384-412, 598-614): lane d < D returns u_d */
 template <int RT>
-__device__ double control_action(Sim& s, const double* cfg, const double* target) {
+__device__ FKS_SHAPE_INLINE double control_action(Sim& s, const double* cfg, const double* target) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const int ln = s.lane;
     double err = 0.0;
     if constexpr (RT == FKS_ROBOT_LINKED) {
-        if (ln < R.D) {
+        if (ln < RDIM(R, D)) {
             const JointDev& jd = s.joints[s.dofj[ln]];
             if (jd.type == FKS_JOINT_CONTINUOUS)
                 err = fks_math::enforce_continuous_revolute_bounds(target[ln] - cfg[ln]);
@@ -808,7 +853,7 @@ __device__ double control_action(Sim& s, const double* cfg, const double* target
         if (ln < 6) err = e;
     }
     double u = 0.0;
-    if (ln < R.D) {
+    if (ln < RDIM(R, D)) {
         const fks_dof_controller& ct = s.ctrl[ln];
         /* SimplePIDController::ComputeFeedbackTerm (PID:122-135), gains made positive (PID:104-113) */
         const double kp = dabs(ct.kp), ki = dabs(ct.ki), kd = dabs(ct.kd), iclamp = dabs(ct.integral_clamp);
@@ -827,11 +872,11 @@ __device__ double control_action(Sim& s, const double* cfg, const double* target
 
 /* configuration distance for the simulation shortcut (SPCS:898) */
 template <int RT>
-__device__ double config_distance(Sim& s, const double* cfg, const double* target) {
+__device__ FKS_SHAPE_INLINE double config_distance(Sim& s, const double* cfg, const double* target) {
     const RobotDev& R = s.A->R;
     if constexpr (RT == FKS_ROBOT_LINKED) {
         double sum = 0.0;
-        for (int k = 0; k < R.D; ++k) {
+        for (int k = 0; k < RDIM(R, D); ++k) {
             const JointDev& jd = s.joints[s.dofj[k]];
             const double sd = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(target[k] - cfg[k])
                                                                 : target[k] - cfg[k];
@@ -939,9 +984,9 @@ enum { kSkipCheck = 1, kSkipCorrections = 2 };
 /* (link, radius) of round r < 64 from the workgroup's LDS copy of R.rounds */
 __device__ __forceinline__ RoundDev lds_round(const Sim& s, int r) {
     RoundDev o;
-    o.link = (int32_t)s.shared[s.A->L.rounds + 2 * r];
+    o.link = (int32_t)s.shared[LAY(*s.A).rounds + 2 * r];
     o.npts = 0;
-    o.radius = s.shared[s.A->L.rounds + 2 * r + 1];
+    o.radius = s.shared[LAY(*s.A).rounds + 2 * r + 1];
     return o;
 }
 
@@ -953,7 +998,7 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
     if (!A.skip_enabled) return 0ull;
     bool sk = false;
     const int ln = s.lane;
-    if (ln < R.nrounds) {
+    if (ln < RDIM(R, nrounds)) {
         const RoundDev rd = lds_round(s, ln);
         const double* st = s.rstate + kRoundState * ln;
         if (rd.link >= 0 && st[12] > kInvalidRound) {
@@ -982,7 +1027,7 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
 /* cache the state of round r after a full evaluation at T (uniform call) */
 __device__ __forceinline__ void round_update(Sim& s, int r, const double* T, double S, double G, double C) {
     const SimArgs& A = *s.A;
-    if (!A.skip_enabled || r >= kWave || r >= A.R.nrounds) return;
+    if (!A.skip_enabled || r >= kWave || r >= RDIM(A.R, nrounds)) return;
     const RoundDev rd = lds_round(s, r);
     if (rd.link < 0) return;
     const double smin = wave_min(S), gmin = wave_min(G), cmin = wave_min(C);
@@ -1000,16 +1045,16 @@ __device__ __forceinline__ void round_update(Sim& s, int r, const double* T, dou
  * cannot reach the max of the round with the largest bound are not evaluated. */
 __device__ __forceinline__ double round_max_motion(const RobotDev& R, const double* TA, const double* TB, int r, int ln) {
     const int i = kWave * r + ln;
-    if (i >= R.P) return 0.0;
+    if (i >= RDIM(R, P)) return 0.0;
     const D4 p = load_point(R, i);
     const int link = gp(R.point_link)[i];
     const D4 a = xform4(TA + 12 * link, p), b = xform4(TB + 12 * link, p);
     return sqnorm4(D4{b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w});
 }
-__device__ double max_point_motion(Sim& s, const double* TA, const double* TB) {
+__device__ FKS_SHAPE_INLINE double max_point_motion(Sim& s, const double* TA, const double* TB) {
     const RobotDev& R = s.A->R;
     const int ln = s.lane;
-    const int nr = R.nrounds;
+    const int nr = RDIM(R, nrounds);
     double m = 0.0;
     if (nr <= 2 || nr > kWave) {
 #pragma unroll 2
@@ -1045,7 +1090,7 @@ __device__ double max_point_motion(Sim& s, const double* TA, const double* TB) {
 __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int i, uint64_t* b, double* S, double* G,
                                           double* C) {
     const RobotDev& R = A.R;
-    if (i >= R.P) return false;
+    if (i >= RDIM(R, P)) return false;
     const D4 p = load_point(R, i);
     const int link = gp(R.point_link)[i];
     const D4 x = xform4(T + 12 * link, p);
@@ -1091,21 +1136,21 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
  * colliding point; algorithmic bytes are counted up to that point, as the reference
  * reads them (its loop returns at the first colliding point).  Provably-free rounds
  * are not read but still counted (4 B per point, all in bounds). */
-__device__ bool env_collision(Sim& s, const double* T) {
+__device__ FKS_SHAPE_INLINE bool env_collision(Sim& s, const double* T) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const uint64_t skip = skippable_rounds(s, T, kSkipCheck);
     /* every round proven free (the common microstep): the reference reads 4 bytes per
      * point and finds nothing; account those reads without walking the rounds */
-    if (R.nrounds <= kWave) {
-        const uint64_t all = (R.nrounds == kWave) ? ~0ull : ((1ull << R.nrounds) - 1ull);
+    if (RDIM(R, nrounds) <= kWave) {
+        const uint64_t all = (RDIM(R, nrounds) == kWave) ? ~0ull : ((1ull << RDIM(R, nrounds)) - 1ull);
         if ((skip & all) == all) {
-            if (s.lane < R.P) s.lane_bytes += 4ull * (uint64_t)((R.P - s.lane + kWave - 1) / kWave);
-            count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (uint64_t)R.nrounds);
+            if (s.lane < RDIM(R, P)) s.lane_bytes += 4ull * (uint64_t)((RDIM(R, P) - s.lane + kWave - 1) / kWave);
+            count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (uint64_t)RDIM(R, nrounds));
             return false;
         }
     }
-    for (int base = 0, r = 0; base < R.P; base += 2 * kWave, r += 2) {
+    for (int base = 0, r = 0; base < RDIM(R, P); base += 2 * kWave, r += 2) {
         const bool sk0 = r < kWave && ((skip >> r) & 1ull);
         const bool sk1 = r + 1 < kWave && ((skip >> (r + 1)) & 1ull);
         uint64_t b0 = 0, b1 = 0;
@@ -1114,17 +1159,17 @@ __device__ bool env_collision(Sim& s, const double* T) {
         bool c0 = false, c1 = false;
         const int i0 = base + s.lane, i1 = base + kWave + s.lane;
         if (sk0)
-            b0 = (i0 < R.P) ? 4 : 0;
+            b0 = (i0 < RDIM(R, P)) ? 4 : 0;
         else
             c0 = env_point(A, T, i0, &b0, &S0, &G0, &C0);
         if (sk1)
-            b1 = (i1 < R.P) ? 4 : 0;
+            b1 = (i1 < RDIM(R, P)) ? 4 : 0;
         else
             c1 = env_point(A, T, i1, &b1, &S1, &G1, &C1);
         if (!sk0) round_update(s, r, T, S0, G0, C0);
-        if (!sk1 && base + kWave < R.P) round_update(s, r + 1, T, S1, G1, C1);
-        count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (sk0 ? 1 : 0) + ((sk1 && base + kWave < R.P) ? 1 : 0));
-        count_event(s, FKS_PHASE_ENV_ROUNDS_EVALUATED, (sk0 ? 0 : 1) + ((!sk1 && base + kWave < R.P) ? 1 : 0));
+        if (!sk1 && base + kWave < RDIM(R, P)) round_update(s, r + 1, T, S1, G1, C1);
+        count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (sk0 ? 1 : 0) + ((sk1 && base + kWave < RDIM(R, P)) ? 1 : 0));
+        count_event(s, FKS_PHASE_ENV_ROUNDS_EVALUATED, (sk0 ? 0 : 1) + ((!sk1 && base + kWave < RDIM(R, P)) ? 1 : 0));
         const uint64_t m0 = __ballot(c0);
         const uint64_t m1 = __ballot(c1);
         if (m0) {
@@ -1337,15 +1382,15 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
                                                        uint32_t err, const double* Tp, const double* Tc);
 
 /* CollectSelfCollisions: returns whether the self-collision map is non-empty */
-__device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
+__device__ FKS_SHAPE_INLINE bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const int ln = s.lane;
-    if (!R.self_possible) return false;
-    double* box = s.lds + s.A->L.box;
+    if (!RDIM(R, self_possible)) return false;
+    double* box = s.lds + LAY(*s.A).box;
     bool bad = false;
-    if (ln < R.G) {
-        const double* gb = s.shared + A.L.gbox + 8 * ln;
+    if (ln < RDIM(R, G)) {
+        const double* gb = s.shared + LAY(A).gbox + 8 * ln;
         const int link = (int)gb[7];
         const double* T = Tc + 12 * link;
         double lo[3], hi[3];
@@ -1384,8 +1429,8 @@ __device__ bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
     }
     wsync();
     bool any = false;
-    const uint32_t* lpairs = reinterpret_cast<const uint32_t*>(s.shared + A.L.gpairs);
-    for (int k = ln; k < R.npairs; k += kWave) {
+    const uint32_t* lpairs = reinterpret_cast<const uint32_t*>(s.shared + LAY(A).gpairs);
+    for (int k = ln; k < RDIM(R, npairs); k += kWave) {
         int a, b;
         if (k < kLdsPairs) {
             const uint32_t ab = lpairs[k];
@@ -1411,7 +1456,7 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
                                                        uint32_t err, const double* Tp, const double* Tc) {
     const SimArgs& A = *Ap;
     const RobotDev& R = A.R;
-    const double* box = lds + A.L.box;
+    const double* box = lds + LAY(A).box;
     /* exact path: extended cell keys (SPCS:1173-1181: division, trunc).  The keys are
      * needed for the points of the geometries in a box-overlapping pair; every other
      * point's key only matters once some cell is shared, so it is computed then. */
@@ -1420,7 +1465,7 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
     double* flag = scratch + SL.flag;
     double* cand = scratch + SL.cand;
     int32_t* list = reinterpret_cast<int32_t*>(scratch + SL.list);
-    int32_t* listb = list + R.P; /* second half of the list region: one pair's b points */
+    int32_t* listb = list + RDIM(R, P); /* second half of the list region: one pair's b points */
     auto key_point = [&](int i) {
         const D4 p = load_point(R, i);
         const int link = gp(R.point_link)[i];
@@ -1460,13 +1505,13 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
     };
     /* geometries of the overlapping pairs; every geometry when a box is not finite (the
      * key-range error is then raised exactly as a pass over all points would) */
-    const bool unbounded = wave_any(ln < R.G && !(box[6 * ln] > -__builtin_huge_val()));
+    const bool unbounded = wave_any(ln < RDIM(R, G) && !(box[6 * ln] > -__builtin_huge_val()));
     uint64_t need = 0ull;
-    for (int k0 = 0; k0 < R.npairs; k0 += kWave) {
+    for (int k0 = 0; k0 < RDIM(R, npairs); k0 += kWave) {
         const int k = k0 + ln;
         int a = 0, b = 0;
         bool ov = false;
-        if (k < R.npairs) {
+        if (k < RDIM(R, npairs)) {
             a = gp(R.pairs)[2 * k];
             b = gp(R.pairs)[2 * k + 1];
             ov = overlap(a, b);
@@ -1479,7 +1524,7 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
         }
     }
     uint64_t done = 0ull;
-    for (int g = 0; g < R.G; ++g) {
+    for (int g = 0; g < RDIM(R, G); ++g) {
         if (!unbounded && !((need >> g) & 1ull)) continue;
         done |= 1ull << g;
         for (int i = (int)gp(R.geom_off)[g] + ln; i < (int)gp(R.geom_off)[g + 1]; i += kWave) key_point(i);
@@ -1489,7 +1534,7 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
      * cell only with the points of b whose keys lie in a's box (and only if its own key
      * lies in b's box), so b's points are first compacted to that list */
     bool any_cand = false;
-    for (int k = 0; k < R.npairs; ++k) {
+    for (int k = 0; k < RDIM(R, npairs); ++k) {
         const int a = gp(R.pairs)[2 * k], b = gp(R.pairs)[2 * k + 1];
         if (!overlap(a, b)) continue;
         const int a0 = (int)gp(R.geom_off)[a], a1 = (int)gp(R.geom_off)[a + 1];
@@ -1524,21 +1569,21 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
         return err << 1;
     }
     /* some cell is shared: the cell members below come from every point */
-    for (int g = 0; g < R.G; ++g) {
+    for (int g = 0; g < RDIM(R, G); ++g) {
         if ((done >> g) & 1ull) continue;
         for (int i = (int)gp(R.geom_off)[g] + ln; i < (int)gp(R.geom_off)[g + 1]; i += kWave) key_point(i);
     }
     wsync();
     /* process each candidate cell once */
-    uint32_t* ui = reinterpret_cast<uint32_t*>(reinterpret_cast<int32_t*>(lds + A.L.ints) + 2 * kMaxDofs); /* spare int words */
+    uint32_t* ui = reinterpret_cast<uint32_t*>(reinterpret_cast<int32_t*>(lds + LAY(A).ints) + 2 * kMaxDofs); /* spare int words */
     if (ln == 0) {
         ui[0] = 0; /* colliding cells */
         ui[1] = 0; /* any corrected point */
     }
     wsync();
-    for (int base = 0; base < R.P; base += kWave) {
+    for (int base = 0; base < RDIM(R, P); base += kWave) {
         const int i0 = base + ln;
-        uint64_t m = __ballot(i0 < R.P && cand[i0] != 0.0);
+        uint64_t m = __ballot(i0 < RDIM(R, P) && cand[i0] != 0.0);
         while (m) {
             const int bit = __ffsll((unsigned long long)m) - 1;
             m &= m - 1ull;
@@ -1547,9 +1592,9 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
             const int64_t kx = keys[3 * ci], ky = keys[3 * ci + 1], kz = keys[3 * ci + 2];
             /* members of the cell in point order */
             int count = 0;
-            for (int b2 = 0; b2 < R.P; b2 += kWave) {
+            for (int b2 = 0; b2 < RDIM(R, P); b2 += kWave) {
                 const int j = b2 + ln;
-                const bool in = j < R.P && keys[3 * j] == kx && keys[3 * j + 1] == ky && keys[3 * j + 2] == kz;
+                const bool in = j < RDIM(R, P) && keys[3 * j] == kx && keys[3 * j + 1] == ky && keys[3 * j + 2] == kz;
                 const uint64_t mm = __ballot(in);
                 if (in) {
                     const int rank = __popcll(mm & ((1ull << ln) - 1ull));
@@ -1566,14 +1611,14 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
         }
     }
     bool nonempty = false;
-    for (int i = ln; i < R.P; i += kWave) nonempty = nonempty || (flag[i] != 0.0);
+    for (int i = ln; i < RDIM(R, P); i += kWave) nonempty = nonempty || (flag[i] != 0.0);
     err = wave_or(err);
     return (err << 1) | (wave_any(nonempty) ? 1u : 0u);
 }
 
 /* CheckCollision (SPCS:1418-1436) */
 template <int RT>
-__device__ bool check_collision(Sim& s, const double* Tp, const double* Tc) {
+__device__ FKS_SHAPE_INLINE bool check_collision(Sim& s, const double* Tp, const double* Tc) {
     uint64_t t0 = tick();
     const bool env = env_collision(s, Tc);
     tock(s, FKS_PHASE_ENV_CHECK, t0);
@@ -1590,15 +1635,15 @@ __device__ bool check_collision(Sim& s, const double* Tp, const double* Tc) {
 
 /* world joint axes/origins per dof for the Jacobian (linked robots) */
 template <int RT>
-__device__ void joint_frames(Sim& s, const double* Tc) {
+__device__ FKS_SHAPE_INLINE void joint_frames(Sim& s, const double* Tc) {
     const RobotDev& R = s.A->R;
     const int ln = s.lane;
-    if (RT == FKS_ROBOT_LINKED && ln < R.D) {
+    if (RT == FKS_ROBOT_LINKED && ln < RDIM(R, D)) {
         const JointDev& jd = s.joints[s.dofj[ln]];
         const double* Tch = Tc + 12 * jd.child;
         const D3 aw = rotate(Tch, D3{jd.axis[0], jd.axis[1], jd.axis[2]});
-        double* axw = s.lds + s.A->L.axis_w;
-        double* orw = s.lds + s.A->L.orig_w;
+        double* axw = s.lds + LAY(*s.A).axis_w;
+        double* orw = s.lds + LAY(*s.A).orig_w;
         axw[3 * ln + 0] = aw.x;
         axw[3 * ln + 1] = aw.y;
         axw[3 * ln + 2] = aw.z;
@@ -1611,38 +1656,38 @@ __device__ void joint_frames(Sim& s, const double* Tc) {
 
 /* CollectPointCorrectionsAndJacobians (SPCS:1818-1939): rows written to scratch, returns R */
 template <int RT>
-__device__ uint32_t collect_corrections(Sim& s, const double* Tp, const double* Tc, const double* cfg) {
+__device__ FKS_SHAPE_INLINE uint32_t collect_corrections(Sim& s, const double* Tp, const double* Tc, const double* cfg) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const int ln = s.lane;
-    const int D = R.D;
+    const int D = RDIM(R, D);
     const ScratchLayout& SL = A.SL;
     FKS_GLOBAL double* J = gpw(s.scratch) + SL.J;
     FKS_GLOBAL double* bv = gpw(s.scratch) + SL.b;
     const FKS_GLOBAL double* corr = gp(s.scratch) + SL.corr;
     const FKS_GLOBAL double* flag = gp(s.scratch) + SL.flag;
-    const uint32_t rc = A.row_cap;
+    const uint32_t rc = ROWCAP(A);
     joint_frames<RT>(s, Tc);
-    const double* axw = s.lds + s.A->L.axis_w;
-    const double* orw = s.lds + s.A->L.orig_w;
+    const double* axw = s.lds + LAY(*s.A).axis_w;
+    const double* orw = s.lds + LAY(*s.A).orig_w;
     uint32_t rows = 0;
     /* rounds that provably hold no corrected point: their EstimateDistance reads are
      * counted (28 B per point, in bounds) but not made */
     const uint64_t skip = skippable_rounds(s, Tc, kSkipCorrections);
-    for (int base = 0; base < R.P; base += kWave) {
+    for (int base = 0; base < RDIM(R, P); base += kWave) {
         const int i = base + ln;
         const int r = base / kWave;
         const bool skr = r < kWave && ((skip >> r) & 1ull);
         count_event(s, skr ? FKS_PHASE_CORR_ROUNDS_SKIPPED : FKS_PHASE_CORR_ROUNDS_EVALUATED, 1);
         if (skr && !s.self_nonempty) {
-            if (i < R.P) s.lane_bytes += 28;
+            if (i < RDIM(R, P)) s.lane_bytes += 28;
             continue;
         }
         bool has = false;
         D3 pcorr{0.0, 0.0, 0.0};
         D4 xc{0.0, 0.0, 0.0, 0.0};
         int link = 0;
-        if (i < R.P) {
+        if (i < RDIM(R, P)) {
             const D4 p = load_point(R, i);
             link = gp(R.point_link)[i];
             xc = xform4(Tc + 12 * link, p);
@@ -1747,13 +1792,13 @@ template <int DM>
 __device__ __noinline__ void qr_solve_regs(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
                                            uint32_t Rn, double* x) {
     const SimArgs& A = *Ap;
-    const int D = A.R.D;
-    const uint32_t rc = A.row_cap;
-    const FKS_GLOBAL double* Jm = gp(scratch) + A.SL.J;
-    const FKS_GLOBAL double* bv = gp(scratch) + A.SL.b;
-    double* colsq = lds + A.L.colsq;
-    double* hco = lds + A.L.hcoef;
-    int32_t* perm = reinterpret_cast<int32_t*>(lds + A.L.ints);
+    const int D = RDIM(A.R, D);
+    const uint32_t rc = ROWCAP(A);
+    const FKS_GLOBAL double* Jm = gp(scratch) + SLAY(A).J;
+    const FKS_GLOBAL double* bv = gp(scratch) + SLAY(A).b;
+    double* colsq = lds + LAY(A).colsq;
+    double* hco = lds + LAY(A).hcoef;
+    int32_t* perm = reinterpret_cast<int32_t*>(lds + LAY(A).ints);
     int32_t* transp = perm + kMaxDofs;
     const bool has = (uint32_t)ln < Rn;
     double a[DM];
@@ -2179,11 +2224,11 @@ template <int RM>
 __device__ __forceinline__ void qr_solve_cols_body(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
                                                    uint32_t Rn, double* x, uint32_t row0) {
     const SimArgs& A = *Ap;
-    const int D = A.R.D;
-    const uint32_t rc = A.row_cap;
-    const FKS_GLOBAL double* Jm = gp(scratch) + A.SL.J + row0; /* rows [row0, row0 + Rn) */
-    const FKS_GLOBAL double* bv = gp(scratch) + A.SL.b + row0;
-    int32_t* perm = reinterpret_cast<int32_t*>(lds + A.L.ints);
+    const int D = RDIM(A.R, D);
+    const uint32_t rc = ROWCAP(A);
+    const FKS_GLOBAL double* Jm = gp(scratch) + SLAY(A).J + row0; /* rows [row0, row0 + Rn) */
+    const FKS_GLOBAL double* bv = gp(scratch) + SLAY(A).b + row0;
+    int32_t* perm = reinterpret_cast<int32_t*>(lds + LAY(A).ints);
     int32_t* transp = perm + kMaxDofs;
     const bool isc = ln < D, isb = ln == D;
     double a[RM];
@@ -2352,15 +2397,15 @@ __device__ __forceinline__ void qr_solve_cols_body(const SimArgs* __restrict__ A
 template <int RM>
 __device__ __noinline__ void qr_solve_cols(const SimArgs* __restrict__ Ap, double* lds, const double* scratch, int ln,
                                            uint32_t Rn, double* x, uint32_t row0 = 0) {
-    if (Ap->R.D <= 7) {
+    if (RDIM(Ap->R, D) <= 7) {
         /* <= 7 columns: the 8 x 8 tile (qr_solve_tile), same arithmetic */
-        const FKS_GLOBAL double* Jm = gp(scratch) + Ap->SL.J + row0;
-        const FKS_GLOBAL double* bv = gp(scratch) + Ap->SL.b + row0;
-        int32_t* perm = reinterpret_cast<int32_t*>(lds + Ap->L.ints);
+        const FKS_GLOBAL double* Jm = gp(scratch) + SLAY(*Ap).J + row0;
+        const FKS_GLOBAL double* bv = gp(scratch) + SLAY(*Ap).b + row0;
+        int32_t* perm = reinterpret_cast<int32_t*>(lds + LAY(*Ap).ints);
         if constexpr (RM <= 8)
-            qr_solve_tile<8, 1>(Jm, bv, perm, Ap->R.D, Ap->row_cap, ln, Rn, x);
+            qr_solve_tile<8, 1>(Jm, bv, perm, RDIM(Ap->R, D), ROWCAP(*Ap), ln, Rn, x);
         else
-            qr_solve_tile<8, 2>(Jm, bv, perm, Ap->R.D, Ap->row_cap, ln, Rn, x);
+            qr_solve_tile<8, 2>(Jm, bv, perm, RDIM(Ap->R, D), ROWCAP(*Ap), ln, Rn, x);
         return;
     }
     /* (16 columns of 4-row blocks for 8-15 dofs measured 2-3 % slower on cfg5, 14 dofs, than
@@ -2379,14 +2424,14 @@ __device__ __noinline__ void qr_solve_cols(const SimArgs* __restrict__ Ap, doubl
 __device__ __noinline__ void qr_solve(const SimArgs* __restrict__ Ap, double* lds, double* scratch, int ln, uint32_t Rn, double* x,
                                       uint32_t row0 = 0) {
     const SimArgs& A = *Ap;
-    const int D = A.R.D;
-    const uint32_t rc = A.row_cap;
+    const int D = RDIM(A.R, D);
+    const uint32_t rc = ROWCAP(A);
     const ScratchLayout& SL = A.SL;
     double* Jm = scratch + SL.J + row0;
     double* c = scratch + SL.b + row0;
-    double* colsq = lds + A.L.colsq;
-    double* hco = lds + A.L.hcoef;
-    int32_t* perm = reinterpret_cast<int32_t*>(lds + A.L.ints);
+    double* colsq = lds + LAY(A).colsq;
+    double* hco = lds + LAY(A).hcoef;
+    int32_t* perm = reinterpret_cast<int32_t*>(lds + LAY(A).ints);
     int32_t* transp = perm + kMaxDofs;
     auto col = [&](int k) { return Jm + (uint64_t)k * rc; };
     /* canonical tail squared norm of column k over rows [begin, Rn) */
@@ -2563,8 +2608,8 @@ __device__ __noinline__ void qr_solve(const SimArgs* __restrict__ Ap, double* ld
  * No corrected point: the zero step (as the stacked solve of an empty system). */
 __device__ __noinline__ void individual_jacobians_solve(Sim& s, uint32_t Rn, double* x) {
     const int ln = s.lane;
-    const int D = s.A->R.D;
-    double* acc = s.lds + s.A->L.real;
+    const int D = RDIM(s.A->R, D);
+    double* acc = s.lds + LAY(*s.A).real;
     for (uint32_t r0 = 0; r0 < Rn; r0 += 3u) {
         if (D < kWave)
             qr_solve_cols<8>(s.A, s.lds, s.scratch, ln, 3u, x, r0);
@@ -2583,29 +2628,29 @@ __device__ __noinline__ void individual_jacobians_solve(Sim& s, uint32_t Rn, dou
  * own, so the default stacked-Jacobian kernel does not carry it; the traced kernels
  * (not on the hot path) read the choice at run time. */
 template <int RT, bool TR, bool IND>
-__device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg, bool allow_contacts, bool* out_collided,
+__device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg, bool allow_contacts, bool* out_collided,
                             bool* out_failed, double*& Tcur, double*& Tprev) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const int ln = s.lane;
-    const int W = R.W, D = R.D;
-    double* u = s.lds + s.A->L.u;
-    double* ustep = s.lds + s.A->L.ustep;
-    double* cfg_tmp = s.lds + s.A->L.cfg_tmp;
-    double* cfg_prev = s.lds + s.A->L.cfg_prev;
-    double* cfg_act = s.lds + s.A->L.cfg_act;
-    double* x = s.lds + s.A->L.x;
-    double* real = s.lds + s.A->L.real;
+    const int W = RDIM(R, W), D = RDIM(R, D);
+    double* u = s.lds + LAY(*s.A).u;
+    double* ustep = s.lds + LAY(*s.A).ustep;
+    double* cfg_tmp = s.lds + LAY(*s.A).cfg_tmp;
+    double* cfg_prev = s.lds + LAY(*s.A).cfg_prev;
+    double* cfg_act = s.lds + LAY(*s.A).cfg_act;
+    double* x = s.lds + LAY(*s.A).x;
+    double* real = s.lds + LAY(*s.A).real;
     /* the trial transforms live in whichever of the three transform buffers is neither
      * Tcur nor Tprev (the paired FK below rotates all three) */
     double* Ttmp;
     {
-        double* b0 = s.lds + s.A->L.Tcur;
-        double* b1 = s.lds + s.A->L.Tprev;
-        double* b2 = s.lds + s.A->L.Ttmp;
+        double* b0 = s.lds + LAY(*s.A).Tcur;
+        double* b1 = s.lds + LAY(*s.A).Tprev;
+        double* b2 = s.lds + LAY(*s.A).Ttmp;
         Ttmp = (b0 != Tcur && b0 != Tprev) ? b0 : ((b1 != Tcur && b1 != Tprev) ? b1 : b2);
     }
-    double* cfg = s.lds + s.A->L.cfg_work; /* robot(immutable_robot->Clone()) SPCS:1548 */
+    double* cfg = s.lds + LAY(*s.A).cfg_work; /* robot(immutable_robot->Clone()) SPCS:1548 */
     *out_collided = false;
     *out_failed = false;
     uint64_t t0 = tick();
@@ -2649,7 +2694,7 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
     tock(s, FKS_PHASE_STEP_SETUP, t0);
     trace_step<TR>(s, u, ustep, M);
     bool collided = false;
-    /* Paired FK (linked robots, A.L.fk_pair): while a microstep runs its FK, the chain's
+    /* Paired FK (linked robots, LAY(A).fk_pair): while a microstep runs its FK, the chain's
      * idle lanes compute the FK of the NEXT microstep's configuration as it will be if
      * this one ends without contact (apply_input with the next noise sample, already in
      * the noise buffer).  If this microstep ends without contact, the next one's
@@ -2657,7 +2702,7 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
      * actuator error bits and those transforms instead of recomputing them; after a
      * contact the prediction is dropped (the resolver reuses cfg_tmp / Ttmp).  Results are
      * unchanged; free microsteps pay about half an FK and half an apply_input each. */
-    const uint32_t noise_per = (uint32_t)(kWave / R.D);
+    const uint32_t noise_per = (uint32_t)(kWave / RDIM(R, D));
     bool pair_ready = false; /* Ttmp holds FK(cfg_tmp), cfg_tmp = the predicted configuration */
     uint32_t pair_err = 0;   /* the predicted configuration's actuator error bits (per lane) */
     for (uint32_t micro = 0; micro < M; ++micro) {
@@ -2675,7 +2720,7 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
             s.err |= pair_err;
             wsync();
         } else {
-            if (micro % (uint32_t)(kWave / R.D) == 0u)
+            if (micro % (uint32_t)(kWave / RDIM(R, D)) == 0u)
                 refill_noise(s, micro, M);
             apply_input<RT>(s, cfg_prev, ustep, cfg, true, micro);
         }
@@ -2703,7 +2748,7 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
             pair_ready = false;
             bool pair = false;
             if constexpr (RT == FKS_ROBOT_LINKED) {
-                pair = A.L.fk_pair && micro + 1u < M && ((micro + 1u) % noise_per) != 0u;
+                pair = LAY(A).fk_pair && micro + 1u < M && ((micro + 1u) % noise_per) != 0u;
                 if (pair) {
                     /* the next microstep's configuration if this one ends free of contact;
                      * its error bits are the next microstep's, not this one's */
@@ -2742,13 +2787,13 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
                 t0 = tick();
                 if (IND || (TR && A.individual_jacobians)) {
                     individual_jacobians_solve(s, Rn, x);
-                } else if (Rn <= 8u && R.D < kWave)
+                } else if (Rn <= 8u && RDIM(R, D) < kWave)
                     qr_solve_cols<8>(s.A, s.lds, s.scratch, ln, Rn, x);
-                else if (Rn <= 16u && R.D < kWave)
+                else if (Rn <= 16u && RDIM(R, D) < kWave)
                     qr_solve_cols<16>(s.A, s.lds, s.scratch, ln, Rn, x);
-                else if (Rn <= (uint32_t)kWave && R.D <= 8)
+                else if (Rn <= (uint32_t)kWave && RDIM(R, D) <= 8)
                     qr_solve_regs<8>(s.A, s.lds, s.scratch, ln, Rn, x);
-                else if (RT == FKS_ROBOT_LINKED && Rn <= (uint32_t)kWave && R.D <= 16)
+                else if (RT == FKS_ROBOT_LINKED && Rn <= (uint32_t)kWave && RDIM(R, D) <= 16)
                     qr_solve_regs<RT == FKS_ROBOT_LINKED ? 16 : 8>(s.A, s.lds, s.scratch, ln, Rn, x);
                 else
                     qr_solve(s.A, s.lds, s.scratch, ln, Rn, x);
@@ -2762,7 +2807,7 @@ __device__ int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg,
                     /* real_correction_step = (x / 1) * 1 == x bit for bit (SPCS:1681-1682): the
                      * corrected configuration is cfg_tmp and its transforms are Ttmp */
                     if (ln < W) cfg_act[ln] = cfg_tmp[ln];
-                    for (int e = ln; e < 12 * R.L; e += kWave) Tcur[e] = Ttmp[e];
+                    for (int e = ln; e < 12 * RDIM(R, L); e += kWave) Tcur[e] = Ttmp[e];
                     wsync();
                 } else {
                     if (ln < D) real[ln] = (x[ln] / step_fraction) * dabs(scaling);
@@ -2835,42 +2880,42 @@ __device__ __forceinline__ void setup_wave(const SimArgs* __restrict__ args, dou
     double* shared = lds_mem;
     {
         const int t = (int)threadIdx.x, nt = (int)blockDim.x;
-        uint64_t* dj = reinterpret_cast<uint64_t*>(shared + A.L.joints);
+        uint64_t* dj = reinterpret_cast<uint64_t*>(shared + LAY(A).joints);
         const uint64_t* sj = reinterpret_cast<const uint64_t*>(R.joints);
-        for (int k = t; k < R.J * kJointWords; k += nt) dj[k] = sj[k];
-        uint64_t* dc = reinterpret_cast<uint64_t*>(shared + A.L.ctrl);
+        for (int k = t; k < RDIM(R, J) * kJointWords; k += nt) dj[k] = sj[k];
+        uint64_t* dc = reinterpret_cast<uint64_t*>(shared + LAY(A).ctrl);
         const uint64_t* sc = reinterpret_cast<const uint64_t*>(R.ctrl);
-        for (int k = t; k < R.D * kCtrlWords; k += nt) dc[k] = sc[k];
-        int32_t* dd = reinterpret_cast<int32_t*>(shared + A.L.dofj);
-        if (RT == FKS_ROBOT_LINKED && t < R.D) dd[t] = gp(R.dof_joint)[t];
-        if (t < 12) shared[A.L.base + t] = R.base[t];
+        for (int k = t; k < RDIM(R, D) * kCtrlWords; k += nt) dc[k] = sc[k];
+        int32_t* dd = reinterpret_cast<int32_t*>(shared + LAY(A).dofj);
+        if (RT == FKS_ROBOT_LINKED && t < RDIM(R, D)) dd[t] = gp(R.dof_joint)[t];
+        if (t < 12) shared[LAY(A).base + t] = R.base[t];
         if (RT == FKS_ROBOT_LINKED) {
-            for (int k = t; k < 8 * R.G; k += nt)
-                shared[A.L.gbox + k] = (k % 8 == 7) ? (double)gp(R.geom_link)[k / 8] : gp(R.geom_box)[7 * (k / 8) + k % 8];
-            uint32_t* lp = reinterpret_cast<uint32_t*>(shared + A.L.gpairs);
-            for (int k = t; k < R.npairs && k < kLdsPairs; k += nt)
+            for (int k = t; k < 8 * RDIM(R, G); k += nt)
+                shared[LAY(A).gbox + k] = (k % 8 == 7) ? (double)gp(R.geom_link)[k / 8] : gp(R.geom_box)[7 * (k / 8) + k % 8];
+            uint32_t* lp = reinterpret_cast<uint32_t*>(shared + LAY(A).gpairs);
+            for (int k = t; k < RDIM(R, npairs) && k < kLdsPairs; k += nt)
                 lp[k] = (uint32_t)gp(R.pairs)[2 * k] | ((uint32_t)gp(R.pairs)[2 * k + 1] << 16);
         }
-        if (t < R.nrounds && t < kWave) {
+        if (t < RDIM(R, nrounds) && t < kWave) {
             const RoundDev rd = load_round(R.rounds, t);
-            shared[A.L.rounds + 2 * t] = (double)rd.link;
-            shared[A.L.rounds + 2 * t + 1] = rd.radius;
+            shared[LAY(A).rounds + 2 * t] = (double)rd.link;
+            shared[LAY(A).rounds + 2 * t + 1] = rd.radius;
         }
         __syncthreads();
     }
     s.A = args;
     s.shared = shared;
-    s.lds = lds_mem + A.L.shared_total + (uint64_t)wave * A.L.total;
-    s.ldsi = reinterpret_cast<int32_t*>(s.lds + A.L.ints);
+    s.lds = lds_mem + LAY(A).shared_total + (uint64_t)wave * LAY(A).total;
+    s.ldsi = reinterpret_cast<int32_t*>(s.lds + LAY(A).ints);
     s.scratch = A.scratch + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)wave) * A.scratch_per_wave;
     s.lane = lane_id();
-    s.stats = reinterpret_cast<uint32_t*>(s.lds + s.A->L.misc + 24);
-    s.phase = reinterpret_cast<uint64_t*>(s.lds + s.A->L.misc + 8);
-    s.joints = reinterpret_cast<const JointDev*>(shared + A.L.joints);
-    s.ctrl = reinterpret_cast<const fks_dof_controller*>(shared + A.L.ctrl);
-    s.dofj = reinterpret_cast<const int32_t*>(shared + A.L.dofj);
-    s.base = shared + A.L.base;
-    s.rstate = s.lds + A.L.rstate; /* (the check / kinematics kernels keep no skip-proof cache) */
+    s.stats = reinterpret_cast<uint32_t*>(s.lds + LAY(*s.A).misc + 24);
+    s.phase = reinterpret_cast<uint64_t*>(s.lds + LAY(*s.A).misc + 8);
+    s.joints = reinterpret_cast<const JointDev*>(shared + LAY(A).joints);
+    s.ctrl = reinterpret_cast<const fks_dof_controller*>(shared + LAY(A).ctrl);
+    s.dofj = reinterpret_cast<const int32_t*>(shared + LAY(A).dofj);
+    s.base = shared + LAY(A).base;
+    s.rstate = s.lds + LAY(A).rstate; /* (the check / kinematics kernels keep no skip-proof cache) */
     s.err = 0;
     s.lane_bytes = 0;
     s.self_nonempty = false;
@@ -2882,7 +2927,7 @@ template <int RT>
 __device__ __forceinline__ void set_position(Sim& s, const double* src, double* cfg) {
     const int ln = s.lane;
     if constexpr (RT == FKS_ROBOT_LINKED) {
-        if (ln < s.A->R.D) {
+        if (ln < RDIM(s.A->R, D)) {
             const JointDev& jd = s.joints[s.dofj[ln]];
             cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(src[ln])
                                                         : clamp(src[ln], jd.lo, jd.hi);
@@ -2903,10 +2948,10 @@ __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict
                                                        double* scratch, int ln, const double* Tc, double res) {
     const SimArgs& A = *Ap;
     const RobotDev& R = A.R;
-    double* box = lds + A.L.box;
+    double* box = lds + LAY(A).box;
     bool bad = false;
-    if (ln < R.G) {
-        const double* gb = shared + A.L.gbox + 8 * ln;
+    if (ln < RDIM(R, G)) {
+        const double* gb = shared + LAY(A).gbox + 8 * ln;
         const double* T = Tc + 12 * (int)gb[7];
         double lo[3], hi[3];
         if (gb[6] != 0.0) {
@@ -2936,7 +2981,7 @@ __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict
     }
     wsync();
     bool any = false;
-    for (int k = ln; k < R.npairs; k += kWave) {
+    for (int k = ln; k < RDIM(R, npairs); k += kWave) {
         const int a = gp(R.pairs)[2 * k], b = gp(R.pairs)[2 * k + 1];
         bool ov = true;
         for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
@@ -2944,9 +2989,9 @@ __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict
     }
     if (!wave_any(any || bad)) return 0u;
     /* exact keys of every point (LocationToExtendedGridIndex SPCS:1173-1181) */
-    int64_t* keys = reinterpret_cast<int64_t*>(scratch + A.SL.keys);
+    int64_t* keys = reinterpret_cast<int64_t*>(scratch + SLAY(A).keys);
     uint32_t err = 0;
-    for (int i = ln; i < R.P; i += kWave) {
+    for (int i = ln; i < RDIM(R, P); i += kWave) {
         const D4 x = xform4(Tc + 12 * (int)gp(R.point_link)[i], load_point(R, i));
         const D4 g = xform4(A.env_g.inv, x);
         const double q[3] = {g.x / res, g.y / res, g.z / res};
@@ -2967,7 +3012,7 @@ __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict
     }
     wsync();
     bool hit = false;
-    for (int k = 0; k < R.npairs && !wave_any(hit); ++k) {
+    for (int k = 0; k < RDIM(R, npairs) && !wave_any(hit); ++k) {
         const int a = gp(R.pairs)[2 * k], b = gp(R.pairs)[2 * k + 1];
         bool ov = true;
         for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
@@ -2993,18 +3038,18 @@ __device__ __forceinline__ void check_configs(const SimArgs* __restrict__ args, 
     const SimArgs& A = *args;
     const RobotDev& R = A.R;
     const int ln = s.lane;
-    double* cfg = s.lds + A.L.cfg;
-    double* T = s.lds + A.L.Tcur;
+    double* cfg = s.lds + LAY(A).cfg;
+    double* T = s.lds + LAY(A).Tcur;
     const uint64_t stride = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint64_t bytes_total = 0;
     for (uint64_t c = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < A.n; c += stride) {
-        set_position<RT>(s, A.starts + c * (uint64_t)R.W, cfg);
+        set_position<RT>(s, A.starts + c * (uint64_t)RDIM(R, W), cfg);
         fk<RT>(s, cfg, T);
         /* CheckEnvironmentCollision: pairs of 64-point rounds, bytes up to the first
          * colliding point (its loop returns there) */
         uint64_t lane_bytes = 0;
         bool env = false;
-        for (int base = 0; base < R.P && !env; base += 2 * kWave) {
+        for (int base = 0; base < RDIM(R, P) && !env; base += 2 * kWave) {
             uint64_t b0 = 0, b1 = 0;
             double S, G, C;
             const bool c0 = env_point(A, T, base + ln, &b0, &S, &G, &C);
@@ -3025,7 +3070,7 @@ __device__ __forceinline__ void check_configs(const SimArgs* __restrict__ args, 
         }
         uint32_t r = 0;
         if constexpr (RT == FKS_ROBOT_LINKED) {
-            if (R.self_possible) r = config_self_collision(args, s.shared, s.lds, s.scratch, ln, T, A.self_res);
+            if (RDIM(R, self_possible)) r = config_self_collision(args, s.shared, s.lds, s.scratch, ln, T, A.self_res);
         }
         const uint64_t bytes = wave_sum_u64(lane_bytes);
         if (ln == 0) {
@@ -3049,26 +3094,26 @@ __device__ __forceinline__ void kinematics(const SimArgs* __restrict__ args, dou
     const SimArgs& A = *args;
     const RobotDev& R = A.R;
     const int ln = s.lane;
-    double* cfg = s.lds + A.L.cfg;
-    double* out_cfg = s.lds + A.L.cfg_tmp;
-    double* T = s.lds + A.L.Tcur;
+    double* cfg = s.lds + LAY(A).cfg;
+    double* out_cfg = s.lds + LAY(A).cfg_tmp;
+    double* T = s.lds + LAY(A).Tcur;
     const uint64_t stride = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t c = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < A.n; c += stride) {
-        set_position<RT>(s, A.starts + c * (uint64_t)R.W, cfg);
+        set_position<RT>(s, A.starts + c * (uint64_t)RDIM(R, W), cfg);
         if (A.kin_mode == FKS_KIN_APPLY_CONTROL_INPUT) {
-            double* in = s.lds + A.L.u;
-            if (ln < R.D) in[ln] = A.targets[c * (uint64_t)R.D + ln];
+            double* in = s.lds + LAY(A).u;
+            if (ln < RDIM(R, D)) in[ln] = A.targets[c * (uint64_t)RDIM(R, D) + ln];
             wsync();
             apply_input<RT>(s, cfg, in, out_cfg, false, 0);
-            if (ln < R.W) A.kin_out[c * (uint64_t)R.W + ln] = out_cfg[ln];
+            if (ln < RDIM(R, W)) A.kin_out[c * (uint64_t)RDIM(R, W) + ln] = out_cfg[ln];
         } else {
             fk<RT>(s, cfg, T);
             if (A.kin_mode == FKS_KIN_LINK_TRANSFORMS) {
-                for (int e = ln; e < 12 * R.L; e += kWave) A.kin_out[c * 12ull * (uint64_t)R.L + e] = T[e];
+                for (int e = ln; e < 12 * RDIM(R, L); e += kWave) A.kin_out[c * 12ull * (uint64_t)RDIM(R, L) + e] = T[e];
             } else {
-                for (int i = ln; i < R.P; i += kWave) {
+                for (int i = ln; i < RDIM(R, P); i += kWave) {
                     const D4 x = xform4(T + 12 * gp(R.point_link)[i], load_point(R, i));
-                    double* o = A.kin_out + (c * (uint64_t)R.P + (uint64_t)i) * 3ull;
+                    double* o = A.kin_out + (c * (uint64_t)RDIM(R, P) + (uint64_t)i) * 3ull;
                     o[0] = x.x;
                     o[1] = x.y;
                     o[2] = x.z;
@@ -3088,55 +3133,55 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     {
         /* one copy per workgroup of the robot tables read in the inner loops */
         const int t = (int)threadIdx.x, nt = (int)blockDim.x;
-        uint64_t* dj = reinterpret_cast<uint64_t*>(shared + A.L.joints);
+        uint64_t* dj = reinterpret_cast<uint64_t*>(shared + LAY(A).joints);
         const uint64_t* sj = reinterpret_cast<const uint64_t*>(R.joints);
-        for (int k = t; k < R.J * kJointWords; k += nt) dj[k] = sj[k];
-        uint64_t* dc = reinterpret_cast<uint64_t*>(shared + A.L.ctrl);
+        for (int k = t; k < RDIM(R, J) * kJointWords; k += nt) dj[k] = sj[k];
+        uint64_t* dc = reinterpret_cast<uint64_t*>(shared + LAY(A).ctrl);
         const uint64_t* sc = reinterpret_cast<const uint64_t*>(R.ctrl);
-        for (int k = t; k < R.D * kCtrlWords; k += nt) dc[k] = sc[k];
-        int32_t* dd = reinterpret_cast<int32_t*>(shared + A.L.dofj);
-        if (RT == FKS_ROBOT_LINKED && t < R.D) dd[t] = gp(R.dof_joint)[t];
-        if (t < 12) shared[A.L.base + t] = R.base[t];
+        for (int k = t; k < RDIM(R, D) * kCtrlWords; k += nt) dc[k] = sc[k];
+        int32_t* dd = reinterpret_cast<int32_t*>(shared + LAY(A).dofj);
+        if (RT == FKS_ROBOT_LINKED && t < RDIM(R, D)) dd[t] = gp(R.dof_joint)[t];
+        if (t < 12) shared[LAY(A).base + t] = R.base[t];
         if (RT == FKS_ROBOT_LINKED) {
-            for (int k = t; k < 8 * R.G; k += nt)
-                shared[A.L.gbox + k] = (k % 8 == 7) ? (double)gp(R.geom_link)[k / 8] : gp(R.geom_box)[7 * (k / 8) + k % 8];
-            uint32_t* lp = reinterpret_cast<uint32_t*>(shared + A.L.gpairs);
-            for (int k = t; k < R.npairs && k < kLdsPairs; k += nt)
+            for (int k = t; k < 8 * RDIM(R, G); k += nt)
+                shared[LAY(A).gbox + k] = (k % 8 == 7) ? (double)gp(R.geom_link)[k / 8] : gp(R.geom_box)[7 * (k / 8) + k % 8];
+            uint32_t* lp = reinterpret_cast<uint32_t*>(shared + LAY(A).gpairs);
+            for (int k = t; k < RDIM(R, npairs) && k < kLdsPairs; k += nt)
                 lp[k] = (uint32_t)gp(R.pairs)[2 * k] | ((uint32_t)gp(R.pairs)[2 * k + 1] << 16);
         }
-        if (t < R.nrounds && t < kWave) {
+        if (t < RDIM(R, nrounds) && t < kWave) {
             const RoundDev rd = load_round(R.rounds, t);
-            shared[A.L.rounds + 2 * t] = (double)rd.link;
-            shared[A.L.rounds + 2 * t + 1] = rd.radius;
+            shared[LAY(A).rounds + 2 * t] = (double)rd.link;
+            shared[LAY(A).rounds + 2 * t + 1] = rd.radius;
         }
         __syncthreads(); /* the only workgroup barrier: waves run independently afterwards */
     }
     Sim s;
     s.A = args;
     s.shared = shared;
-    s.lds = lds_mem + A.L.shared_total + (uint64_t)wave * A.L.total;
-    s.ldsi = reinterpret_cast<int32_t*>(s.lds + A.L.ints);
+    s.lds = lds_mem + LAY(A).shared_total + (uint64_t)wave * LAY(A).total;
+    s.ldsi = reinterpret_cast<int32_t*>(s.lds + LAY(A).ints);
     s.scratch = A.scratch + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)wave) * A.scratch_per_wave;
     s.lane = lane_id();
-    s.stats = reinterpret_cast<uint32_t*>(s.lds + s.A->L.misc + 24); /* 8 x u32 */
-    s.phase = reinterpret_cast<uint64_t*>(s.lds + s.A->L.misc + 8); /* FKS_NUM_PHASES x u64 */
-    s.joints = reinterpret_cast<const JointDev*>(shared + A.L.joints);
-    s.ctrl = reinterpret_cast<const fks_dof_controller*>(shared + A.L.ctrl);
-    s.dofj = reinterpret_cast<const int32_t*>(shared + A.L.dofj);
-    s.base = shared + A.L.base;
+    s.stats = reinterpret_cast<uint32_t*>(s.lds + LAY(*s.A).misc + 24); /* 8 x u32 */
+    s.phase = reinterpret_cast<uint64_t*>(s.lds + LAY(*s.A).misc + 8); /* FKS_NUM_PHASES x u64 */
+    s.joints = reinterpret_cast<const JointDev*>(shared + LAY(A).joints);
+    s.ctrl = reinterpret_cast<const fks_dof_controller*>(shared + LAY(A).ctrl);
+    s.dofj = reinterpret_cast<const int32_t*>(shared + LAY(A).dofj);
+    s.base = shared + LAY(A).base;
     /* skip-proof cache of the first 64 rounds (the skip masks are 64-bit; later rounds are always
      * read): in the wave's LDS block, or in its scratch for a lean block (fixed per kernel, so
      * each instantiation addresses it with one kind of load) */
-    s.rstate = LEAN ? s.scratch + A.SL.rstate : s.lds + A.L.rstate;
-    if (s.lane < R.nrounds) s.rstate[kRoundState * s.lane + 12] = kInvalidRound;
+    s.rstate = LEAN ? s.scratch + SLAY(A).rstate : s.lds + LAY(A).rstate;
+    if (s.lane < RDIM(R, nrounds)) s.rstate[kRoundState * s.lane + 12] = kInvalidRound;
     wsync();
     const int ln = s.lane;
-    const int W = R.W, D = R.D;
-    double* cfg = s.lds + s.A->L.cfg;
-    double* res_cfg = s.lds + s.A->L.cfg_res;
-    double* u = s.lds + s.A->L.u;
-    unsigned long long* next_particle = reinterpret_cast<unsigned long long*>(s.lds + s.A->L.misc + 31);
-    uint32_t* seg_seen = reinterpret_cast<uint32_t*>(s.lds + s.A->L.misc + 30);
+    const int W = RDIM(R, W), D = RDIM(R, D);
+    double* cfg = s.lds + LAY(*s.A).cfg;
+    double* res_cfg = s.lds + LAY(*s.A).cfg_res;
+    double* u = s.lds + LAY(*s.A).u;
+    unsigned long long* next_particle = reinterpret_cast<unsigned long long*>(s.lds + LAY(*s.A).misc + 31);
+    uint32_t* seg_seen = reinterpret_cast<uint32_t*>(s.lds + LAY(*s.A).misc + 30);
     const uint64_t t_resident = __builtin_amdgcn_s_memrealtime();
     const uint32_t nseg = A.nseg;
     uint64_t carry = kNoTicket; /* the next segment of the particle just run, claimed by this wave */
@@ -3270,12 +3315,12 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             micro_before = load_coherent_u64(sw + 1);
             resolver_before = load_coherent_u64(sw + 2);
             /* the particle's own skip-proof cache (the rounds' last full evaluations) */
-            const int nrc = kRoundState * (R.nrounds < kWave ? R.nrounds : kWave);
+            const int nrc = kRoundState * (RDIM(R, nrounds) < kWave ? RDIM(R, nrounds) : kWave);
             for (int e = ln; e < nrc; e += kWave) s.rstate[e] = load_coherent(st + 2 * D + 4 + e);
         }
         wsync();
-        double* Tcur = s.lds + s.A->L.Tcur;
-        double* Tprev = s.lds + s.A->L.Tprev;
+        double* Tcur = s.lds + LAY(*s.A).Tcur;
+        double* Tprev = s.lds + LAY(*s.A).Tprev;
         bool ended = false;
         /* ForwardSimulateMutableRobot (SPCS:843-919) */
         for (uint32_t step = step_begin; step < step_end; ++step) {
@@ -3283,7 +3328,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             const int ln = s.lane;
             s.step = step;
             s.step_count++;
-            double* tgt_lds = s.lds + s.A->L.tgt;
+            double* tgt_lds = s.lds + LAY(*s.A).tgt;
             const uint64_t t0 = tick();
             const double uc = control_action<RT>(s, cfg, target);
             if (ln < D) u[ln] = uc * A.dt;
@@ -3341,7 +3386,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                 store_coherent_u64(sw + 1, micro_total);
                 store_coherent_u64(sw + 2, resolver_total);
             }
-            const int nrc = kRoundState * (R.nrounds < kWave ? R.nrounds : kWave);
+            const int nrc = kRoundState * (RDIM(R, nrounds) < kWave ? RDIM(R, nrounds) : kWave);
             for (int e = ln; e < nrc; e += kWave) store_coherent(st + 2 * D + 4 + e, s.rstate[e]);
         }
         w_steps += s.step_count;
@@ -3411,6 +3456,15 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
 #define FKS_WAVES_PER_EU 5
 #endif
 #define FKS_KERNEL_ATTRS __launch_bounds__(64 * kMaxWavesPerGroup) __attribute__((amdgpu_waves_per_eu(FKS_WAVES_PER_EU)))
+#if defined(FKS_SHAPE_L)
+/* the shape-specialised build (fks_specialize.cpp, hiprtc): one throughput kernel for one
+ * robot shape, the same template and launch attributes as the generic kernel it replaces
+ * (fks_simulate_<family>[_lean]) */
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_shaped(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_SHAPE_TYPE, false, false, FKS_SHAPE_LEAN != 0>(args, lds_mem);
+}
+#else
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
     simulate_particles<FKS_ROBOT_LINKED, false>(args, lds_mem);
@@ -3512,6 +3566,9 @@ extern "C" __global__ void FKS_KERNEL_ATTRS fks_kinematics_se3(const SimArgs* __
     kinematics<FKS_ROBOT_SE3>(args, lds_mem);
 }
 
+#endif /* FKS_SHAPE_L */
+
+#if !defined(FKS_SHAPE_L)
 /* device self-test of the portable libm (fks_selftest_math) */
 extern "C" __global__ void fks_math_probe(const double* a, const double* b, double* out, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3526,3 +3583,4 @@ extern "C" __global__ void fks_math_probe(const double* a, const double* b, doub
     out[8 * i + 6] = fks_math::enforce_continuous_revolute_bounds(x);
     out[8 * i + 7] = (x * y + x) * y - x * x;
 }
+#endif

@@ -266,4 +266,57 @@ fks_status fks_multi_set_call_index(fks_multi_context* m, uint64_t call_index) {
     return FKS_OK;
 }
 
+fks_status fks_multi_check_config_collision(fks_multi_context* m, const double* configs, uint64_t n, double inflation_ratio,
+                                            uint8_t* out_collided, uint32_t* out_error_flags) {
+    if (!m) return FKS_ERR_INVALID_ARGUMENT;
+    if (m->width <= 0) return mfail(m, FKS_ERR_NO_ROBOT, "fks_multi_set_robot has not been called");
+    if (n > 0 && (!configs || !out_collided)) return mfail(m, FKS_ERR_INVALID_ARGUMENT, "null host buffer");
+    const size_t W = (size_t)m->width;
+    const int32_t ndev = (int32_t)m->devices.size();
+    /* the configurations and flags reuse the simulation buffers (starts, collided, errors) */
+    for (int32_t g = 0; g < ndev; ++g) {
+        auto& d = m->devices[(size_t)g];
+        uint64_t lo = 0, hi = 0;
+        fks_shard_bounds(n, ndev, g, &lo, &hi);
+        const uint64_t k = hi - lo;
+        MHIP(m, hipSetDevice(d.device));
+        if (k > d.cap) {
+            MHIP(m, grow(&d.d_starts, k * W));
+            MHIP(m, grow(&d.d_out, k * W));
+            MHIP(m, grow(&d.d_coll, k));
+            MHIP(m, grow(&d.d_micro, k));
+            MHIP(m, grow(&d.d_res, k));
+            MHIP(m, grow(&d.d_err, k));
+            d.cap = k;
+        }
+        if (k == 0) continue;
+        MHIP(m, hipMemcpyAsync(d.d_starts, configs + lo * W, k * W * sizeof(double), hipMemcpyHostToDevice, d.stream));
+        const fks_status st =
+            fks_check_config_collision_device(d.ctx, d.d_starts, k, inflation_ratio, d.d_coll, d.d_err, d.stream, 0);
+        if (st != FKS_OK) return mctx(m, st, d.ctx, "fks_check_config_collision_device");
+    }
+    for (int32_t g = 0; g < ndev; ++g) {
+        auto& d = m->devices[(size_t)g];
+        uint64_t lo = 0, hi = 0;
+        fks_shard_bounds(n, ndev, g, &lo, &hi);
+        const uint64_t k = hi - lo;
+        if (k == 0) continue;
+        MHIP(m, hipSetDevice(d.device));
+        MHIP(m, hipMemcpyAsync(out_collided + lo, d.d_coll, k, hipMemcpyDeviceToHost, d.stream));
+        if (out_error_flags)
+            MHIP(m, hipMemcpyAsync(out_error_flags + lo, d.d_err, k * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
+        MHIP(m, hipStreamSynchronize(d.stream));
+        fks_call_counters c;
+        const fks_status st = fks_get_last_check_counters(d.ctx, &c); /* settles the device's check */
+        if (st != FKS_OK) return mctx(m, st, d.ctx, "fks_get_last_check_counters");
+    }
+    return FKS_OK;
+}
+
+int32_t fks_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
 }  // extern "C"

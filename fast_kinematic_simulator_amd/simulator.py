@@ -162,6 +162,19 @@ class HipParticleContactSimulator:
         (fks_set_small_batch_kernel; default on).  Results do not depend on it."""
         _capi.check(self._lib.fks_set_small_batch_kernel(self._ctx, 1 if enabled else 0), self._ctx, "small batch kernel")
 
+    def set_specialization(self, enabled: bool = True):
+        """Run the plain throughput simulation of this robot (and of every robot set later) on a
+        kernel compiled at run time for its shape (fks_set_specialization: hiprtc, cached per
+        process and on disk).  Results do not depend on it; raises FksError with the compiler
+        log when the current robot's kernel cannot be built."""
+        _capi.check(self._lib.fks_set_specialization(self._ctx, 1 if enabled else 0), self._ctx, "specialization")
+
+    def specialization(self) -> dict:
+        """fks_get_specialization: enabled, active, from_cache, compile_seconds, launches, shape"""
+        info = _capi.SpecializationInfo()
+        _capi.check(self._lib.fks_get_specialization(self._ctx, ctypes.byref(info)), self._ctx, "specialization")
+        return info.as_dict()
+
     def set_individual_jacobians(self, simulate_with_individual_jacobians: bool):
         """The simulate_with_individual_jacobians constructor flag of the reference class
         (SPCS:420-423, 1629): True selects ComputeResolverCorrectionStepIndividualJacobians
@@ -524,6 +537,20 @@ class MultiDeviceSimulator:
         self._check(st, "fks_multi_forward_simulate")
         return {"positions": out, "collided": collided.astype(bool), "microsteps": micro, "resolver_iterations": resolver,
                 "error_flags": errors}
+
+    def check_config_collisions(self, robot: RobotDescription, configs, inflation_ratio: float):
+        """Batched CheckConfigCollision (SPCS:1398-1416) sharded over the devices:
+        (collided bool[n], error bits uint32[n])."""
+        self.set_robot(robot)
+        W = robot.config_width
+        c = np.ascontiguousarray(np.asarray(configs, dtype=np.float64).reshape(-1, W))
+        n = c.shape[0]
+        collided = np.zeros(n, dtype=np.uint8)
+        errors = np.zeros(n, dtype=np.uint32)
+        st = self._lib.fks_multi_check_config_collision(self._ctx, _capi.as_ptr(c, ctypes.c_double), n, float(inflation_ratio),
+                                                        _capi.as_ptr(collided, ctypes.c_uint8), _capi.as_ptr(errors, ctypes.c_uint32))
+        self._check(st, "fks_multi_check_config_collision")
+        return collided.astype(bool), errors
 
     def get_statistics(self) -> dict:
         s = _capi.Statistics()

@@ -39,6 +39,7 @@
 #include <string>
 #include <vector>
 
+#include "fast_kinematic_simulator_amd/device_set.hpp"
 #include "fast_kinematic_simulator_amd/environment.hpp"
 #include "fast_kinematic_simulator_amd/fks_external_types.hpp"
 #include "fast_kinematic_simulator_amd/tnuva_robot_models.hpp"
@@ -95,41 +96,48 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
     typedef fks_planner_types::MarkerArray MarkerArray;
     typedef fks_planner_types::ColorRGBA ColorRGBA;
 
-    /* SPCS:420-444; `device` selects the MI355X (no reference counterpart) */
+    /* SPCS:420-444.  `devices` lists the MI355X devices the simulator runs on (no reference
+     * counterpart; the reference's batch loop runs over the host's cores, SPCS:795): batches
+     * of at least ShardThreshold() particles are split into contiguous shards by global
+     * particle id, one per listed device (fks_create_multi), bit-identical to one device;
+     * smaller batches and single-particle calls run on devices[0].  The same device may be
+     * listed more than once. */
+    HipParticleContactSimulator(const sdf_tools::TaggedObjectCollisionMapGrid& environment,
+                                const sdf_tools::SignedDistanceField& environment_sdf,
+                                const SurfaceNormalGrid& surface_normals_grid, const SimulatorSolverParameters& solver_config,
+                                const double simulation_controller_frequency, const bool simulate_with_individual_jacobians,
+                                const uint64_t prng_seed, const int32_t debug_level, const std::vector<int32_t>& devices)
+        : environment_(environment), environment_sdf_(environment_sdf), surface_normals_grid_(surface_normals_grid),
+          solver_config_(solver_config), simulation_controller_frequency_(simulation_controller_frequency),
+          dev_(MakeDevices(environment_, environment_sdf_, surface_normals_grid_, solver_config, simulation_controller_frequency, prng_seed,
+                           debug_level, devices)) {
+        ctx_ = dev_->primary();
+        dev_->set_individual_jacobians(simulate_with_individual_jacobians);
+        ResetGenerators(prng_seed);
+    }
+    /* one device (the constructor of the reference's parameter list plus `device`) */
     HipParticleContactSimulator(const sdf_tools::TaggedObjectCollisionMapGrid& environment,
                                 const sdf_tools::SignedDistanceField& environment_sdf,
                                 const SurfaceNormalGrid& surface_normals_grid, const SimulatorSolverParameters& solver_config,
                                 const double simulation_controller_frequency, const bool simulate_with_individual_jacobians,
                                 const uint64_t prng_seed, const int32_t debug_level, const int32_t device = 0)
-        : environment_(environment), environment_sdf_(environment_sdf), surface_normals_grid_(surface_normals_grid),
-          solver_config_(solver_config), simulation_controller_frequency_(simulation_controller_frequency) {
-        std::vector<float> sdf_storage; /* the values fks_create uploads (real sdf_tools only) */
-        const fks_environment env =
-            simulator_environment_builder::ToFksEnvironment(environment_, environment_sdf_, surface_normals_grid_, sdf_storage);
-        const fks_solver_params p = solver_config.ToFks();
-        fks_context* ctx = nullptr;
-        Check(fks_create(&env, &p, simulation_controller_frequency, prng_seed, debug_level, device, &ctx), nullptr, "fks_create");
-        ctx_.reset(ctx);
-        Check(fks_set_individual_jacobians(ctx_.get(), simulate_with_individual_jacobians ? 1 : 0), ctx_.get(),
-              "fks_set_individual_jacobians");
-        ResetGenerators(prng_seed);
-    }
+        : HipParticleContactSimulator(environment, environment_sdf, surface_normals_grid, solver_config, simulation_controller_frequency,
+                                      simulate_with_individual_jacobians, prng_seed, debug_level, std::vector<int32_t>{device}) {}
 
     /* ---- SimulatorInterface (SPCS:446-1416) ---- */
-    int32_t GetDebugLevel() const override { return fks_get_debug_level(ctx_.get()); }
-    int32_t SetDebugLevel(const int32_t debug_level) override { return fks_set_debug_level(ctx_.get(), debug_level); }
+    int32_t GetDebugLevel() const override { return fks_get_debug_level(ctx_); }
+    int32_t SetDebugLevel(const int32_t debug_level) override { return dev_->set_debug_level(debug_level); }
     /* SPCS:457-471: the host generator seeded as the reference seeds its thread 0 one; the
      * simulation's own noise is the counter RNG re-keyed by the same seed */
     void ResetGenerators(const uint64_t prng_seed) {
         RNG prng(prng_seed);
         std::uniform_int_distribution<uint64_t> seed_dist(0, std::numeric_limits<uint64_t>::max());
         rng_ = RNG(seed_dist(prng));
-        Check(fks_reset_generators(ctx_.get(), prng_seed), ctx_.get(), "ResetGenerators");
+        dev_->reset_generators(prng_seed);
     }
     RNG& GetRandomGenerator() override { return rng_; }
     std::map<std::string, double> GetStatistics() const override {
-        fks_statistics s;
-        Check(fks_get_statistics(ctx_.get(), &s), ctx_.get(), "GetStatistics");
+        const fks_statistics s = dev_->statistics(); /* summed over the devices */
         return {{"successful_resolves", (double)s.successful_resolves},
                 {"unsuccessful_resolves", (double)s.unsuccessful_resolves},
                 {"free_resolves", (double)s.free_resolves},
@@ -139,7 +147,7 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
                 {"unsuccessful_env_collision_resolves", (double)s.unsuccessful_env_collision_resolves},
                 {"recovered_unsuccessful_resolves", (double)s.recovered_unsuccessful_resolves}};
     }
-    void ResetStatistics() override { Check(fks_reset_statistics(ctx_.get()), ctx_.get(), "ResetStatistics"); }
+    void ResetStatistics() override { dev_->reset_statistics(); }
     std::string GetFrame() const override { return environment_.GetFrame(); }
     double GetResolution() const { return environment_.GetResolution(); }
 
@@ -276,9 +284,9 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
         uint8_t collided = 0;
         uint32_t micro = 0, resolver = 0, errors = 0;
         if (!enable_tracing) {
-            Check(fks_forward_simulate_mutable(ctx_.get(), s.data(), 1, t.data(), 1, allow_contacts ? 1 : 0, pid.data(), q.data(),
+            Check(fks_forward_simulate_mutable(ctx_, s.data(), 1, t.data(), 1, allow_contacts ? 1 : 0, pid.data(), q.data(),
                                                &collided, &micro, &resolver, &errors),
-                  ctx_.get(), "ForwardSimulateMutableRobot");
+                  ctx_, "ForwardSimulateMutableRobot");
         } else {
             /* the trace holds one step record per controller step and every pushed
              * configuration.  The capacity starts at TraceCapacityHint() configurations
@@ -287,21 +295,21 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
              * reproduces it), and the statistics and call totals the first run added are taken
              * back, so GetStatistics counts the particle once */
             const uint32_t steps = ForwardSteps();
-            const uint64_t call = fks_get_call_index(ctx_.get());
+            const uint64_t call = fks_get_call_index(ctx_);
             const std::vector<double> pid0 = pid;
             fks_statistics stats0{};
             fks_call_counters totals0{};
-            Check(fks_get_statistics(ctx_.get(), &stats0), ctx_.get(), "fks_get_statistics");
-            Check(fks_get_total_counters(ctx_.get(), &totals0), ctx_.get(), "fks_get_total_counters");
+            Check(fks_get_statistics(ctx_, &stats0), ctx_, "fks_get_statistics");
+            Check(fks_get_total_counters(ctx_, &totals0), ctx_, "fks_get_total_counters");
             uint32_t cap = trace_capacity_hint_;
             for (int attempt = 0;; ++attempt) {
                 std::vector<double> inputs((size_t)steps * 2 * D), configs((size_t)cap * W);
                 std::vector<uint32_t> step_micro(steps), tags((size_t)cap * 3);
                 uint32_t num_steps = 0, num_configs = 0;
                 fks_trace tr{steps, cap, inputs.data(), step_micro.data(), configs.data(), tags.data(), &num_steps, &num_configs};
-                Check(fks_forward_simulate_traced_mutable(ctx_.get(), s.data(), 1, t.data(), 1, allow_contacts ? 1 : 0, pid.data(),
+                Check(fks_forward_simulate_traced_mutable(ctx_, s.data(), 1, t.data(), 1, allow_contacts ? 1 : 0, pid.data(),
                                                           q.data(), &collided, &micro, &resolver, &errors, &tr),
-                      ctx_.get(), "ForwardSimulateMutableRobot (traced)");
+                      ctx_, "ForwardSimulateMutableRobot (traced)");
                 if (num_steps <= steps && num_configs <= cap) {
                     AppendTrace(r, trace, inputs, num_steps, configs, tags, num_configs, D);
                     break;
@@ -309,9 +317,9 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
                 if (attempt > 0 || num_steps > steps) throw std::runtime_error("trace capacity exceeded");
                 cap = num_configs;
                 pid = pid0;
-                Check(fks_set_call_index(ctx_.get(), call), ctx_.get(), "fks_set_call_index");
-                Check(fks_set_statistics(ctx_.get(), &stats0), ctx_.get(), "fks_set_statistics");
-                Check(fks_set_total_counters(ctx_.get(), &totals0), ctx_.get(), "fks_set_total_counters");
+                Check(fks_set_call_index(ctx_, call), ctx_, "fks_set_call_index");
+                Check(fks_set_statistics(ctx_, &stats0), ctx_, "fks_set_statistics");
+                Check(fks_set_total_counters(ctx_, &totals0), ctx_, "fks_set_total_counters");
                 retried_traces_++;
             }
         }
@@ -327,7 +335,7 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
         SetRobot(robot);
         const std::vector<double> c = robot.ToFlat(config);
         uint8_t collided = 0;
-        Check(fks_check_config_collision(ctx_.get(), c.data(), 1, inflation_ratio, &collided, nullptr), ctx_.get(),
+        Check(fks_check_config_collision(ctx_, c.data(), 1, inflation_ratio, &collided, nullptr), ctx_,
               "CheckConfigCollision");
         return collided != 0;
     }
@@ -337,7 +345,31 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
     const std::vector<uint32_t>& LastParticleErrors() const { return last_errors_; }
     const std::vector<uint32_t>& LastMicrosteps() const { return last_micro_; }
     const std::vector<uint32_t>& LastResolverIterations() const { return last_resolver_; }
-    fks_context* Context() const { return ctx_.get(); }
+    /* the context of devices[0] (single-particle calls and batches below ShardThreshold()) */
+    fks_context* Context() const { return ctx_; }
+    const std::vector<int32_t>& Devices() const { return dev_->devices(); }
+    /* batches of at least this many particles are sharded over Devices() (0: automatic = the
+     * resident waves of devices[0] for the current robot, so that a batch one device runs in
+     * a single wave per particle pays no fan-out); 1 shards every batch */
+    void SetShardThreshold(uint64_t particles) { dev_->set_shard_threshold(particles); }
+    uint64_t ShardThreshold() const { return dev_->shard_threshold(); }
+    /* whether the last batch call ran sharded over every listed device */
+    bool LastBatchSharded() const { return dev_->last_sharded(); }
+    /* batched CheckConfigCollision (SPCS:1398-1416, one configuration per call there),
+     * sharded like the simulation batches */
+    std::vector<uint8_t> CheckConfigCollisions(const std::shared_ptr<BaseRobotType>& immutable_robot,
+                                               const std::vector<Configuration, ConfigAlloc>& configs, const double inflation_ratio) const {
+        const DerivedRobotType& robot = Derived(immutable_robot);
+        SetRobot(robot);
+        std::vector<double> c;
+        for (const auto& q : configs) {
+            const std::vector<double> f = robot.ToFlat(q);
+            c.insert(c.end(), f.begin(), f.end());
+        }
+        std::vector<uint8_t> collided(configs.size());
+        dev_->check_configs(c.data(), configs.size(), inflation_ratio, collided.data(), nullptr, "CheckConfigCollisions");
+        return collided;
+    }
     /* the configuration capacity a traced call starts with (a longer trace is re-run once with
      * the exact size); RetriedTraces() counts those re-runs */
     void SetTraceCapacityHint(uint32_t configs) { trace_capacity_hint_ = configs > 0 ? configs : 1; }
@@ -345,9 +377,19 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
     uint64_t RetriedTraces() const { return retried_traces_; }
 
   private:
-    struct Destroy {
-        void operator()(fks_context* c) const { fks_destroy(c); }
-    };
+    static std::unique_ptr<fks::DeviceSet> MakeDevices(const sdf_tools::TaggedObjectCollisionMapGrid& environment,
+                                                       const sdf_tools::SignedDistanceField& environment_sdf,
+                                                       const SurfaceNormalGrid& surface_normals_grid,
+                                                       const SimulatorSolverParameters& solver_config,
+                                                       const double simulation_controller_frequency, const uint64_t prng_seed,
+                                                       const int32_t debug_level, const std::vector<int32_t>& devices) {
+        std::vector<float> sdf_storage; /* the values fks_create uploads (real sdf_tools only) */
+        const fks_environment env =
+            simulator_environment_builder::ToFksEnvironment(environment, environment_sdf, surface_normals_grid, sdf_storage);
+        const fks_solver_params p = solver_config.ToFks();
+        return std::unique_ptr<fks::DeviceSet>(
+            new fks::DeviceSet(env, p, simulation_controller_frequency, prng_seed, debug_level, devices));
+    }
     typedef fks_status (*BatchFn)(fks_context*, const double*, uint64_t, const double*, uint64_t, int32_t, double*, uint8_t*,
                                   uint32_t*, uint32_t*, uint32_t*);
 
@@ -393,14 +435,14 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
         if (d == robot_key_) return;
         robot_key_.reset();
         const fks_robot_desc v = d->View();
-        Check(fks_set_robot(ctx_.get(), &v), ctx_.get(), "fks_set_robot");
+        dev_->set_robot(v);
         robot_key_ = d;
     }
     std::vector<double> Kinematics(const DerivedRobotType& robot, int32_t mode, const std::vector<std::vector<double>>& configs,
                                    const std::vector<std::vector<double>>& inputs = {}) const {
         SetRobot(robot);
         int32_t links = 0, points = 0, dofs = 0, width = 0;
-        Check(fks_robot_sizes(ctx_.get(), &links, &points, &dofs, &width), ctx_.get(), "fks_robot_sizes");
+        Check(fks_robot_sizes(ctx_, &links, &points, &dofs, &width), ctx_, "fks_robot_sizes");
         std::vector<double> c, u;
         for (const auto& q : configs) c.insert(c.end(), q.begin(), q.end());
         for (const auto& q : inputs) u.insert(u.end(), q.begin(), q.end());
@@ -408,7 +450,7 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
             throw std::invalid_argument("control input has the wrong width");
         const size_t per = mode == FKS_KIN_LINK_TRANSFORMS ? 12u * (size_t)links : (mode == FKS_KIN_POINTS ? 3u * (size_t)points : (size_t)width);
         std::vector<double> out(configs.size() * per);
-        Check(fks_kinematics(ctx_.get(), mode, c.data(), configs.size(), u.empty() ? nullptr : u.data(), out.data()), ctx_.get(),
+        Check(fks_kinematics(ctx_, mode, c.data(), configs.size(), u.empty() ? nullptr : u.data(), out.data()), ctx_,
               "fks_kinematics");
         return out;
     }
@@ -432,9 +474,8 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
         last_micro_.assign(n, 0);
         last_resolver_.assign(n, 0);
         last_errors_.assign(n, 0);
-        Check(fn(ctx_.get(), s.data(), n, t.data(), targets.size(), allow_contacts ? 1 : 0, q.data(), collided.data(),
-                 last_micro_.data(), last_resolver_.data(), last_errors_.data()),
-              ctx_.get(), "ForwardSimulateRobots");
+        dev_->simulate(fn == fks_reverse_simulate, s.data(), n, t.data(), targets.size(), allow_contacts, q.data(), collided.data(),
+                       last_micro_.data(), last_resolver_.data(), last_errors_.data(), "ForwardSimulateRobots");
         std::vector<SimulationResult> out;
         out.reserve(n);
         for (size_t i = 0; i < n; ++i) /* SimulationResult(reached, target, collided, true), SPCS:918 */
@@ -472,7 +513,8 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
     SurfaceNormalGrid surface_normals_grid_;
     SimulatorSolverParameters solver_config_;
     double simulation_controller_frequency_;
-    std::unique_ptr<fks_context, Destroy> ctx_;
+    std::unique_ptr<fks::DeviceSet> dev_; /* the devices (DeviceSet: sharded batches, summed statistics) */
+    fks_context* ctx_ = nullptr;          /* devices[0]: single-particle calls, small batches */
     mutable std::shared_ptr<const fks::RobotDescription> robot_key_;
     RNG rng_;
     std::vector<uint32_t> last_errors_, last_micro_, last_resolver_;
@@ -489,40 +531,43 @@ typedef simple_particle_contact_simulator::SimulatorSolverParameters SolverParam
 /* FKS.hpp:13-16 */
 inline SolverParameters GetDefaultSolverParameters() { return SolverParameters(); }
 
-/* FKS.hpp:18-22 / FKS.cpp:4-71: simulate_with_individual_jacobians = false.  `device`
- * (default 0) selects the MI355X; the reference's parameter list is otherwise unchanged. */
-inline uncertainty_planning_core::SE2SimulatorPtr MakeSE2Simulator(
-    const sdf_tools::TaggedObjectCollisionMapGrid& environment, const sdf_tools::SignedDistanceField& environment_sdf,
-    const simple_particle_contact_simulator::SurfaceNormalGrid& surface_normals_grid, const SolverParameters& solver_config,
-    const double simulation_controller_frequency, const uint64_t prng_seed, const int32_t debug_level, const int32_t device = 0) {
-    using namespace uncertainty_planning_core;
-    return SE2SimulatorPtr(new simple_particle_contact_simulator::HipParticleContactSimulator<
-                           tnuva_robot_models::TnuvaSE2Robot<PRNG>, SE2Config, PRNG, SE2ConfigAlloc>(
-        environment, environment_sdf, surface_normals_grid, solver_config, simulation_controller_frequency, false, prng_seed,
-        debug_level, device));
-}
+using fks::AllVisibleDevices;
 
-inline uncertainty_planning_core::SE3SimulatorPtr MakeSE3Simulator(
-    const sdf_tools::TaggedObjectCollisionMapGrid& environment, const sdf_tools::SignedDistanceField& environment_sdf,
-    const simple_particle_contact_simulator::SurfaceNormalGrid& surface_normals_grid, const SolverParameters& solver_config,
-    const double simulation_controller_frequency, const uint64_t prng_seed, const int32_t debug_level, const int32_t device = 0) {
-    using namespace uncertainty_planning_core;
-    return SE3SimulatorPtr(new simple_particle_contact_simulator::HipParticleContactSimulator<
-                           tnuva_robot_models::TnuvaSE3Robot<PRNG>, SE3Config, PRNG, SE3ConfigAlloc>(
-        environment, environment_sdf, surface_normals_grid, solver_config, simulation_controller_frequency, false, prng_seed,
-        debug_level, device));
-}
+/* FKS.hpp:18-22 / FKS.cpp:4-71: simulate_with_individual_jacobians = false.  The reference's
+ * parameter list runs on every visible MI355X (batches sharded by particle, small batches on
+ * the first); an extra `device` or `devices` argument selects them explicitly. */
+#define FKS_DEFINE_FACTORY(NAME, PTR, ROBOT, CONFIG, ALLOC)                                                                          \
+    inline uncertainty_planning_core::PTR NAME(                                                                                   \
+        const sdf_tools::TaggedObjectCollisionMapGrid& environment, const sdf_tools::SignedDistanceField& environment_sdf,        \
+        const simple_particle_contact_simulator::SurfaceNormalGrid& surface_normals_grid, const SolverParameters& solver_config,  \
+        const double simulation_controller_frequency, const uint64_t prng_seed, const int32_t debug_level,                        \
+        const std::vector<int32_t>& devices) {                                                                                    \
+        using namespace uncertainty_planning_core;                                                                                \
+        return PTR(new simple_particle_contact_simulator::HipParticleContactSimulator<tnuva_robot_models::ROBOT<PRNG>, CONFIG, PRNG, \
+                                                                                       ALLOC>(                                     \
+            environment, environment_sdf, surface_normals_grid, solver_config, simulation_controller_frequency, false, prng_seed,  \
+            debug_level, devices));                                                                                               \
+    }                                                                                                                             \
+    inline uncertainty_planning_core::PTR NAME(                                                                                   \
+        const sdf_tools::TaggedObjectCollisionMapGrid& environment, const sdf_tools::SignedDistanceField& environment_sdf,        \
+        const simple_particle_contact_simulator::SurfaceNormalGrid& surface_normals_grid, const SolverParameters& solver_config,  \
+        const double simulation_controller_frequency, const uint64_t prng_seed, const int32_t debug_level,                        \
+        const int32_t device) {                                                                                                   \
+        return NAME(environment, environment_sdf, surface_normals_grid, solver_config, simulation_controller_frequency, prng_seed, \
+                    debug_level, std::vector<int32_t>{device});                                                                   \
+    }                                                                                                                             \
+    inline uncertainty_planning_core::PTR NAME(                                                                                   \
+        const sdf_tools::TaggedObjectCollisionMapGrid& environment, const sdf_tools::SignedDistanceField& environment_sdf,        \
+        const simple_particle_contact_simulator::SurfaceNormalGrid& surface_normals_grid, const SolverParameters& solver_config,  \
+        const double simulation_controller_frequency, const uint64_t prng_seed, const int32_t debug_level) {                     \
+        return NAME(environment, environment_sdf, surface_normals_grid, solver_config, simulation_controller_frequency, prng_seed, \
+                    debug_level, AllVisibleDevices());                                                                            \
+    }
 
-inline uncertainty_planning_core::LinkedSimulatorPtr MakeLinkedSimulator(
-    const sdf_tools::TaggedObjectCollisionMapGrid& environment, const sdf_tools::SignedDistanceField& environment_sdf,
-    const simple_particle_contact_simulator::SurfaceNormalGrid& surface_normals_grid, const SolverParameters& solver_config,
-    const double simulation_controller_frequency, const uint64_t prng_seed, const int32_t debug_level, const int32_t device = 0) {
-    using namespace uncertainty_planning_core;
-    return LinkedSimulatorPtr(new simple_particle_contact_simulator::HipParticleContactSimulator<
-                              tnuva_robot_models::TnuvaLinkedRobot<PRNG>, LinkedConfig, PRNG, LinkedConfigAlloc>(
-        environment, environment_sdf, surface_normals_grid, solver_config, simulation_controller_frequency, false, prng_seed,
-        debug_level, device));
-}
+FKS_DEFINE_FACTORY(MakeSE2Simulator, SE2SimulatorPtr, TnuvaSE2Robot, SE2Config, SE2ConfigAlloc)
+FKS_DEFINE_FACTORY(MakeSE3Simulator, SE3SimulatorPtr, TnuvaSE3Robot, SE3Config, SE3ConfigAlloc)
+FKS_DEFINE_FACTORY(MakeLinkedSimulator, LinkedSimulatorPtr, TnuvaLinkedRobot, LinkedConfig, LinkedConfigAlloc)
+#undef FKS_DEFINE_FACTORY
 
 }  // namespace fast_kinematic_simulator
 

@@ -30,18 +30,10 @@
 #include <utility>
 #include <vector>
 
+#include "fast_kinematic_simulator_amd/device_set.hpp"
 #include "fks_capi.h"
 
 namespace fks {
-
-class SimulatorError : public std::runtime_error {
-  public:
-    SimulatorError(fks_status status, const std::string& what) : std::runtime_error(what), status_(status) {}
-    fks_status status() const { return status_; }
-
-  private:
-    fks_status status_;
-};
 
 inline void check(fks_status st, const fks_context* ctx, const char* what) {
     if (st == FKS_OK) return;
@@ -198,19 +190,19 @@ class RobotDescription {
     }
 };
 
-/* SimpleParticleContactSimulator on one MI355X.  The stacked-Jacobian resolver is
- * always used, as the reference factories hard-wire (FKS.cpp:22,45,68). */
+/* SimpleParticleContactSimulator on one or several MI355X devices (DeviceSet: batches of
+ * at least ShardThreshold() particles are sharded by particle id, bit-identical to one
+ * device).  The stacked-Jacobian resolver is always used, as the reference factories
+ * hard-wire (FKS.cpp:22,45,68). */
 class HipParticleContactSimulator {
   public:
     using DisplayFn = std::function<void(const void*)>;
 
     HipParticleContactSimulator(const fks_environment& environment, const fks_solver_params& solver_config,
                                 double simulation_controller_frequency, uint64_t prng_seed, int32_t debug_level,
-                                int32_t device = 0) {
-        fks_context* ctx = nullptr;
-        check(fks_create(&environment, &solver_config, simulation_controller_frequency, prng_seed, debug_level, device, &ctx),
-              nullptr, "fks_create");
-        ctx_.reset(ctx);
+                                const std::vector<int32_t>& devices)
+        : dev_(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level, devices) {
+        ctx_ = dev_.primary();
         forward_steps_ = (uint32_t)std::max(1.0, solver_config.forward_simulation_time * simulation_controller_frequency);
         resolution_ = environment.collision_map.resolution;
         /* ResetGenerators (SPCS:457-471): the first per-thread generator */
@@ -218,6 +210,16 @@ class HipParticleContactSimulator {
         std::uniform_int_distribution<uint64_t> seed_dist(0, std::numeric_limits<uint64_t>::max());
         rng_ = std::mt19937_64(seed_dist(prng));
     }
+    HipParticleContactSimulator(const fks_environment& environment, const fks_solver_params& solver_config,
+                                double simulation_controller_frequency, uint64_t prng_seed, int32_t debug_level,
+                                int32_t device = 0)
+        : HipParticleContactSimulator(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level,
+                                      std::vector<int32_t>{device}) {}
+
+    const std::vector<int32_t>& Devices() const { return dev_.devices(); }
+    void SetShardThreshold(uint64_t particles) { dev_.set_shard_threshold(particles); }
+    uint64_t ShardThreshold() const { return dev_.shard_threshold(); }
+    bool LastBatchSharded() const { return dev_.last_sharded(); }
 
     /* GetFrame (SPCS:517-520) */
     std::string GetFrame() const { return frame_; }
@@ -232,7 +234,7 @@ class HipParticleContactSimulator {
                                    const std::vector<std::vector<double>>& inputs = {}) {
         SetRobot(robot);
         int32_t links = 0, points = 0, dofs = 0, width = 0;
-        check(fks_robot_sizes(ctx_.get(), &links, &points, &dofs, &width), ctx_.get(), "fks_robot_sizes");
+        check(fks_robot_sizes(ctx_, &links, &points, &dofs, &width), ctx_, "fks_robot_sizes");
         const size_t n = configs.size(), W = (size_t)width;
         std::vector<double> c(n * W), u;
         for (size_t i = 0; i < n; ++i) {
@@ -248,7 +250,7 @@ class HipParticleContactSimulator {
         }
         const size_t per = mode == FKS_KIN_LINK_TRANSFORMS ? 12u * (size_t)links : (mode == FKS_KIN_POINTS ? 3u * (size_t)points : W);
         std::vector<double> out(n * per);
-        check(fks_kinematics(ctx_.get(), mode, c.data(), n, u.empty() ? nullptr : u.data(), out.data()), ctx_.get(),
+        check(fks_kinematics(ctx_, mode, c.data(), n, u.empty() ? nullptr : u.data(), out.data()), ctx_,
               "fks_kinematics");
         return out;
     }
@@ -306,13 +308,12 @@ class HipParticleContactSimulator {
     }
 
     /* SPCS:446-455 */
-    int32_t GetDebugLevel() const { return fks_get_debug_level(ctx_.get()); }
-    int32_t SetDebugLevel(int32_t debug_level) { return fks_set_debug_level(ctx_.get(), debug_level); }
+    int32_t GetDebugLevel() const { return fks_get_debug_level(ctx_); }
+    int32_t SetDebugLevel(int32_t debug_level) { return dev_.set_debug_level(debug_level); }
 
     /* SPCS:488-512: the eight resolve counters, by the reference's names */
     std::vector<std::pair<std::string, double>> GetStatistics() const {
-        fks_statistics s;
-        check(fks_get_statistics(ctx_.get(), &s), ctx_.get(), "GetStatistics");
+        const fks_statistics s = dev_.statistics();
         return {{"successful_resolves", (double)s.successful_resolves},
                 {"unsuccessful_resolves", (double)s.unsuccessful_resolves},
                 {"free_resolves", (double)s.free_resolves},
@@ -322,9 +323,9 @@ class HipParticleContactSimulator {
                 {"unsuccessful_self_collision_resolves", (double)s.unsuccessful_self_collision_resolves},
                 {"recovered_unsuccessful_resolves", (double)s.recovered_unsuccessful_resolves}};
     }
-    void ResetStatistics() { check(fks_reset_statistics(ctx_.get()), ctx_.get(), "ResetStatistics"); }
+    void ResetStatistics() { dev_.reset_statistics(); }
     /* SPCS:457-471 */
-    void ResetGenerators(uint64_t prng_seed) { check(fks_reset_generators(ctx_.get(), prng_seed), ctx_.get(), "ResetGenerators"); }
+    void ResetGenerators(uint64_t prng_seed) { dev_.reset_generators(prng_seed); }
 
     /* ForwardSimulateRobots (SPCS:788-804).  display_fn is accepted for interface
      * parity; the batch path never draws (SPCS:801 passes enable_tracing=false). */
@@ -366,9 +367,9 @@ class HipParticleContactSimulator {
         uint32_t num_steps = 0, num_configs = 0, microsteps = 0, resolver = 0, errors = 0;
         uint8_t collided = 0;
         fks_trace t{step_cap, cfg_cap, inputs.data(), micro.data(), configs.data(), tags.data(), &num_steps, &num_configs};
-        check(fks_forward_simulate_traced(ctx_.get(), start_position.data(), 1, target_position.data(), 1, allow_contacts ? 1 : 0,
+        check(fks_forward_simulate_traced(ctx_, start_position.data(), 1, target_position.data(), 1, allow_contacts ? 1 : 0,
                                           out.data(), &collided, &microsteps, &resolver, &errors, &t),
-              ctx_.get(), "ForwardSimulateRobot");
+              ctx_, "ForwardSimulateRobot");
         trace.truncated = trace.truncated || num_steps > step_cap || num_configs > cfg_cap;
         const size_t base = trace.resolver_steps.size(); /* the reference appends to the caller's trace */
         for (uint32_t k = 0; k < num_steps && k < step_cap; ++k) {
@@ -420,18 +421,15 @@ class HipParticleContactSimulator {
             std::copy(configs[i].begin(), configs[i].end(), c.begin() + i * W);
         }
         std::vector<uint8_t> collided(n);
-        check(fks_check_config_collision(ctx_.get(), c.data(), n, inflation_ratio, collided.data(), nullptr), ctx_.get(),
-              "CheckConfigCollision");
+        dev_.check_configs(c.data(), n, inflation_ratio, collided.data(), nullptr, "CheckConfigCollision");
         return std::vector<bool>(collided.begin(), collided.end());
     }
 
-    fks_context* context() { return ctx_.get(); }
+    fks_context* context() { return ctx_; }
 
   private:
-    struct Destroy {
-        void operator()(fks_context* c) const { fks_destroy(c); }
-    };
-    std::unique_ptr<fks_context, Destroy> ctx_;
+    DeviceSet dev_;
+    fks_context* ctx_ = nullptr; /* devices[0] */
     std::vector<unsigned char> robot_fingerprint_; /* the robot set last (RobotDescription::Fingerprint) */
     uint32_t forward_steps_ = 1; /* controller steps per simulation (SPCS:856): the trace's step capacity */
     double resolution_ = 0.0;
@@ -445,7 +443,7 @@ class HipParticleContactSimulator {
         if (!robot_fingerprint_.empty() && fp == robot_fingerprint_) return;
         robot_fingerprint_.clear();
         const fks_robot_desc d = robot.View();
-        check(fks_set_robot(ctx_.get(), &d), ctx_.get(), "fks_set_robot");
+        dev_.set_robot(d);
         robot_fingerprint_ = std::move(fp);
     }
 
@@ -468,10 +466,8 @@ class HipParticleContactSimulator {
         }
         std::vector<uint8_t> collided(n);
         std::vector<uint32_t> micro(n), resolver(n), errors(n);
-        auto fn = reverse ? fks_reverse_simulate : fks_forward_simulate;
-        check(fn(ctx_.get(), s.data(), n, t.data(), targets.size(), allow_contacts ? 1 : 0, out.data(), collided.data(),
-                 micro.data(), resolver.data(), errors.data()),
-              ctx_.get(), reverse ? "ReverseSimulateRobots" : "ForwardSimulateRobots");
+        dev_.simulate(reverse, s.data(), n, t.data(), targets.size(), allow_contacts, out.data(), collided.data(), micro.data(),
+                      resolver.data(), errors.data(), reverse ? "ReverseSimulateRobots" : "ForwardSimulateRobots");
         std::vector<SimulationResult> results(n);
         for (size_t i = 0; i < n; ++i) {
             SimulationResult& r = results[i];
@@ -487,31 +483,37 @@ class HipParticleContactSimulator {
     }
 };
 
-/* fast_kinematic_simulator::Make{SE2,SE3,Linked}Simulator (FKS.cpp:4-71) */
-inline std::shared_ptr<HipParticleContactSimulator> MakeSE2Simulator(const fks_environment& environment,
-                                                                     const fks_solver_params& solver_config,
-                                                                     double simulation_controller_frequency,
-                                                                     uint64_t prng_seed, int32_t debug_level,
-                                                                     int32_t device = 0) {
-    return std::make_shared<HipParticleContactSimulator>(environment, solver_config, simulation_controller_frequency,
-                                                         prng_seed, debug_level, device);
+/* fast_kinematic_simulator::Make{SE2,SE3,Linked}Simulator (FKS.cpp:4-71).  Without a device
+ * argument the simulator runs on every visible MI355X (batches sharded by particle); `device`
+ * or `devices` select them explicitly. */
+inline std::shared_ptr<HipParticleContactSimulator> MakeSimulator(const fks_environment& environment, const fks_solver_params& solver_config,
+                                                                  double simulation_controller_frequency, uint64_t prng_seed,
+                                                                  int32_t debug_level, const std::vector<int32_t>& devices) {
+    return std::make_shared<HipParticleContactSimulator>(environment, solver_config, simulation_controller_frequency, prng_seed,
+                                                         debug_level, devices);
 }
-inline std::shared_ptr<HipParticleContactSimulator> MakeSE3Simulator(const fks_environment& environment,
-                                                                     const fks_solver_params& solver_config,
-                                                                     double simulation_controller_frequency,
-                                                                     uint64_t prng_seed, int32_t debug_level,
-                                                                     int32_t device = 0) {
-    return std::make_shared<HipParticleContactSimulator>(environment, solver_config, simulation_controller_frequency,
-                                                         prng_seed, debug_level, device);
-}
-inline std::shared_ptr<HipParticleContactSimulator> MakeLinkedSimulator(const fks_environment& environment,
-                                                                        const fks_solver_params& solver_config,
-                                                                        double simulation_controller_frequency,
-                                                                        uint64_t prng_seed, int32_t debug_level,
-                                                                        int32_t device = 0) {
-    return std::make_shared<HipParticleContactSimulator>(environment, solver_config, simulation_controller_frequency,
-                                                         prng_seed, debug_level, device);
-}
+#define FKS_WRAPPER_FACTORY(NAME)                                                                                                 \
+    inline std::shared_ptr<HipParticleContactSimulator> NAME(const fks_environment& environment, const fks_solver_params& solver_config, \
+                                                             double simulation_controller_frequency, uint64_t prng_seed,        \
+                                                             int32_t debug_level, const std::vector<int32_t>& devices) {       \
+        return MakeSimulator(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level, devices);     \
+    }                                                                                                                            \
+    inline std::shared_ptr<HipParticleContactSimulator> NAME(const fks_environment& environment, const fks_solver_params& solver_config, \
+                                                             double simulation_controller_frequency, uint64_t prng_seed,        \
+                                                             int32_t debug_level, int32_t device) {                            \
+        return MakeSimulator(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level,               \
+                             std::vector<int32_t>{device});                                                                     \
+    }                                                                                                                            \
+    inline std::shared_ptr<HipParticleContactSimulator> NAME(const fks_environment& environment, const fks_solver_params& solver_config, \
+                                                             double simulation_controller_frequency, uint64_t prng_seed,        \
+                                                             int32_t debug_level) {                                             \
+        return MakeSimulator(environment, solver_config, simulation_controller_frequency, prng_seed, debug_level,               \
+                             AllVisibleDevices());                                                                              \
+    }
+FKS_WRAPPER_FACTORY(MakeSE2Simulator)
+FKS_WRAPPER_FACTORY(MakeSE3Simulator)
+FKS_WRAPPER_FACTORY(MakeLinkedSimulator)
+#undef FKS_WRAPPER_FACTORY
 
 }  // namespace fks
 

@@ -37,7 +37,23 @@
 #ifndef FKS_CAPI_H
 #define FKS_CAPI_H
 
+#if defined(__HIPCC_RTC__)
+/* run-time compilation of shape-specialised kernels (fks_specialize): hiprtc's prelude
+ * declares the fixed-width types in its own namespace and has no libc headers */
+using __hip_internal::int16_t;
+using __hip_internal::int32_t;
+using __hip_internal::int64_t;
+using __hip_internal::int8_t;
+using __hip_internal::uint16_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+using __hip_internal::uint8_t;
+#ifndef INT32_MIN
+#define INT32_MIN (-2147483647 - 1)
+#endif
+#else
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -49,7 +65,7 @@ extern "C" {
  * environment builder's public steps (fks_env_discretize_obstacle, fks_env_build_normals,
  * fks_env_cell_objects), fks_set_statistics / fks_set_total_counters.
  * 7: fks_set_small_batch_kernel */
-#define FKS_ABI_VERSION 7
+#define FKS_ABI_VERSION 8
 
 typedef enum {
     FKS_OK = 0,
@@ -450,6 +466,29 @@ fks_status fks_set_small_batch_kernel(fks_context* ctx, int32_t enabled);
  * FKS.cpp:22,45,68 hard-wire, the default), 1 = ComputeResolverCorrectionStepIndividualJacobians
  * (SPCS:1966-1988: one ColPivHouseholderQR solve per corrected point, summed in point order). */
 fks_status fks_set_individual_jacobians(fks_context* ctx, int32_t simulate_with_individual_jacobians);
+/* Robot-shape specialisation (ABI 8; no reference counterpart, results are bit-identical
+ * either way).  With `enabled`, the plain throughput simulation (fks_forward_simulate*,
+ * not traced, individual-Jacobian or small-batch calls) of the current robot and of every
+ * robot set later runs a kernel compiled at run time (hiprtc) from the library's own kernel
+ * source with the robot's link / joint / dof / geometry counts and LDS and scratch carve-outs
+ * as constants (cfg3: 11-12 % faster).  The first robot of a shape costs one
+ * compile (tens of seconds, in the calling thread: fks_set_specialization, then
+ * fks_set_robot); code objects are cached per process and on disk (FKS_KERNEL_CACHE=<dir>,
+ * default ~/.cache/fast_kinematic_simulator_amd; "off" disables it).  Returns
+ * FKS_ERR_UNSUPPORTED with the compiler log in fks_get_last_error when the current robot's
+ * kernel cannot be built (its calls then keep the generic kernel); 0 = generic kernels only.
+ * The default is 0, or 1 when the environment variable FKS_SPECIALIZE=1 is set at fks_create. */
+fks_status fks_set_specialization(fks_context* ctx, int32_t enabled);
+typedef struct fks_specialization_info {
+    int32_t enabled;         /* fks_set_specialization */
+    int32_t active;          /* the current robot's plain simulation calls run the shape-specialised kernel */
+    int32_t from_cache;      /* its code object came from the process or disk cache */
+    int32_t reserved;
+    double compile_seconds;  /* hiprtc time of that code object (0 when it came from a cache) */
+    uint64_t launches;       /* launches of the specialised kernel since the robot was set */
+    char shape[64];          /* the shape key, e.g. "t0-L8-J7-D7-W7-G8-P512-p1-l0" */
+} fks_specialization_info;
+fks_status fks_get_specialization(const fks_context* ctx, fks_specialization_info* out);
 
 /* sums over every call since fks_create / fks_reset_total_counters */
 fks_status fks_get_total_counters(const fks_context* ctx, fks_call_counters* out);
@@ -569,6 +608,13 @@ fks_status fks_multi_get_statistics(const fks_multi_context* m, fks_statistics* 
 fks_status fks_multi_reset_statistics(fks_multi_context* m);
 fks_status fks_multi_get_last_call_counters(const fks_multi_context* m, fks_call_counters* out);
 fks_status fks_multi_set_call_index(fks_multi_context* m, uint64_t call_index);
+/* Batched CheckConfigCollision (SPCS:1398-1416) over all devices: configuration i on the
+ * device whose fks_shard_bounds range holds it; arguments as fks_check_config_collision. */
+fks_status fks_multi_check_config_collision(fks_multi_context* m, const double* configs, uint64_t n, double inflation_ratio,
+                                            uint8_t* out_collided, uint32_t* out_error_flags);
+/* Number of MI355X devices visible to this process (HIP_VISIBLE_DEVICES applies); 0 when there
+ * is none.  The planner-facing factories default to all of them (fast_kinematic_simulator.hpp). */
+int32_t fks_device_count(void);
 
 /* Device self-test of the portable libm against the host (bit equality). */
 fks_status fks_selftest_math(int32_t device, uint64_t n, uint64_t* out_mismatches);

@@ -28,7 +28,9 @@
 #ifndef FKS_PORTABLE_MATH_H
 #define FKS_PORTABLE_MATH_H
 
+#if !defined(__HIPCC_RTC__)
 #include <stdint.h>
+#endif
 
 #if defined(__HIPCC__)
 #define FKS_HD __host__ __device__

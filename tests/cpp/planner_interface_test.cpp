@@ -129,6 +129,25 @@ static simple_robot_models::PointSphereGeometry read_points(Reader& r) {
 /* --dump: the flattened robot the GPU receives and the flat starts / targets (no GPU needed) */
 static bool g_dump = false;
 
+/* the devices the simulators run on: FKS_TEST_DEVICES="0,0" (a list), "all" (every visible
+ * device, the factories' default), unset = {0}; FKS_TEST_SHARD=<n> sets the shard threshold
+ * (1: every batch is sharded over the list).  The printed results must not depend on either. */
+static std::vector<int32_t> test_devices() {
+    const char* e = std::getenv("FKS_TEST_DEVICES");
+    if (!e || !e[0]) return {0};
+    if (std::string(e) == "all") return fks::AllVisibleDevices();
+    std::vector<int32_t> d;
+    std::stringstream ss(e);
+    std::string tok;
+    while (std::getline(ss, tok, ',')) d.push_back((int32_t)std::stoi(tok));
+    return d;
+}
+template <typename Hip>
+static void apply_shard_threshold(Hip* hip) {
+    const char* e = std::getenv("FKS_TEST_SHARD");
+    if (hip && e && e[0]) hip->SetShardThreshold(std::strtoull(e, nullptr, 10));
+}
+
 /* FNV-1a of a byte range (environment fingerprints in --dump) */
 static uint64_t fnv(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
     const unsigned char* b = static_cast<const unsigned char*>(p);
@@ -280,7 +299,9 @@ static void custom_normals(const Scene& s, const std::shared_ptr<Robot>& robot, 
     if (off[cells]) std::fwrite(grid.CsrEntries(), sizeof(double), 6 * (size_t)off[cells], f);
     std::fclose(f);
     upc::LinkedSimulatorPtr sim = fast_kinematic_simulator::MakeLinkedSimulator(E.GetEnvironment(), E.GetEnvironmentSDF(), grid, s.solver,
-                                                                                s.frequency, s.seed, 0);
+                                                                                s.frequency, s.seed, 0, test_devices());
+    apply_shard_threshold(dynamic_cast<simple_particle_contact_simulator::HipParticleContactSimulator<
+                              tnuva_robot_models::TnuvaLinkedRobot<upc::PRNG>, upc::LinkedConfig, upc::PRNG, upc::LinkedConfigAlloc>*>(sim.get()));
     const auto res_c = sim->ForwardSimulateRobots(robot, starts, targets, s.allow, {});
     for (size_t i = 0; i < res_c.size(); ++i) {
         std::printf("custom %zu", i);
@@ -301,8 +322,12 @@ static int exercise(const Scene& s, const std::shared_ptr<simple_simulator_inter
         for (double v : robot->ToFlat(res.result_config)) hex(v);
         std::printf(" %d %d\n", res.did_contact ? 1 : 0, res.outcome_is_valid ? 1 : 0);
     };
+    auto* hip = dynamic_cast<simple_particle_contact_simulator::HipParticleContactSimulator<Robot, Config, upc::PRNG, Alloc>*>(sim.get());
+    if (!hip) throw std::runtime_error("the factory did not return the HIP simulator");
+    apply_shard_threshold(hip);
     /* call index 0: ForwardSimulateRobots (SPCS:788) */
     const auto fwd = sim->ForwardSimulateRobots(base, starts, targets, s.allow, [](const fks_planner_types::MarkerArray&) {});
+    std::fprintf(stderr, "devices %zu sharded %d\n", hip->Devices().size(), hip->LastBatchSharded() ? 1 : 0);
     for (size_t i = 0; i < fwd.size(); ++i) print("fwd", i, fwd[i]);
     for (const auto& kv : sim->GetStatistics()) std::printf("stat %s %.0f\n", kv.first.c_str(), kv.second);
     /* call index 1: ReverseSimulateRobots (SPCS:806) */
@@ -312,8 +337,6 @@ static int exercise(const Scene& s, const std::shared_ptr<simple_simulator_inter
      * trace capacity of 8 configurations so the longer trace is re-run at its exact size; the
      * statistics must count the particle once (reset before, printed after) */
     typename Interface::ForwardSimulationStepTrace trace;
-    auto* hip = dynamic_cast<simple_particle_contact_simulator::HipParticleContactSimulator<Robot, Config, upc::PRNG, Alloc>*>(sim.get());
-    if (!hip) throw std::runtime_error("the factory did not return the HIP simulator");
     hip->SetTraceCapacityHint(8);
     sim->ResetStatistics();
     const auto tr = sim->ForwardSimulateRobot(base, starts[0], targets[0], s.allow, trace, true, {});
@@ -329,6 +352,12 @@ static int exercise(const Scene& s, const std::shared_ptr<simple_simulator_inter
     /* CheckConfigCollision (SPCS:1398) of every reached configuration, inflation 0.5 */
     std::printf("check");
     for (const auto& r : fwd) std::printf(" %d", sim->CheckConfigCollision(base, r.result_config, 0.5) ? 1 : 0);
+    std::printf("\n");
+    /* the same configurations in one batched call (sharded like the simulation batches) */
+    std::vector<Config, Alloc> reached;
+    for (const auto& r : fwd) reached.push_back(r.result_config);
+    std::printf("check_batch");
+    for (uint8_t c : hip->CheckConfigCollisions(base, reached, 0.5)) std::printf(" %d", (int)c);
     std::printf("\n");
     /* call indices 3 and 4: ForwardSimulateMutableRobot (SPCS:843) twice on one robot, the
      * second continuing the first's controllers */
@@ -425,7 +454,7 @@ int main(int argc, char** argv) {
                 return 0;
             }
             upc::LinkedSimulatorPtr sim = fast_kinematic_simulator::MakeLinkedSimulator(
-                E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
+                E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0, test_devices());
             const int rc = exercise<upc::LinkedConfig, upc::LinkedConfigAlloc>(s, sim, robot, starts, targets);
             if (rc != 0) return rc;
             step_by_hand(s, *robot, starts[0], targets[0]);
@@ -489,7 +518,7 @@ int main(int argc, char** argv) {
                 return 0;
             }
             upc::SE2SimulatorPtr sim = fast_kinematic_simulator::MakeSE2Simulator(
-                E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
+                E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0, test_devices());
             const int rc = exercise<upc::SE2Config, upc::SE2ConfigAlloc>(s, sim, robot, starts, targets);
             if (rc == 0) step_by_hand(s, *robot, starts[0], targets[0]);
             return rc;
@@ -514,7 +543,7 @@ int main(int argc, char** argv) {
             return 0;
         }
         upc::SE3SimulatorPtr sim = fast_kinematic_simulator::MakeSE3Simulator(
-            E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0);
+            E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0, test_devices());
         const int rc = exercise<upc::SE3Config, upc::SE3ConfigAlloc>(s, sim, robot, starts, targets);
         if (rc == 0) step_by_hand(s, *robot, starts[0], targets[0]);
         return rc;

@@ -8,7 +8,7 @@ COUNTER_KEYS = ("microsteps", "resolver_iterations", "controller_steps", "sdf_by
 
 
 def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, first_particle_id=0, sim=None,
-             individual_jacobians=False, segment_steps=None, small_batch_kernel=None):
+             individual_jacobians=False, segment_steps=None, small_batch_kernel=None, specialize=False):
     import oracle
     from fast_kinematic_simulator_amd import make_linked_simulator
 
@@ -25,10 +25,21 @@ def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, f
         sim.set_segment_steps(segment_steps)
     if small_batch_kernel is not None:
         sim.set_small_batch_kernel(small_batch_kernel)
+    if specialize:
+        # the robot-shape-specialised throughput kernel (fks_set_specialization); small batches
+        # would otherwise run the small-batch kernel
+        sim.set_robot(wl.robot)
+        sim.set_specialization(True)
+        sim.set_small_batch_kernel(False)
+        before = sim.specialization()["launches"]
     sim.set_call_index(call_index)
     g = sim.forward_simulate_arrays(wl.robot, starts, targets, allow)
     g["statistics"] = sim.get_statistics()
     g["counters"] = sim.last_call_counters()
+    if specialize:
+        info = sim.specialization()
+        assert info["active"] and info["launches"] == before + 1, info
+        g["specialization"] = info
     if own:
         sim.close()
     o = oracle.forward_simulate(env, wl.robot, wl.solver, wl.controller_frequency, wl.seed, starts, targets, allow,

@@ -109,6 +109,21 @@ def test_bench_refuses_world_size_mismatch():
     assert p.returncode == 2 and "WORLD_SIZE=2" in p.stderr
 
 
+def test_bench_takes_world_size_without_gpus_flag():
+    """A launcher that starts `bench.py` without --gpus: the rank count comes from WORLD_SIZE
+    (only an explicit, different --gpus is refused)."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    p = _run_bench(["--particles", "64", "--no-cpu-baseline", "--dry-run"], env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert _json_lines(p.stdout)[0]["n_gpus"] == 1
+
+
 @pytest.mark.gpu
 def test_bench_spawns_ranks_on_gpus():
     """The real RCCL path of `bench.py --gpus 2` (two GPUs, one rank each)."""

@@ -100,17 +100,25 @@ def _hexrow(row):
     return np.array([float.fromhex(v) for v in row])
 
 
-def _run(name, workspace=False, normals=False):
+def _run(name, workspace=False, normals=False, devices=None, shard=None):
     """Run the planner program on a scene; with normals=True (linked) it also builds a
-    surface-normal grid through the SurfaceNormalGrid API and returns its CSR as p.normals."""
+    surface-normal grid through the SurfaceNormalGrid API and returns its CSR as p.normals.
+    devices ("0,0", "all") and shard (threshold) select the simulators' device list."""
     family, wl, obstacles, grid = _scene(name)
     exe = build_planner_test(workspace=workspace)
+    env = dict(os.environ)
+    env.pop("FKS_TEST_DEVICES", None)
+    env.pop("FKS_TEST_SHARD", None)
+    if devices is not None:
+        env["FKS_TEST_DEVICES"] = devices
+    if shard is not None:
+        env["FKS_TEST_SHARD"] = str(shard)
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "scene.txt")
         _write_scene(path, family, wl, obstacles, grid)
         out = os.path.join(d, "normals.bin")
         p = subprocess.run([exe, path] + (["--normals-out", out] if normals else []), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                           text=True, timeout=600)
+                           text=True, timeout=600, env=env)
         p.normals = open(out, "rb").read() if normals and os.path.exists(out) else None
     return p, family, wl, obstacles, grid
 
@@ -215,6 +223,7 @@ def test_planner_interface_matches_oracle(fks_lib, oracle_lib, name, workspace):
     fwd = run(wl.starts, wl.targets, 0)
     c = oracle.check_config_collision(env, wl.robot, wl.solver, fwd["positions"], 0.5)
     assert [int(v) for v in rows["check"][0]] == [int(v) for v in c["collided"]]
+    assert rows["check_batch"][0] == rows["check"][0]  # the batched CheckConfigCollisions
     # mutable robot: the second call continues the first call's controllers
     D = wl.robot.num_dofs
     state = np.zeros((1, 2 * D))
@@ -265,6 +274,31 @@ def test_planner_interface_matches_oracle(fks_lib, oracle_lib, name, workspace):
         other = np.array([_hexrow(r[2:2 + W_]) for r in rows["alt_other"] if int(r[0]) == 5])
         same5 = run(wl.starts, wl.targets, 5)["positions"]
         assert other.shape == same5.shape and not np.array_equal(other, same5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["linked", "se2", "se3"])
+def test_planner_interface_sharded_over_device_lists(fks_lib, name):
+    """The planner drop-in over several devices (DeviceSet / fks_create_multi): with the shard
+    threshold at 1 every batch call (ForwardSimulateRobots, ReverseSimulateRobots, the batched
+    CheckConfigCollisions, the alternating-robot calls) is split by particle id over the list,
+    and everything the program prints — results, statistics, traces, mutable-robot state —
+    is byte-identical to the one-device run that test_planner_interface_matches_oracle pins
+    to the oracle.  [0, 0] exercises two contexts on one MI355X; "all" is the factories'
+    default (every visible device)."""
+    base, *_ = _run(name, normals=(name == "linked"))
+    assert base.returncode == 0, base.stderr
+    assert "devices 1 sharded 0" in base.stderr
+    for devices in ("0,0", "0,0,0", "all"):
+        p, *_ = _run(name, normals=(name == "linked"), devices=devices, shard=1)
+        assert p.returncode == 0, (devices, p.stderr)
+        ndev = len(devices.split(",")) if devices != "all" else int(_capi.lib().fks_device_count())
+        assert f"devices {ndev} sharded {1 if ndev > 1 else 0}" in p.stderr, (devices, p.stderr)
+        assert p.stdout == base.stdout, devices
+        assert p.normals == base.normals
+    # the automatic threshold (one device's resident waves) keeps these small batches whole
+    p, *_ = _run(name, devices="0,0")
+    assert p.returncode == 0 and "devices 2 sharded 0" in p.stderr, p.stderr
 
 
 @pytest.mark.parametrize("name", ["linked", "se2", "se3"])

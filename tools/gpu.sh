@@ -71,6 +71,14 @@ run_task() {
     timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $D/wait -o tail -- $T1 > $D.wait.log 2>&1 &&
     timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 --kernel-trace --output-format csv -d $D/valu -o tail -- $T1 > $D.valu.log 2>&1
     rc=$?; unset FKS_LIB_PATH FKS_VARIANT_LIB; return $rc ;;
+  mix:*)
+    spec=${1#mix:}; w=${spec%%:*}; l=$(lib ${spec#*:}); n=$(basename $l .so); D=$O/${TAG}_mix_${w}_$n
+    BM="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0 --workload $w"
+    export FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1
+    timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES --kernel-trace --output-format csv -d $D/mix -o m -- $BM > $D.mix.log 2>&1 &&
+    timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $D/wait -o m -- $BM > $D.wait.log 2>&1 &&
+    timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $D/more -o m -- $BM > $D.more.log 2>&1
+    rc=$?; unset FKS_LIB_PATH FKS_VARIANT_LIB; return $rc ;;
   sched:*)
     spec=${1#sched:}; w=${spec%%:*}; rest=${spec#*:}; seg=${rest%%:*}; heavy=${rest#*:}
     timeout -k 10 600 python tools/sched_sweep.py --workload $w --segments $seg --heavy $heavy --prio 1 --json $O/${TAG}_sched_$w.json > $O/${TAG}_sched_$w.log 2>&1 ;;
