@@ -372,7 +372,8 @@ static fks_status spec_prepare(fks_context* ctx) {
     sh.lean = ctx->lean ? 1 : 0;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     std::string log;
-    const std::shared_ptr<const fks_spec::CodeObject> co = fks_spec::code_object(sh, &log);
+    bool compiled = false;
+    const std::shared_ptr<const fks_spec::CodeObject> co = fks_spec::code_object(sh, &log, &compiled);
     if (!co) return fail(ctx, FKS_ERR_UNSUPPORTED, "shape specialisation: " + log);
     hipModule_t m = nullptr;
     hipFunction_t f = nullptr;
@@ -399,8 +400,8 @@ static fks_status spec_prepare(fks_context* ctx) {
     ctx->spec_module = m;
     ctx->spec_fn = f;
     ctx->spec_shape = fks_spec::shape_key(sh);
-    ctx->spec_seconds = co->compile_seconds;
-    ctx->spec_from_cache = co->compile_seconds > 0.0 ? 0 : 1;
+    ctx->spec_seconds = compiled ? co->compile_seconds : 0.0;
+    ctx->spec_from_cache = compiled ? 0 : 1;
     return FKS_OK;
 }
 

@@ -41,9 +41,9 @@ struct CodeObject {
 };
 
 /* The code object of `fks_simulate_shaped` for shape `s`: from the process cache, the disk
- * cache, or a hiprtc compile (seconds; one compile at a time per process).  On failure
- * returns null and sets *log. */
-std::shared_ptr<const CodeObject> code_object(const Shape& s, std::string* log);
+ * cache, or a hiprtc compile (seconds; one compile at a time per process; *compiled says
+ * which).  On failure returns null and sets *log. */
+std::shared_ptr<const CodeObject> code_object(const Shape& s, std::string* log, bool* compiled);
 
 /* an unsigned field of the (single) kernel's entry in a code object's AMDGPU metadata note
  * (MessagePack: the key string followed by a positive integer), e.g. ".vgpr_count"; -1 if
