@@ -190,6 +190,29 @@ class SpecializationInfo(ctypes.Structure):
         return d
 
 
+class LaunchInfo(ctypes.Structure):
+    """fks_launch_info (ABI 8)"""
+    _fields_ = [
+        ("resident_waves", c_uint32),
+        ("waves_per_group", c_uint32),
+        ("lds_bytes_per_group", c_uint64),
+        ("small_batch_resident_waves", c_uint32),
+        ("standard_layout_resident_waves", c_uint32),
+        ("fk_pair", c_int32),
+        ("lean", c_int32),
+        ("last_kernel", c_int32),
+        ("reserved", c_int32),
+    ]
+
+    def as_dict(self):
+        d = {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
+        d["last_kernel"] = KERNEL_KINDS.get(d["last_kernel"], d["last_kernel"])
+        return d
+
+
+KERNEL_KINDS = {0: "none", 1: "throughput", 2: "small_batch", 3: "shaped", 4: "traced", 5: "individual"}
+
+
 class Trace(ctypes.Structure):
     """fks_trace: ForwardSimulationStepTrace flattened per particle (include/fks_capi.h)."""
     _fields_ = [
@@ -291,6 +314,7 @@ PROTOTYPES = [
     ("fks_set_segment_policy", c_int32, [c_void_p, c_uint32, c_uint32]),
     ("fks_set_small_batch_kernel", c_int32, [c_void_p, c_int32]),
     ("fks_set_specialization", c_int32, [c_void_p, c_int32]),
+    ("fks_get_launch_info", c_int32, [c_void_p, POINTER(LaunchInfo)]),
     ("fks_get_specialization", c_int32, [c_void_p, POINTER(SpecializationInfo)]),
     ("fks_set_individual_jacobians", c_int32, [c_void_p, c_int32]),
     ("fks_env_build", c_int32, [POINTER(Obstacle), c_int32, c_double, POINTER(c_double), POINTER(c_int64), POINTER(c_void_p)]),

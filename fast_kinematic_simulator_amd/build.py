@@ -15,11 +15,12 @@ ROOT = os.path.dirname(PKG)
 SOURCES = ["csrc/fks_kernels.hip", "csrc/fks_capi.cpp", "csrc/fks_multi.cpp", "csrc/fks_env_builder.cpp", "csrc/fks_env_gpu.hip",
            "csrc/fks_robot_control.cpp", "csrc/fks_specialize.cpp"]
 HEADERS = ["csrc/fks_device.h", "csrc/fks_env_internal.h", "csrc/fks_se3.h", "csrc/fks_specialize.h", "../include/fks_capi.h",
-           "../include/fks_portable_math.h"]
+           "../include/fks_portable_math.h", "../include/fks_control.h"]
 # the kernel source and the headers it includes, carried inside the library for the run-time
 # compilation of shape-specialised kernels (fks_specialize.cpp): name as included -> path
 EMBEDDED = [("fks_kernels.hip", "csrc/fks_kernels.hip"), ("fks_device.h", "csrc/fks_device.h"), ("fks_se3.h", "csrc/fks_se3.h"),
-            ("fks_capi.h", "../include/fks_capi.h"), ("fks_portable_math.h", "../include/fks_portable_math.h")]
+            ("fks_capi.h", "../include/fks_capi.h"), ("fks_portable_math.h", "../include/fks_portable_math.h"),
+            ("fks_control.h", "../include/fks_control.h")]
 GENERATED = os.path.join(ROOT, "build", "generated")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 

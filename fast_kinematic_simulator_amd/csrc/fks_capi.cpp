@@ -275,6 +275,8 @@ struct fks_context {
     int32_t small_batch = 1;          /* fks_set_small_batch_kernel */
     bool fk_pair = false;             /* paired FK of free microsteps (fks_set_robot) */
     bool lean = false;                /* lean LDS block + lean kernels (fks_set_robot) */
+    uint32_t standard_resident_waves = 0; /* resident waves of the non-lean layout (fks_get_launch_info) */
+    int32_t last_kernel = FKS_KERNEL_NONE; /* the simulation kernel of the last call */
     double* d_seg_state = nullptr;
     uint32_t* d_seg_done = nullptr;
     size_t cap_seg_state = 0, cap_seg_done = 0;
@@ -490,10 +492,16 @@ static fks_status create_impl(const fks_environment* henv, const fks_device_env*
         if ((e = dev_upload(&ctx->d_sdf, henv->sdf_values, cells)) != hipSuccess) return bail(e, "sdf upload");
         analyzed = analyze_sdf(henv->sdf_values, henv->sdf.num_cells[0], henv->sdf.num_cells[1], henv->sdf.num_cells[2],
                                henv->sdf.resolution, &lp, &cm);
-        if (henv->normal_offsets && henv->normal_entries) {
+        /* an initialized grid with no stored entries (every cell empty: a lookup in bounds finds
+         * the zero normal, SPCS:219-222) has offsets and may have no entry array */
+        if (henv->normal_offsets) {
             const size_t ncells =
                 (size_t)henv->normals.num_cells[0] * (size_t)henv->normals.num_cells[1] * (size_t)henv->normals.num_cells[2];
             const size_t entries = henv->normal_offsets[ncells];
+            if (entries > 0 && !henv->normal_entries) {
+                fks_destroy(ctx);
+                return FKS_ERR_INVALID_ARGUMENT;
+            }
             if ((e = dev_upload(&ctx->d_noff, henv->normal_offsets, ncells + 1)) != hipSuccess)
                 return bail(e, "normal offsets upload");
             if (entries > 0 && (e = dev_upload(&ctx->d_nent, henv->normal_entries, 6 * entries)) != hipSuccess)
@@ -641,6 +649,7 @@ static fks_status launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
         pair = blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, true), fksd::kWavesPerGroup, &w, &b) >= w0;
     }
     int waves_per_cu = blocks(fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, pair), fksd::kWavesPerGroup, &wpg, &bytes);
+    const int standard_waves_per_cu = waves_per_cu;
     /* a linked robot whose LDS block caps the resident waves below the register limit may run
      * lean blocks (the skip-proof cache in scratch) in workgroups of up to 8 waves, if that
      * keeps more waves resident (cfg5's 14-dof arm: 12 -> 16 per CU) */
@@ -685,6 +694,7 @@ static fks_status launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
     }
     ctx->fk_pair = pair;
     ctx->lean = lean;
+    ctx->standard_resident_waves = (uint32_t)(cus * std::max(0, standard_waves_per_cu));
     ctx->waves_per_group = wpg;
     ctx->lds_bytes = bytes;
     ctx->grid_groups = grid_groups;
@@ -1196,6 +1206,9 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     /* the plain throughput path runs the robot's shape-specialised kernel when there is one */
     const bool shaped = ctx->spec_fn && !tr && !small && !ctx->individual_jacobians;
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
+    ctx->last_kernel = tr ? FKS_KERNEL_TRACED
+                          : (shaped ? FKS_KERNEL_SHAPED
+                                    : (small ? FKS_KERNEL_SMALL_BATCH : (ctx->individual_jacobians ? FKS_KERNEL_INDIVIDUAL : FKS_KERNEL_THROUGHPUT)));
     if (shaped) {
         const fksd::SimArgs* argp = ctx->d_args;
         void* params[] = {&argp};
@@ -1705,6 +1718,21 @@ fks_status fks_get_launch_geometry(const fks_context* ctx, uint32_t* resident_wa
     if (!ctx->has_robot) return FKS_ERR_NO_ROBOT;
     *resident_waves = ctx->grid_waves;
     *lds_bytes_per_group = (uint64_t)ctx->lds_bytes;
+    return FKS_OK;
+}
+
+fks_status fks_get_launch_info(const fks_context* ctx, fks_launch_info* out) {
+    if (!ctx || !out) return FKS_ERR_INVALID_ARGUMENT;
+    if (!ctx->has_robot) return FKS_ERR_NO_ROBOT;
+    std::memset(out, 0, sizeof(*out));
+    out->resident_waves = ctx->grid_waves;
+    out->waves_per_group = ctx->waves_per_group;
+    out->lds_bytes_per_group = (uint64_t)ctx->lds_bytes;
+    out->small_batch_resident_waves = ctx->small_grid_waves;
+    out->standard_layout_resident_waves = ctx->standard_resident_waves;
+    out->fk_pair = ctx->fk_pair ? 1 : 0;
+    out->lean = ctx->lean ? 1 : 0;
+    out->last_kernel = ctx->last_kernel;
     return FKS_OK;
 }
 

@@ -282,7 +282,7 @@ extern "C" fks_status fks_env_occupancy(const fks_env_handle* env, uint8_t* out,
 
 extern "C" void fks_env_free(fks_env_handle* env) { delete env; }
 
-/* DiscretizeObstacle (SEB.cpp:21-46): the world positions of the obstacle's half-resolution
+/* DiscretizeObstacle (SEB.cpp:21-46): the positions, relative to the obstacle, of its half-resolution
  * sample lattice, x then y then z (the order BuildEnvironment's SetValue calls take) */
 extern "C" fks_status fks_env_discretize_obstacle(const fks_obstacle* obstacle, double resolution, double* out_xyz,
                                                   uint64_t capacity, uint64_t* count) {
@@ -297,7 +297,7 @@ extern "C" fks_status fks_env_discretize_obstacle(const fks_obstacle* obstacle, 
     for (int32_t xi = 0; xi < nc[0]; ++xi)
         for (int32_t yi = 0; yi < nc[1]; ++yi)
             for (int32_t zi = 0; zi < nc[2]; ++zi, ++k)
-                fks_env::obstacle_sample_world(*obstacle, resolution, resolution * 0.5, xi, yi, zi, out_xyz + 3 * k);
+                fks_env::obstacle_sample_local(*obstacle, resolution, resolution * 0.5, xi, yi, zi, out_xyz + 3 * k);
     return FKS_OK;
 }
 

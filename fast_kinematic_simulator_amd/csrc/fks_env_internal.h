@@ -102,12 +102,18 @@ FKS_HD inline void obstacle_samples(const fks_obstacle& ob, double resolution, i
 }
 /* world position of sample (xi, yi, zi); `inset` = resolution * 0.5 for the occupancy
  * lattice (SEB.cpp:33-35), effective_resolution for the surface lattice (SEB.cpp:295-297) */
+FKS_HD inline void obstacle_sample_local(const fks_obstacle& ob, double resolution, double inset, int32_t xi, int32_t yi,
+                                         int32_t zi, double local[3]) {
+    const double effective_resolution = resolution * 0.5;
+    local[0] = -(ob.extents[0] - inset) + (effective_resolution * xi);
+    local[1] = -(ob.extents[1] - inset) + (effective_resolution * yi);
+    local[2] = -(ob.extents[2] - inset) + (effective_resolution * zi);
+}
 FKS_HD inline void obstacle_sample_world(const fks_obstacle& ob, double resolution, double inset, int32_t xi, int32_t yi,
                                          int32_t zi, double w[3]) {
-    const double effective_resolution = resolution * 0.5;
-    const double local[3] = {-(ob.extents[0] - inset) + (effective_resolution * xi), -(ob.extents[1] - inset) + (effective_resolution * yi),
-                             -(ob.extents[2] - inset) + (effective_resolution * zi)};
-    xform3(ob.pose, local, w);
+    double local[3];
+    obstacle_sample_local(ob, resolution, inset, xi, yi, zi, local);
+    xform3(ob.pose, local, w); /* obstacle.pose * relative_location (SEB.cpp:84-85) */
 }
 
 /* StoredSurfaceNormal entry of a boundary sample along axis a (SEB.cpp:300-460):

@@ -31,6 +31,7 @@
 #endif
 
 #include "fks_capi.h"
+#include "fks_control.h"
 #include "fks_device.h"
 #include "fks_portable_math.h"
 #include "fks_se3.h"
@@ -751,10 +752,8 @@ __device__ __forceinline__ double actuator_noisy(Sim& s, const fks_dof_controlle
         s.err |= FKS_PARTICLE_ERR_NO_NOISE_BIN;
         return real + 0.0;
     }
-    const double vmax = dabs(ct.velocity_limit);
-    const double prop = dabs(ct.max_actuator_proportional_noise) * dabs(real);
-    const double floor_noise = dabs(ct.max_actuator_minimum_noise) * vmax;
-    const double bound = dmax(prop, floor_noise);
+    const double bound = fks_control::actuator_noise_bound(real, dabs(ct.max_actuator_proportional_noise),
+                                                           dabs(ct.max_actuator_minimum_noise), dabs(ct.velocity_limit));
     return real + ns * bound;
 }
 
@@ -855,17 +854,11 @@ __device__ FKS_SHAPE_INLINE double control_action(Sim& s, const double* cfg, con
     double u = 0.0;
     if (ln < RDIM(R, D)) {
         const fks_dof_controller& ct = s.ctrl[ln];
-        /* SimplePIDController::ComputeFeedbackTerm (PID:122-135), gains made positive (PID:104-113) */
-        const double kp = dabs(ct.kp), ki = dabs(ct.ki), kd = dabs(ct.kd), iclamp = dabs(ct.integral_clamp);
-        const double timestep = A.dt;
-        const double timestep_error_integral = ((err * 0.5) + (s.pid_last * 0.5)) * timestep;
-        const double new_error_integral = s.pid_integral + timestep_error_integral;
-        s.pid_integral = dmax(-iclamp, dmin(iclamp, new_error_integral));
-        const double error_derivative = (err - s.pid_last) / timestep;
-        s.pid_last = err;
-        const double term = (err * kp) + (s.pid_integral * ki) + (error_derivative * kd);
-        const double vmax = dabs(ct.velocity_limit);
-        u = clamp(term, -vmax, vmax);
+        /* SimplePIDController::ComputeFeedbackTerm (PID:122-135), gains made positive (PID:104-113),
+         * then the actuator's clamp (UNC:70-75) */
+        const double term = fks_control::pid_feedback_term(dabs(ct.kp), dabs(ct.ki), dabs(ct.kd), dabs(ct.integral_clamp),
+                                                           &s.pid_integral, &s.pid_last, err, A.dt);
+        u = fks_control::actuator_clamp(term, dabs(ct.velocity_limit));
     }
     return u;
 }

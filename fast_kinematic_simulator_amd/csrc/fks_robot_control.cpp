@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "fks_capi.h"
+#include "fks_control.h"
 #include "fks_portable_math.h"
 #include "fks_se3.h"
 
@@ -99,16 +100,9 @@ extern "C" fks_status fks_robot_control_action(const fks_robot_desc* robot, cons
         const fks_dof_controller& ct = robot->controllers[k];
         double& integral = pid_state[k];
         double& last = pid_state[D + k];
-        const double e = err[(size_t)k];
-        const double kp = dabs(ct.kp), ki = dabs(ct.ki), kd = dabs(ct.kd), iclamp = dabs(ct.integral_clamp);
-        const double timestep_error_integral = ((e * 0.5) + (last * 0.5)) * controller_interval;
-        const double new_error_integral = integral + timestep_error_integral;
-        integral = dmax(-iclamp, dmin(iclamp, new_error_integral));
-        const double error_derivative = (e - last) / controller_interval;
-        last = e;
-        const double term = (e * kp) + (integral * ki) + (error_derivative * kd);
-        const double vmax = dabs(ct.velocity_limit);
-        out_control[k] = clamp(term, -vmax, vmax);
+        const double term = fks_control::pid_feedback_term(dabs(ct.kp), dabs(ct.ki), dabs(ct.kd), dabs(ct.integral_clamp), &integral,
+                                                           &last, err[(size_t)k], controller_interval);
+        out_control[k] = fks_control::actuator_clamp(term, dabs(ct.velocity_limit));
     }
     return FKS_OK;
 }
@@ -125,13 +119,12 @@ extern "C" fks_status fks_robot_apply_control_input(const fks_robot_desc* robot,
     for (int k = 0; k < D; ++k) {
         const fks_dof_controller& ct = robot->controllers[k];
         const double vmax = dabs(ct.velocity_limit);
-        double r = clamp(input[k], -vmax, vmax); /* GetControlValue(u) (UNC:70-75) */
+        double r = fks_control::actuator_clamp(input[k], vmax); /* GetControlValue(u) (UNC:70-75) */
         if (unit_noise) {
             /* GetControlValue(u, rng) (UNC:77-90): the caller drew the truncated-normal sample */
             if (sampled(robot, k)) return FKS_ERR_UNSUPPORTED;
-            const double prop = dabs(ct.max_actuator_proportional_noise) * dabs(r);
-            const double floor_noise = dabs(ct.max_actuator_minimum_noise) * vmax;
-            r = r + unit_noise[k] * dmax(prop, floor_noise);
+            r = r + unit_noise[k] * fks_control::actuator_noise_bound(r, dabs(ct.max_actuator_proportional_noise),
+                                                                     dabs(ct.max_actuator_minimum_noise), vmax);
         }
         real[(size_t)k] = r;
     }

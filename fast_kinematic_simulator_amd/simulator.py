@@ -169,6 +169,12 @@ class HipParticleContactSimulator:
         log when the current robot's kernel cannot be built."""
         _capi.check(self._lib.fks_set_specialization(self._ctx, 1 if enabled else 0), self._ctx, "specialization")
 
+    def launch_info(self) -> dict:
+        """fks_get_launch_info: the layout fks_set_robot chose and the kernel of the last call."""
+        info = _capi.LaunchInfo()
+        _capi.check(self._lib.fks_get_launch_info(self._ctx, ctypes.byref(info)), self._ctx, "launch info")
+        return info.as_dict()
+
     def specialization(self) -> dict:
         """fks_get_specialization: enabled, active, from_cache, compile_seconds, launches, shape"""
         info = _capi.SpecializationInfo()

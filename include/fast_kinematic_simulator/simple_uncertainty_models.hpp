@@ -1,0 +1,7 @@
+/* <fast_kinematic_simulator/simple_uncertainty_models.hpp> — the include path planner and execution code use for the
+ * reference's header of this name, forwarded to this package's header so the #include lines
+ * stay as they are ("Swapping it in under the planner"). */
+#ifndef FKS_FORWARD_SIMPLE_UNCERTAINTY_MODELS_HPP
+#define FKS_FORWARD_SIMPLE_UNCERTAINTY_MODELS_HPP
+#include "fast_kinematic_simulator_amd/simple_uncertainty_models.hpp"
+#endif

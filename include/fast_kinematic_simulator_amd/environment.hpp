@@ -490,8 +490,9 @@ inline float sdf_at(const sdf_tools::SignedDistanceField& sdf, const double p[3]
 }
 }  // namespace detail
 
-/* DiscretizeObstacle (SEB.cpp:21-46): the obstacle's half-resolution sample positions (world
- * frame), each with TAGGED_OBJECT_COLLISION_CELL(1.0, object_id) */
+/* DiscretizeObstacle (SEB.cpp:21-46): the obstacle's half-resolution sample positions relative
+ * to the obstacle (BuildEnvironment places them with obstacle.pose, SEB.cpp:84-85), each with
+ * TAGGED_OBJECT_COLLISION_CELL(1.0, object_id) */
 inline std::vector<std::pair<fks_planner_types::Vector3d, sdf_tools::TAGGED_OBJECT_COLLISION_CELL>> DiscretizeObstacle(
     const OBSTACLE_CONFIG& obstacle, const double resolution) {
     const fks_obstacle ob = detail::to_fks({obstacle})[0];

@@ -126,6 +126,15 @@ class RobotDescription {
         allowed_pairs.push_back(geometry_a);
         allowed_pairs.push_back(geometry_b);
     }
+    /* dof `dof` draws its actuation noise from `bins` (SampledUncertainVelocityActuator,
+     * UNC:224-281; simple_uncertainty_models::SetSampledActuator builds them from a LoadModel
+     * result); `owner` keeps the arrays the bins point to alive with this description */
+    void SetSampledActuator(int32_t dof, const fks_sampled_actuator& bins, std::shared_ptr<const void> owner) {
+        if (dof < 0 || dof >= NumDofs()) throw std::invalid_argument("SetSampledActuator: dof out of range");
+        if (sampled_actuators.size() != (size_t)NumDofs()) sampled_actuators.assign((size_t)NumDofs(), fks_sampled_actuator{});
+        sampled_actuators[(size_t)dof] = bins;
+        sampled_owners_.push_back(std::move(owner));
+    }
     int32_t NumDofs() const { return type == FKS_ROBOT_SE2 ? 3 : (type == FKS_ROBOT_SE3 ? 6 : num_dofs); }
     int32_t ConfigurationWidth() const {
         return type == FKS_ROBOT_SE2 ? 3 : (type == FKS_ROBOT_SE3 ? 12 : num_dofs);
@@ -169,6 +178,10 @@ class RobotDescription {
         }
         return out;
     }
+  private:
+    std::vector<std::shared_ptr<const void>> sampled_owners_;
+
+  public:
     fks_robot_desc View() const {
         fks_robot_desc d{};
         d.robot_type = type;

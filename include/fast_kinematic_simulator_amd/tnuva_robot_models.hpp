@@ -35,6 +35,7 @@
 
 #include "fast_kinematic_simulator_amd/fks_external_types.hpp"
 #include "fast_kinematic_simulator_amd/hip_particle_contact_simulator.hpp"
+#include "fast_kinematic_simulator_amd/truncated_normal.hpp"
 
 namespace tnuva_robot_models {
 
@@ -115,7 +116,7 @@ class HipRobotState {
         desc_ = desc;
         pid_.assign(2 * (size_t)desc->NumDofs(), 0.0);
         /* TruncatedNormalUncertainVelocityActuator(..., 0.5): TN(0, 0.5) on [-1, 1] (TNUVA:130, 322, 469) */
-        noise_.assign((size_t)desc->NumDofs(), std::normal_distribution<double>(0.0, 1.0));
+        noise_.assign((size_t)desc->NumDofs(), fks::TruncatedNormalDistribution(0.0, 0.5, -1.0, 1.0));
     }
     static void Check(fks_status st, const char* what) {
         if (st != FKS_OK) throw std::runtime_error(std::string(what) + ": " + fks_status_string(st));
@@ -140,25 +141,19 @@ class HipRobotState {
               "ApplyControlInput");
         return out;
     }
-    /* TruncatedNormalDistribution(0, 0.5, -1, 1) of each actuator, in dof order: the naive
-     * accept-reject of its standardised bounds [-2, 2] over the actuator's own normal draws */
+    /* one draw of each actuator's TruncatedNormalDistribution(0, 0.5, -1, 1) (UNC:61, 86), in dof
+     * order: fks::TruncatedNormalDistribution (truncated_normal.hpp; arc_helpers' sampler
+     * restated, parity unpinned), whose standardised bounds [-2, 2] take the naive
+     * accept-reject of each actuator's own normal draws */
     template <typename RNG>
     std::vector<double> DrawNoise(RNG& rng) {
         std::vector<double> n(noise_.size());
-        for (size_t k = 0; k < noise_.size(); ++k) {
-            for (;;) {
-                const double draw = noise_[k](rng);
-                if ((draw <= 2.0) && (draw >= -2.0)) {
-                    n[k] = 0.0 + 0.5 * draw;
-                    break;
-                }
-            }
-        }
+        for (size_t k = 0; k < noise_.size(); ++k) n[k] = noise_[k](rng);
         return n;
     }
     std::shared_ptr<const fks::RobotDescription> desc_;
     std::vector<double> pid_;
-    std::vector<std::normal_distribution<double>> noise_;
+    std::vector<fks::TruncatedNormalDistribution> noise_;
 };
 
 /* ---------------------------------------------------------------- SE(2) (TNUVA:26-199) */

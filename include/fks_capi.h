@@ -433,6 +433,28 @@ fks_status fks_get_phase_cycles(const fks_context* ctx, int which, uint64_t* out
  * per wave at a time) and LDS bytes per workgroup.  Diagnostic (no reference
  * counterpart); with FKS_PHASE_WAVE_RESIDENCY it gives the busy share of the grid. */
 fks_status fks_get_launch_geometry(const fks_context* ctx, uint32_t* resident_waves, uint64_t* lds_bytes_per_group);
+/* which simulation kernel a call ran (fks_launch_info.last_kernel) */
+typedef enum {
+    FKS_KERNEL_NONE = 0,
+    FKS_KERNEL_THROUGHPUT = 1,   /* fks_simulate_<family>[_lean] */
+    FKS_KERNEL_SMALL_BATCH = 2,  /* fks_simulate_<family>_small (fks_set_small_batch_kernel) */
+    FKS_KERNEL_SHAPED = 3,       /* the robot-shape-specialised kernel (fks_set_specialization) */
+    FKS_KERNEL_TRACED = 4,       /* fks_simulate_<family>[_lean]_traced */
+    FKS_KERNEL_INDIVIDUAL = 5    /* fks_simulate_<family>[_lean]_indiv (fks_set_individual_jacobians) */
+} fks_kernel_kind;
+/* The launch layout fks_set_robot chose (ABI 8; diagnostic, no reference counterpart). */
+typedef struct fks_launch_info {
+    uint32_t resident_waves;                 /* the persistent grid (fks_get_launch_geometry) */
+    uint32_t waves_per_group;
+    uint64_t lds_bytes_per_group;
+    uint32_t small_batch_resident_waves;     /* the small-batch kernel's grid (0: not for this layout) */
+    uint32_t standard_layout_resident_waves; /* what the non-lean LDS layout would hold */
+    int32_t fk_pair;                         /* paired FK of free microsteps */
+    int32_t lean;                            /* lean LDS block (skip-proof cache in scratch) */
+    int32_t last_kernel;                     /* fks_kernel_kind of the last simulation call */
+    int32_t reserved;
+} fks_launch_info;
+fks_status fks_get_launch_info(const fks_context* ctx, fks_launch_info* out);
 /* Scheduling granularity of fks_forward_simulate*: when a batch holds more particles
  * than the grid has resident waves, each particle's controller steps are run in
  * segments of `controller_steps` (0 = automatic: 14 when the batch outnumbers the
@@ -560,7 +582,9 @@ fks_status fks_create_from_device_env(const fks_device_env* env, const fks_solve
                                       double simulation_controller_frequency, uint64_t prng_seed,
                                       int32_t debug_level, fks_context** out_ctx);
 /* DiscretizeObstacle (SEB.cpp:21-46): *count = the obstacle's half-resolution samples; with
- * out_xyz (capacity >= *count triples) their world positions, x then y then z */
+ * out_xyz (capacity >= *count triples) their positions relative to the obstacle (its frame: the
+ * caller places them with obstacle.pose, as BuildEnvironment does, SEB.cpp:84-85), x then y
+ * then z */
 fks_status fks_env_discretize_obstacle(const fks_obstacle* obstacle, double resolution, double* out_xyz, uint64_t capacity,
                                        uint64_t* count);
 /* BuildSurfaceNormalsGrid (SEB.cpp:258-468) on the caller's SDF (VoxelGrid order over

@@ -26,6 +26,9 @@
 #include <vector>
 
 #include "fast_kinematic_simulator_amd/fast_kinematic_simulator.hpp"
+/* the reference's two remaining public headers, by the include paths planner code uses */
+#include <fast_kinematic_simulator/simple_pid_controller.hpp>
+#include <fast_kinematic_simulator/simple_uncertainty_models.hpp>
 
 namespace upc = uncertainty_planning_core;
 using fks_planner_types::Isometry3d;
@@ -310,6 +313,85 @@ static void custom_normals(const Scene& s, const std::shared_ptr<Robot>& robot, 
     }
 }
 
+/* `--pid-replay`: SimplePIDController (PID:55-136) over error sequences from stdin, lines
+ * "kp ki kd iclamp n" then n lines "error timestep zero" (zero = 1: Zero() before the step);
+ * prints one hex-float ComputeFeedbackTerm output per step */
+static int pid_replay() {
+    double kp, ki, kd, iclamp;
+    long n = 0;
+    while (std::scanf("%la %la %la %la %ld", &kp, &ki, &kd, &iclamp, &n) == 5) {
+        simple_pid_controller::SimplePIDController pid(simple_pid_controller::PIDParams(kp, ki, kd, iclamp));
+        if (!pid.IsInitialized()) return 1;
+        for (long i = 0; i < n; ++i) {
+            double e, dt;
+            int zero = 0;
+            if (std::scanf("%la %la %d", &e, &dt, &zero) != 3) return 1;
+            if (zero) pid.Zero();
+            std::printf("%a\n", pid.ComputeFeedbackTerm(e, dt));
+        }
+    }
+    return 0;
+}
+
+/* `--sampled <csv>` (linked scenes): every dof's actuator a SampledUncertainVelocityActuator
+ * whose model LoadModel (UNC:156-222) builds from the CSV (8 bins, 32 samples, seed = scene
+ * seed + dof); the models go into the robot's description (SetSampledActuator) and the plain
+ * C++ simulator runs the batch on the GPU.  Prints the bins (for the oracle) and the results. */
+template <typename Robot, typename Configs>
+static int sampled_actuators(const Scene& s, const Robot& robot, const Configs& starts, const Configs& targets, const char* csv) {
+    namespace sum = simple_uncertainty_models;
+    fks::RobotDescription desc = robot.HipDescription();
+    for (int32_t k = 0; k < desc.NumDofs(); ++k) {
+        const double vmax = std::abs(desc.controllers[(size_t)k].velocity_limit);
+        const std::shared_ptr<sum::JointUncertaintySampleModel> model = sum::LoadModel(csv, vmax, 8, 32, s.seed + (uint64_t)k);
+        /* the host actuator over the same model: clamp, then the picked sample */
+        const sum::SampledUncertainVelocityActuator act(model, vmax);
+        std::mt19937_64 rng(5);
+        const double probe = act.GetControlValue(0.25 * vmax, rng), clamp = act.GetControlValue(3.0 * vmax);
+        std::printf("host_sampled %d %a %a %d\n", k, probe, clamp, act.IsInitialized() ? 1 : 0);
+        sum::SetSampledActuator(desc, k, *model);
+        std::printf("bins %d", k);
+        for (const auto& bin : *model) {
+            hex(bin.first.first);
+            hex(bin.first.second);
+        }
+        std::printf("\nsamples %d", k);
+        for (const auto& bin : *model)
+            for (double v : bin.second) hex(v);
+        std::printf("\n");
+    }
+    std::vector<float> sdf_storage;
+    const auto& E = *s.env;
+    const fks_environment env =
+        simulator_environment_builder::ToFksEnvironment(E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), sdf_storage);
+    fks::HipParticleContactSimulator sim(env, s.solver.ToFks(), s.frequency, s.seed, 0, test_devices());
+    std::vector<std::vector<double>> st, tg;
+    for (const auto& c : starts) st.push_back(robot.ToFlat(c));
+    for (const auto& c : targets) tg.push_back(robot.ToFlat(c));
+    const auto res = sim.ForwardSimulateRobots(desc, st, tg, s.allow);
+    for (size_t i = 0; i < res.size(); ++i) {
+        std::printf("sampled %zu", i);
+        for (double v : res[i].result_config) hex(v);
+        std::printf(" %d %u\n", res[i].did_contact ? 1 : 0, res[i].error_flags);
+    }
+    /* the truncated-normal models of the same header: sensor and velocity actuator */
+    const sum::TruncatedNormalUncertainSensor sensor(-0.1, 0.1);
+    const sum::TruncatedNormalUncertainVelocityActuator tn(1.0, 2.0, 0.5, 0.1, 0.5);
+    std::mt19937_64 rng(11);
+    double smin = 1e300, smax = -1e300, amin = 1e300, amax = -1e300;
+    for (int i = 0; i < 4000; ++i) {
+        const double v = sensor.GetSensorValue(1.0, rng) - 1.0;
+        smin = std::min(smin, v);
+        smax = std::max(smax, v);
+        const double a = tn.GetControlValue(0.4, rng) - 0.4;
+        amin = std::min(amin, a);
+        amax = std::max(amax, a);
+    }
+    std::printf("tn_models %a %a %a %a %a %a %a\n", smin, smax, amin, amax, tn.GetControlValue(5.0), tn.GetMaxVelocityNoise(),
+                tn.GetMaxVelocityNoise(-0.5));
+    return 0;
+}
+
 /* the interface calls every family goes through; `to_flat` prints a configuration */
 template <typename Config, typename Alloc, typename Robot>
 static int exercise(const Scene& s, const std::shared_ptr<simple_simulator_interface::SimulatorInterface<Config, upc::PRNG, Alloc>>& sim,
@@ -384,7 +466,9 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "usage: %s <scene> [--dump]\n", argv[0]);
         return 2;
     }
+    if (std::string(argv[1]) == "--pid-replay") return pid_replay();
     g_dump = argc > 2 && std::string(argv[2]) == "--dump";
+    const char* sampled_csv = (argc > 3 && std::string(argv[2]) == "--sampled") ? argv[3] : nullptr;
     const bool hand_only = argc > 2 && std::string(argv[2]) == "--hand"; /* TnuvaRobot stepping only: no GPU */
     const char* normals_out = (argc > 3 && std::string(argv[2]) == "--normals-out") ? argv[3] : nullptr;
     try {
@@ -453,6 +537,7 @@ int main(int argc, char** argv) {
                 step_by_hand(s, *robot, starts[0], targets[0]);
                 return 0;
             }
+            if (sampled_csv) return sampled_actuators(s, *robot, starts, targets, sampled_csv);
             upc::LinkedSimulatorPtr sim = fast_kinematic_simulator::MakeLinkedSimulator(
                 E.GetEnvironment(), E.GetEnvironmentSDF(), E.GetSurfaceNormalsGrid(), s.solver, s.frequency, s.seed, 0, test_devices());
             const int rc = exercise<upc::LinkedConfig, upc::LinkedConfigAlloc>(s, sim, robot, starts, targets);

@@ -36,9 +36,11 @@ def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, f
     g = sim.forward_simulate_arrays(wl.robot, starts, targets, allow)
     g["statistics"] = sim.get_statistics()
     g["counters"] = sim.last_call_counters()
+    g["launch"] = sim.launch_info()
     if specialize:
         info = sim.specialization()
         assert info["active"] and info["launches"] == before + 1, info
+        assert g["launch"]["last_kernel"] == "shaped", g["launch"]
         g["specialization"] = info
     if own:
         sim.close()

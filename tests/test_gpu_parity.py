@@ -31,7 +31,10 @@ def test_forward_parity(fks_lib, oracle_lib, name, scale, small_batch_kernel):
     (fks_set_small_batch_kernel); both kernels must match the oracle."""
     wl = W.WORKLOADS[name](scale)
     g, o = run_both(wl, small_batch_kernel=small_batch_kernel)
-    print(name, mismatch_report(g, o))
+    print(name, mismatch_report(g, o), g["launch"])
+    # the kernel the call ran is the one the parameter asks for (a failed occupancy query would
+    # leave the small-batch grid empty and run the throughput kernel both times)
+    assert g["launch"]["last_kernel"] == ("small_batch" if small_batch_kernel else "throughput"), g["launch"]
     assert_identical(g, o)
     assert_counters_identical(g, o)
 
@@ -143,14 +146,32 @@ def test_lean_block_cfg5(fks_lib, oracle_lib):
     wl = W.cfg5(48 / 1048576)
     sim = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
     sim.set_robot(wl.robot)
-    geo = sim.launch_geometry()
-    import torch
-
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    assert geo["resident_waves"] == 16 * cus, geo
+    info = sim.launch_info()
+    # the lean block is chosen because it holds more resident waves than the standard layout
+    # (the occupancy query of both, not a constant: cfg5 measured 16 against 12 per CU)
+    assert info["lean"] == 1 and info["waves_per_group"] == 8, info
+    assert info["resident_waves"] > info["standard_layout_resident_waves"] > 0, info
     for seg in (None, 7):
         sim.reset_statistics()  # GetStatistics accumulates over calls (SPCS:488-512)
         g, o = run_both(wl, sim=sim, segment_steps=seg)
         assert_identical(g, o)
         assert_counters_identical(g, o)
     sim.close()
+
+
+@pytest.mark.gpu
+def test_empty_surface_normal_grid(fks_lib, oracle_lib):
+    """An initialized SurfaceNormalGrid with no stored entries (every cell empty; a planner's
+    freshly constructed grid, SPCS:138-186) still answers in-bounds lookups with the zero
+    normal (SPCS:219-222): the corrections of contacts get no normal-based term, and no
+    particle is flagged FKS_PARTICLE_ERR_NORMAL_OOB.  The same as the oracle, bit for bit."""
+    from fast_kinematic_simulator_amd.environment import SimulatorEnvironment
+
+    wl = W.cfg3(24 / 65536)
+    env = wl.environment()
+    empty = SimulatorEnvironment(env.geometry, env.sdf, np.zeros_like(env.normal_offsets), np.zeros(0), env.oob_value)
+    wl._env = empty
+    g, o = run_both(wl)
+    assert_identical(g, o)
+    assert_counters_identical(g, o)
+    assert g["counters"]["resolver_iterations"] > 0  # contacts were resolved against empty cells
