@@ -29,14 +29,18 @@ def hipcc() -> str:
     return shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 
-def write_embedded_sources(directory: str = GENERATED) -> str:
+def write_embedded_sources(directory: str = GENERATED, defines=()) -> str:
     """fks_spec_sources.inc: the EMBEDDED files as byte arrays (cmake/fks_embed_sources.cmake
-    writes the same file for the CMake build)."""
+    writes the same file for the CMake build).  A variant build's defines (build_variant) are
+    prepended to the kernel source, so its shape-specialised kernels are built the same way."""
     os.makedirs(directory, exist_ok=True)
     lines = ["/* generated from the library's sources by fast_kinematic_simulator_amd/build.py: do not edit */"]
     entries = []
     for k, (name, rel) in enumerate(EMBEDDED):
         data = open(os.path.join(PKG, rel), "rb").read()
+        if name == "fks_kernels.hip" and defines:
+            prelude = "".join("#define " + d.replace("=", " ", 1) + "\n" for d in defines)
+            data = prelude.encode() + data
         body = ",".join(f"0x{b:02x}" for b in data)
         lines.append(f"static const unsigned char kFksSrc{k}[] = {{{body}}};")
         entries.append(f'{{"{name}", kFksSrc{k}, sizeof(kFksSrc{k})}}')
@@ -53,7 +57,7 @@ def write_embedded_sources(directory: str = GENERATED) -> str:
 
 
 def build_command(output: str, defines=(), flags=()) -> list:
-    write_embedded_sources()
+    write_embedded_sources(defines=defines)
     return [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
             *[f"-D{d}" for d in defines], *flags,
             f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(PKG, 'csrc')}", f"-I{GENERATED}", "-x", "hip",

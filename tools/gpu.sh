@@ -28,6 +28,8 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 O=gpurun_out
 L=fast_kinematic_simulator_amd/libfks_hip.so
+# variant libraries (build/variants) compile their shape-specialised kernels with the product's helper
+export FKS_SHAPEC=$PWD/fast_kinematic_simulator_amd/fks_shapec
 BP="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --pipeline-batches 0"
 lib() { [ "$1" = L ] && echo $L || echo "$1"; }
 

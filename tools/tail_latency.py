@@ -44,14 +44,19 @@ def main():
     ap.add_argument("--workload", default="cfg3")
     ap.add_argument("--top", type=int, default=3)
     ap.add_argument("--json", default="")
+    ap.add_argument("--specialize", choices=("on", "off"), default="on",
+                    help="the robot-shape-specialised kernel (the lone particles then skip the small-batch kernel)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     wl = W.WORKLOADS[a.workload]()
     sim = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
     sim.set_robot(wl.robot)
+    if a.specialize == "on":
+        sim.set_specialization(True)
+        sim.set_small_batch_kernel(False)
     run(sim, wl, wl.starts[:256], 0, dev)
     m, it, kms, ph = run(sim, wl, wl.starts, 0, dev)
-    out = {"workload": a.workload, "batch_kernel_ms": kms, "particles": int(m.size), "alone": [],
+    out = {"workload": a.workload, "specialization": sim.specialization(), "batch_kernel_ms": kms, "particles": int(m.size), "alone": [],
            "batch_phase_share": ({k: round(v / max(1, ph.get("particle", 0)), 4) for k, v in ph.items() if k not in COUNTS}
                                  if ph.get("control", 0) > 0 else None),
            "batch_phase_counts": {k: ph[k] for k in COUNTS if k in ph}}
