@@ -189,6 +189,12 @@ def main():
     ap.add_argument("--specialize", choices=("on", "off"), default="on",
                     help="run the robot's shape-specialised kernel (fks_set_specialization: compiled at setup, outside the "
                          "timed region; results identical) or the generic one")
+    ap.add_argument("--in-process", action="store_true",
+                    help="one process driving --gpus devices through fks_create_multi: the planner drop-in's path "
+                         "(HipParticleContactSimulator / MultiDeviceSimulator), host buffers in and out, as a planner's "
+                         "ForwardSimulateRobots call gets it; no launcher, no collective")
+    ap.add_argument("--devices", default=None, help="--in-process: comma-separated device ids (default 0..gpus-1; "
+                                                      "a device may repeat)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous / shard / gather check without a GPU (gloo): no simulation, value null")
     args = ap.parse_args()
@@ -197,6 +203,8 @@ def main():
     if args.gpus < 1:
         log("--gpus must be >= 1")
         return 2
+    if args.in_process:
+        return in_process(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no external launcher: start one rank process per GPU before anything touches a GPU
         return spawn_ranks(args.gpus)
@@ -503,6 +511,92 @@ def pipelined_batches(sim, denv, wl, dev, starts, targets, n, first_id, batches)
             "contexts": 2, "streams": 2, "identical_to_sequential": same,
             "note": "throughput of back-to-back batches whose tails overlap the next batch's start (two contexts, two "
                     "streams, fks_forward_simulate_device without synchronisation); `value` above is the one-stream figure"}
+
+
+def in_process(args) -> int:
+    """`--in-process`: the planner drop-in's multi-device path timed as a planner sees it.  One
+    process, one fks_create_multi context over the devices (Make*Simulator's default device list
+    is every visible device); each step is one fks_multi_forward_simulate call on host arrays
+    (starts H2D, the shards' kernels concurrently on their devices' streams, outcomes D2H into
+    the caller's arrays), so `value` includes the PCIe copies, unlike the launcher path's
+    device-resident `value`.  Weak scaling: 65,536 cfg3 particles per listed device, sharded
+    contiguously by global particle id; every device runs the shape-specialised kernel."""
+    import numpy as np
+    import torch
+
+    from fast_kinematic_simulator_amd import workloads as W
+    from fast_kinematic_simulator_amd.simulator import MultiDeviceSimulator
+
+    devices = [int(d) for d in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    visible = torch.cuda.device_count()
+    if not devices or max(devices) >= visible or min(devices) < 0:
+        log(f"--in-process needs devices {devices}, {visible} visible")
+        return 1
+    ndev = len(devices)
+    base, per_gpu, workload_desc = WORKLOADS[args.workload]
+    n_total = (args.particles or per_gpu) * ndev
+    wl = W.WORKLOADS[args.workload](scale=n_total / float(base))
+    t0 = time.perf_counter()
+    env_stats = {}
+    denv = W.SCENES[args.workload](device=devices[0], stats=env_stats, resident=True)
+    henv = denv.download()  # the planner hands the simulator a host environment
+    log(f"environment built on device {devices[0]} and downloaded in {time.perf_counter() - t0:.2f}s")
+    sim = MultiDeviceSimulator(henv, wl.solver, wl.controller_frequency, wl.seed, devices)
+    sim.set_robot(wl.robot)
+    starts = np.ascontiguousarray(wl.starts[:n_total])
+    for w in range(args.warmup):  # the first call builds each device's shape-specialised kernel
+        sim.set_call_index(1000 + w)
+        sim.forward_simulate_arrays(wl.robot, starts, wl.targets, not args.no_contacts)
+    micro = 0
+    kernel_ms = []
+    totals = {k: 0 for k in ("calls", "sdf_bytes", "microsteps", "controller_steps", "resolver_iterations", "least_squares_rows",
+                             "error_particles")}
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        sim.set_call_index(k)
+        r = sim.forward_simulate_arrays(wl.robot, starts, wl.targets, not args.no_contacts)
+        micro += int(np.sum(r["microsteps"], dtype=np.int64))
+        c = sim.last_call_counters()
+        kernel_ms.append(c["kernel_ms"])
+        for key in totals:
+            totals[key] += c[key] if key != "calls" else 1
+    elapsed = time.perf_counter() - t_start
+    assert micro == totals["microsteps"], (micro, totals["microsteps"])
+    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    bytes_per_device_launch = totals["sdf_bytes"] / totals["calls"] / ndev
+    achieved = bytes_per_device_launch / avg_kernel_s / 1e9
+    cpu = None
+    if not args.no_cpu_baseline:
+        sample = min(args.cpu_sample, n_total)
+        cwl = W.WORKLOADS[args.workload](scale=sample / float(base))
+        cwl._env = henv
+        cpu = cpu_baseline(cwl, sample)
+    line = {
+        "metric": METRIC, "value": micro / elapsed, "unit": UNIT, "n_gpus": len(set(devices)), "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": f"synthetic (seeded {args.workload} scene and start perturbations, workloads.py)",
+        "config": {
+            "workload": f"{workload_desc}, {n_total // ndev} particles per listed device, "
+                        + ("allow_contacts = false (A/B only)" if args.no_contacts else "allow_contacts")
+                        + f", one process over devices {devices} (fks_create_multi, host buffers: PCIe included)",
+            "mode": "in-process", "devices": devices, "particles_per_gpu": n_total // ndev, "particles_total": n_total,
+            "controller_steps": wl.steps, "parallelism": f"in-process x{ndev} (particle shards, no collective)",
+            "microsteps_per_step": micro / args.steps,
+            "mean_microsteps_per_controller_step": totals["microsteps"] / max(1, totals["controller_steps"]),
+            "resolver_iterations_per_step": totals["resolver_iterations"] / args.steps,
+            "error_particles": totals["error_particles"],
+        },
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": None, "kernel": "fks_simulate_shaped (per device)", "avg_kernel_ms": avg_kernel_s * 1e3,
+                     "note": "per device: algorithmic bytes of one shard's launch / the slowest shard's kernel time"},
+        "statistics": sim.get_statistics(),
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    sim.close()
+    denv.close()
+    return 0
 
 
 def spawn_ranks(n: int) -> int:

@@ -178,7 +178,7 @@ class SpecializationInfo(ctypes.Structure):
         ("enabled", c_int32),
         ("active", c_int32),
         ("from_cache", c_int32),
-        ("reserved", c_int32),
+        ("pending", c_int32),
         ("compile_seconds", c_double),
         ("launches", c_uint64),
         ("shape", ctypes.c_char * 64),

@@ -69,12 +69,12 @@ SHAPEC = os.path.join(PKG, "fks_shapec")
 
 def build_shapec(force: bool = False) -> str:
     """The compiler process of the shape specialisation (csrc/fks_shapec.cpp): a host program
-    over ROCm's hiprtc, next to libfks_hip.so, carrying the same embedded kernel source."""
-    inc = write_embedded_sources()
+    over ROCm's hiprtc, next to libfks_hip.so; it compiles the sources the calling library
+    writes out for it, so one helper serves the product and every variant build."""
     src = os.path.join(PKG, "csrc", "fks_shapec.cpp")
-    if not force and os.path.exists(SHAPEC) and os.path.getmtime(SHAPEC) >= max(os.path.getmtime(src), os.path.getmtime(inc)):
+    if not force and os.path.exists(SHAPEC) and os.path.getmtime(SHAPEC) >= os.path.getmtime(src):
         return SHAPEC
-    cmd = ["g++", "-std=c++17", "-O2", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", f"-I{GENERATED}", src, "-o", SHAPEC + ".tmp",
+    cmd = ["g++", "-std=c++17", "-O2", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", src, "-o", SHAPEC + ".tmp",
            "-L/opt/rocm/lib", "-lhiprtc", "-Wl,-rpath,/opt/rocm/lib"]
     proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if proc.returncode != 0:

@@ -241,6 +241,7 @@ struct fks_context {
     size_t cap_scratch = 0; /* doubles allocated at d_scratch */
     uint64_t scratch_per_wave = 0;
     uint32_t grid_waves = 0;
+    uint32_t waves_per_cu = 0;     /* resident waves per CU of the layout (LDS and registers) */
     uint32_t small_grid_waves = 0; /* resident waves of the small-batch kernel (0: none for this layout) */
     uint32_t grid_groups = 0;
     uint32_t waves_per_group = fksd::kWavesPerGroup;
@@ -284,7 +285,8 @@ struct fks_context {
     fks_call_counters last;
     fks_call_counters total;
     /* robot-shape specialisation (fks_set_specialization, fks_specialize.cpp) */
-    int32_t specialize = 0;
+    int32_t specialize = 1;
+    bool spec_pending = false; /* robot set, its kernel not built yet (built at the first launch that runs it) */
     hipModule_t spec_module = nullptr;
     hipFunction_t spec_fn = nullptr; /* fks_simulate_shaped of the current robot's shape */
     std::string spec_shape;
@@ -372,6 +374,18 @@ static fks_status spec_prepare(fks_context* ctx) {
     sh.P = ctx->R.P;
     sh.pair = ctx->fk_pair ? 1 : 0;
     sh.lean = ctx->lean ? 1 : 0;
+    /* the waves a SIMD holds at this layout (4 SIMDs per CU): when the LDS block keeps fewer
+     * resident than the register budget allows (cfg5's lean blocks: 16 per CU), the
+     * specialised kernel is compiled for that many and may use their registers */
+    const int per_simd = (int)((ctx->waves_per_cu + 3) / 4);
+    if (per_simd >= 1 && per_simd < fksd::kThroughputWavesPerEU) sh.waves_per_eu = per_simd;
+    /* FKS_SPEC_WAVES_PER_EU=n (tuning and A/B runs): compile for n waves per SIMD instead
+     * (n >= the layout's waves; 0 = the library's budget) */
+    if (const char* e = std::getenv("FKS_SPEC_WAVES_PER_EU")) {
+        const int n = std::atoi(e);
+        if (n == 0 || n == fksd::kThroughputWavesPerEU) sh.waves_per_eu = 0;
+        else if (n >= per_simd && n <= 8) sh.waves_per_eu = n;
+    }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     std::string log;
     bool compiled = false;
@@ -392,12 +406,14 @@ static fks_status spec_prepare(fks_context* ctx) {
      * different quantity for module kernels than for the library's own) */
     const int shaped_vgpr = fks_spec::metadata_uint(co->bytes, ".vgpr_count") + fks_spec::metadata_uint(co->bytes, ".agpr_count");
     hipFuncAttributes gen{};
-    if (hipFuncGetAttributes(&gen, reinterpret_cast<const void*>(kernel_for(ctx->R.type, false, ctx->lean))) != hipSuccess ||
-        shaped_vgpr <= 0 || shaped_vgpr > gen.numRegs) {
+    if (hipFuncGetAttributes(&gen, reinterpret_cast<const void*>(kernel_for(ctx->R.type, false, ctx->lean))) != hipSuccess) gen.numRegs = 0;
+    /* 512 VGPRs per SIMD lane, allocated in granules of 8 */
+    const int budget = sh.waves_per_eu > 0 ? (512 / sh.waves_per_eu) & ~7 : gen.numRegs;
+    if (shaped_vgpr <= 0 || shaped_vgpr > budget) {
         (void)hipModuleUnload(m);
         return fail(ctx, FKS_ERR_UNSUPPORTED,
-                    "shape specialisation: the specialised kernel needs " + std::to_string(shaped_vgpr) + " VGPRs, the generic " +
-                        std::to_string(gen.numRegs));
+                    "shape specialisation: the specialised kernel needs " + std::to_string(shaped_vgpr) + " VGPRs, the budget is " +
+                        std::to_string(budget));
     }
     ctx->spec_module = m;
     ctx->spec_fn = f;
@@ -468,7 +484,7 @@ static fks_status create_impl(const fks_environment* henv, const fks_device_env*
     ctx->debug_level = debug_level;
     {
         const char* sp = std::getenv("FKS_SPECIALIZE");
-        ctx->specialize = (sp && std::string(sp) == "1") ? 1 : 0;
+        ctx->specialize = (sp && std::string(sp) == "0") ? 0 : 1;
     }
     std::memset(&ctx->stats, 0, sizeof(ctx->stats));
     std::memset(&ctx->last, 0, sizeof(ctx->last));
@@ -695,6 +711,7 @@ static fks_status launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
     ctx->fk_pair = pair;
     ctx->lean = lean;
     ctx->standard_resident_waves = (uint32_t)(cus * std::max(0, standard_waves_per_cu));
+    ctx->waves_per_cu = (uint32_t)waves_per_cu;
     ctx->waves_per_group = wpg;
     ctx->lds_bytes = bytes;
     ctx->grid_groups = grid_groups;
@@ -1006,13 +1023,10 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     }
     ctx->R = R;
     ctx->has_robot = true;
-    /* with fks_set_specialization, the new robot's shape-specialised kernel (a failure keeps the
-     * generic kernels and is reported by fks_get_specialization, not by fks_set_robot) */
+    /* the new robot's shape-specialised kernel is built at the first launch that runs it
+     * (simulate_device), so robots only ever simulated in small batches cost no compile */
     spec_release(ctx);
-    if (ctx->specialize) {
-        const std::string keep = ctx->last_error;
-        if (spec_prepare(ctx) != FKS_OK) ctx->last_error = keep + (keep.empty() ? "" : "; ") + ctx->last_error;
-    }
+    ctx->spec_pending = ctx->specialize != 0;
     return FKS_OK;
 }
 
@@ -1203,7 +1217,15 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
      * simulation: that kernel (every particle has its wave from the start either way) */
     const bool small = ctx->small_batch && !tr && !ctx->individual_jacobians && !ctx->lean && a.nseg == 1 &&
                        n <= (uint64_t)ctx->small_grid_waves;
-    /* the plain throughput path runs the robot's shape-specialised kernel when there is one */
+    /* the plain throughput path runs the robot's shape-specialised kernel: built (or fetched
+     * from a cache) here at the first such launch; a failure keeps the generic kernel and is
+     * reported by fks_get_specialization / fks_get_last_error, not by this call */
+    if (ctx->spec_pending && !tr && !small && !ctx->individual_jacobians) {
+        ctx->spec_pending = false;
+        const std::string keep = ctx->last_error;
+        if (spec_prepare(ctx) != FKS_OK) ctx->last_error = keep + (keep.empty() ? "" : "; ") + ctx->last_error;
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+    }
     const bool shaped = ctx->spec_fn && !tr && !small && !ctx->individual_jacobians;
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
     ctx->last_kernel = tr ? FKS_KERNEL_TRACED
@@ -1698,7 +1720,8 @@ fks_status fks_set_specialization(fks_context* ctx, int32_t enabled) {
     fks_status st = settle(ctx);
     if (st != FKS_OK) return st;
     ctx->specialize = enabled ? 1 : 0;
-    return spec_prepare(ctx);
+    ctx->spec_pending = false;
+    return spec_prepare(ctx); /* now, for the current robot (releases it when disabled) */
 }
 
 fks_status fks_get_specialization(const fks_context* ctx, fks_specialization_info* out) {
@@ -1706,6 +1729,7 @@ fks_status fks_get_specialization(const fks_context* ctx, fks_specialization_inf
     std::memset(out, 0, sizeof(*out));
     out->enabled = ctx->specialize;
     out->active = ctx->spec_fn ? 1 : 0;
+    out->pending = ctx->spec_pending ? 1 : 0;
     out->from_cache = ctx->spec_from_cache;
     out->compile_seconds = ctx->spec_seconds;
     out->launches = ctx->spec_launches;

@@ -128,6 +128,9 @@ constexpr int kWavesPerGroup = 4;
 /* an LDS-bound robot may run a lean block (its round skip-proof cache in the wave's scratch,
  * fks_simulate_*_lean kernels) at up to 8 waves per workgroup */
 constexpr int kMaxWavesPerGroup = 8;
+/* the throughput kernels' register budget: amdgpu_waves_per_eu(FKS_WAVES_PER_EU) in
+ * fks_kernels.hip, 5 waves per SIMD = 96 VGPRs */
+constexpr int kThroughputWavesPerEU = 5;
 struct LdsLayout {
     uint32_t joints, ctrl, base, dofj, gbox, gpairs, rounds, shared_total;
     uint32_t rstate, noise, noise_err, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u,

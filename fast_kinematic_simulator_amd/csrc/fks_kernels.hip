@@ -3446,13 +3446,14 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
  * The occupancy target bounds the VGPR budget of the kernel and of its out-of-line
  * callees (the rare self-contact path would otherwise set the budget for all). */
 #ifndef FKS_WAVES_PER_EU
-#define FKS_WAVES_PER_EU 5
+#define FKS_WAVES_PER_EU 5 /* fksd::kThroughputWavesPerEU */
 #endif
 #define FKS_KERNEL_ATTRS __launch_bounds__(64 * kMaxWavesPerGroup) __attribute__((amdgpu_waves_per_eu(FKS_WAVES_PER_EU)))
 #if defined(FKS_SHAPE_L)
 /* the shape-specialised build (fks_specialize.cpp, hiprtc): one throughput kernel for one
  * robot shape, the same template and launch attributes as the generic kernel it replaces
- * (fks_simulate_<family>[_lean]) */
+ * (fks_simulate_<family>[_lean]); a robot whose LDS block keeps fewer waves resident than
+ * the register budget allows gets the registers of the absent waves (FKS_WAVES_PER_EU) */
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_shaped(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
     simulate_particles<FKS_SHAPE_TYPE, false, false, FKS_SHAPE_LEAN != 0>(args, lds_mem);

@@ -29,9 +29,12 @@ struct Shape {
     int32_t L, J, D, W, G, P;
     int32_t pair;   /* LdsLayout.fk_pair */
     int32_t lean;   /* LdsLayout.lean (the fks_simulate_linked_lean variant) */
+    int32_t waves_per_eu = 0; /* 0: the library's register budget (fksd::kThroughputWavesPerEU waves
+                               * per SIMD); fewer when the LDS block caps the resident waves lower,
+                               * so the kernel may use the registers those absent waves leave */
 };
 
-/* "t0-L8-J7-D7-W7-G8-P512-p1-l0": names the shape in logs and cache files */
+/* "t0-L8-J7-D7-W7-G8-P512-p1-l0" (+ "-w4" for a raised register budget): names the shape in logs and cache files */
 std::string shape_key(const Shape& s);
 
 struct CodeObject {

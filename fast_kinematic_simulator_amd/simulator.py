@@ -165,8 +165,9 @@ class HipParticleContactSimulator:
     def set_specialization(self, enabled: bool = True):
         """Run the plain throughput simulation of this robot (and of every robot set later) on a
         kernel compiled at run time for its shape (fks_set_specialization: hiprtc, cached per
-        process and on disk).  Results do not depend on it; raises FksError with the compiler
-        log when the current robot's kernel cannot be built."""
+        process and on disk).  On by default, built at the first call that runs it; enabling
+        it builds the current robot's kernel now.  Results do not depend on it; raises FksError
+        with the compiler log when the current robot's kernel cannot be built."""
         _capi.check(self._lib.fks_set_specialization(self._ctx, 1 if enabled else 0), self._ctx, "specialization")
 
     def launch_info(self) -> dict:
@@ -176,7 +177,7 @@ class HipParticleContactSimulator:
         return info.as_dict()
 
     def specialization(self) -> dict:
-        """fks_get_specialization: enabled, active, from_cache, compile_seconds, launches, shape"""
+        """fks_get_specialization: enabled, active, pending, from_cache, compile_seconds, launches, shape"""
         info = _capi.SpecializationInfo()
         _capi.check(self._lib.fks_get_specialization(self._ctx, ctypes.byref(info)), self._ctx, "specialization")
         return info.as_dict()

@@ -489,23 +489,25 @@ fks_status fks_set_small_batch_kernel(fks_context* ctx, int32_t enabled);
  * (SPCS:1966-1988: one ColPivHouseholderQR solve per corrected point, summed in point order). */
 fks_status fks_set_individual_jacobians(fks_context* ctx, int32_t simulate_with_individual_jacobians);
 /* Robot-shape specialisation (ABI 8; no reference counterpart, results are bit-identical
- * either way).  With `enabled`, the plain throughput simulation (fks_forward_simulate*,
- * not traced, individual-Jacobian or small-batch calls) of the current robot and of every
- * robot set later runs a kernel compiled at run time (hiprtc) from the library's own kernel
- * source with the robot's link / joint / dof / geometry counts and LDS and scratch carve-outs
- * as constants (cfg3: 11-12 % faster).  The first robot of a shape costs one
- * compile (tens of seconds, in the calling thread: fks_set_specialization, then
- * fks_set_robot); code objects are cached per process and on disk (FKS_KERNEL_CACHE=<dir>,
- * default ~/.cache/fast_kinematic_simulator_amd; "off" disables it).  Returns
- * FKS_ERR_UNSUPPORTED with the compiler log in fks_get_last_error when the current robot's
- * kernel cannot be built (its calls then keep the generic kernel); 0 = generic kernels only.
- * The default is 0, or 1 when the environment variable FKS_SPECIALIZE=1 is set at fks_create. */
+ * either way).  While enabled (the default), the plain throughput simulation
+ * (fks_forward_simulate*, not traced, individual-Jacobian or small-batch calls) runs a kernel
+ * compiled at run time (hiprtc, in the helper process fks_shapec installed beside the
+ * library) from the library's own kernel source with the robot's link / joint / dof /
+ * geometry counts and LDS and scratch carve-outs as constants (cfg3: 10-13 % faster,
+ * DESIGN.md §4.9).  A robot's kernel is built at the first call that runs it (a robot only
+ * simulated in small batches never compiles) or at once by fks_set_specialization(ctx, 1);
+ * the first robot of a shape on a machine costs one compile (2-20 s in the calling thread),
+ * later ones come from the per-process cache or the disk cache (FKS_KERNEL_CACHE=<dir>,
+ * default ~/.cache/fast_kinematic_simulator_amd; "off" disables it).  When the kernel cannot
+ * be built the calls keep the generic kernel and fks_get_last_error holds the compiler log;
+ * fks_set_specialization(ctx, 1) then returns FKS_ERR_UNSUPPORTED.  0 = generic kernels only
+ * (also the default when the environment variable FKS_SPECIALIZE=0 is set at fks_create). */
 fks_status fks_set_specialization(fks_context* ctx, int32_t enabled);
 typedef struct fks_specialization_info {
     int32_t enabled;         /* fks_set_specialization */
     int32_t active;          /* the current robot's plain simulation calls run the shape-specialised kernel */
     int32_t from_cache;      /* its code object came from the process or disk cache */
-    int32_t reserved;
+    int32_t pending;         /* enabled, robot set, kernel to be built at the first call that runs it */
     double compile_seconds;  /* hiprtc time of that code object (0 when it came from a cache) */
     uint64_t launches;       /* launches of the specialised kernel since the robot was set */
     char shape[64];          /* the shape key, e.g. "t0-L8-J7-D7-W7-G8-P512-p1-l0" */

@@ -32,6 +32,10 @@ def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, f
         sim.set_specialization(True)
         sim.set_small_batch_kernel(False)
         before = sim.specialization()["launches"]
+    elif own:
+        # the generic kernels (the library's default is the specialised one: test_specialize.py
+        # and the planner / full-size tests run that)
+        sim.set_specialization(False)
     sim.set_call_index(call_index)
     g = sim.forward_simulate_arrays(wl.robot, starts, targets, allow)
     g["statistics"] = sim.get_statistics()

@@ -138,3 +138,30 @@ def test_bench_spawns_ranks_on_gpus():
     d = _json_lines(p.stdout)[0]
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["outcome_gather"] == "rccl"
     assert d["config"]["particles_total"] == 2048
+
+
+def test_bench_in_process_refuses_missing_devices():
+    """`--in-process` lists devices for one fks_create_multi context: a device beyond the visible
+    ones fails (non-zero) before anything is timed."""
+    import torch
+
+    n = torch.cuda.device_count()
+    p = _run_bench(["--in-process", "--devices", f"0,{n}", "--particles", "64", "--no-cpu-baseline"])
+    assert p.returncode == 1 and not _json_lines(p.stdout)
+    assert "--in-process needs devices" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_in_process_line():
+    """The planner drop-in's multi-device path (one process, fks_create_multi, host buffers),
+    here over device 0 listed twice: two shards, one line, the same contract keys."""
+    p = _run_bench(["--in-process", "--devices", "0,0", "--particles", "2048", "--steps", "1", "--warmup", "1",
+                    "--no-cpu-baseline"], timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["value"] > 0 and d["n_gpus"] == 1 and d["scaling"] == "weak" and d["dtype"] == "f64"
+    c = d["config"]
+    assert c["mode"] == "in-process" and c["devices"] == [0, 0] and c["particles_total"] == 4096 and c["error_particles"] == 0
+    assert d["statistics"]["successful_resolves"] > 0 and d["roofline"]["avg_kernel_ms"] > 0

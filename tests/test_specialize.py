@@ -33,12 +33,39 @@ def test_shape_build_compiles_for_every_family():
         assert p.returncode == 0, p.stdout[-3000:]
 
 
+def test_shapec_compiles_the_sources_it_is_handed(tmp_path):
+    """fks_shapec (the compiler process the library starts) compiles the kernel sources the
+    library writes out for it, with hiprtc, into a gfx950 code object; a robot whose LDS block
+    holds 4 waves per SIMD (cfg5's lean block) gets their registers (FKS_WAVES_PER_EU=4)."""
+    from fast_kinematic_simulator_amd import build
+
+    shapec = build.build_shapec()
+    src = tmp_path / "src"
+    src.mkdir()
+    for name, rel in build.EMBEDDED:
+        (src / name).write_bytes(open(os.path.join(build.PKG, rel), "rb").read())
+    out = tmp_path / "k.hsaco"
+    shape = dict(TYPE=0, L=17, J=16, D=14, W=14, G=17, P=1088, PAIR=0, LEAN=1)
+    cmd = [shapec, str(out), str(src), "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17",
+           "-DFKS_WAVES_PER_EU=4"] + [f"-DFKS_SHAPE_{k}={v}" for k, v in shape.items()]
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout[-3000:]
+    notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", str(out)], stdout=subprocess.PIPE, text=True).stdout
+    vgprs = [int(l.split(":")[1]) for l in notes.splitlines() if l.strip().startswith(".vgpr_count:")]
+    assert vgprs and 96 < vgprs[0] <= 128, vgprs
+    assert ".name:           fks_simulate_shaped" in notes
+    bad = subprocess.run([shapec, str(out), str(tmp_path / "missing")], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    assert bad.returncode != 0 and "fks_kernels.hip" in bad.stdout
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,scale", SPEC_CASES)
 def test_specialized_kernel_parity(fks_lib, oracle_lib, name, scale):
     wl = {**W.WORKLOADS, **W.COVERAGE}[name](scale)
     g, o = run_both(wl, specialize=True)
     print(name, g["specialization"], mismatch_report(g, o))
+    if name == "cfg5":  # the lean block holds 4 waves per SIMD: the kernel gets their registers
+        assert g["specialization"]["shape"].endswith("-w4"), g["specialization"]
     assert_identical(g, o)
     assert_counters_identical(g, o)
 
@@ -54,28 +81,39 @@ def test_specialized_segmented_cfg3(fks_lib, oracle_lib):
 
 @pytest.mark.gpu
 def test_specialization_follows_the_robot_and_is_cached(fks_lib, tmp_path, monkeypatch):
-    """Setting another robot releases the old kernel and builds (or fetches) the new shape's;
-    a second context finds the code object in the process cache; switching it off returns to
-    the generic kernel; results never change."""
+    """Specialisation is on by default and lazy: setting a robot leaves its kernel pending, a
+    small batch (small-batch kernel) does not build it, the first throughput call does.
+    Setting another robot releases the old kernel; a second context finds the code object in
+    the process cache; switching it off returns to the generic kernel; results never change."""
     from fast_kinematic_simulator_amd import make_linked_simulator
 
     a, b = W.cfg3(32 / 65536), W.folding_arm(1.0)
     sim = make_linked_simulator(a.environment(), a.solver, a.controller_frequency, a.seed)
-    sim.set_small_batch_kernel(False)
     sim.set_robot(a.robot)
-    sim.set_specialization(True)
+    i0 = sim.specialization()
+    assert i0["enabled"] and i0["pending"] and not i0["active"], i0
+    sim.forward_simulate_arrays(a.robot, a.starts, a.targets, True)  # 32 particles: the small-batch kernel
+    assert sim.launch_info()["last_kernel"] == "small_batch" and sim.specialization()["pending"]
+    sim.set_small_batch_kernel(False)
+    sim.set_call_index(0)
+    ra = sim.forward_simulate_arrays(a.robot, a.starts, a.targets, True)  # builds the kernel, then runs it
     ia = sim.specialization()
-    assert ia["enabled"] and ia["active"] and ia["shape"].startswith("t0-L8-J7-D7")
-    ra = sim.forward_simulate_arrays(a.robot, a.starts, a.targets, True)
+    assert ia["active"] and not ia["pending"] and ia["launches"] == 1 and ia["shape"].startswith("t0-L8-J7-D7"), ia
+    assert sim.launch_info()["last_kernel"] == "shaped"
     sim.set_robot(b.robot)
     ib = sim.specialization()
-    assert ib["active"] and ib["shape"] != ia["shape"] and ib["launches"] == 0
+    assert ib["pending"] and not ib["active"] and ib["launches"] == 0
+    sim.forward_simulate_arrays(b.robot, b.starts, b.targets, True)
+    ib = sim.specialization()
+    assert ib["active"] and ib["shape"] != ia["shape"] and ib["launches"] == 1
     sim.set_robot(a.robot)
-    assert sim.specialization()["from_cache"]
+    sim.set_specialization(True)  # builds now (from the process cache)
+    assert sim.specialization()["active"] and sim.specialization()["from_cache"]
     sim.set_specialization(False)
-    assert not sim.specialization()["active"]
+    assert not sim.specialization()["active"] and not sim.specialization()["pending"]
     sim.set_call_index(0)
     rg = sim.forward_simulate_arrays(a.robot, a.starts, a.targets, True)
+    assert sim.launch_info()["last_kernel"] == "throughput"
     for k in ("positions", "collided", "microsteps", "resolver_iterations", "error_flags"):
         assert np.array_equal(ra[k], rg[k]), k
     sim.close()

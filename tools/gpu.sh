@@ -30,6 +30,10 @@ O=gpurun_out
 L=fast_kinematic_simulator_amd/libfks_hip.so
 # variant libraries (build/variants) compile their shape-specialised kernels with the product's helper
 export FKS_SHAPEC=$PWD/fast_kinematic_simulator_amd/fks_shapec
+# profiled runs find their shape-specialised kernels compiled by an unprofiled run beforehand
+# (warm), so no compiler process starts under rocprofv3
+export FKS_KERNEL_CACHE=/tmp/fks_kernel_cache_$TAG
+warm() { timeout -k 10 300 "$@" > /dev/null 2>&1; }
 BP="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --pipeline-batches 0"
 lib() { [ "$1" = L ] && echo $L || echo "$1"; }
 
@@ -41,19 +45,22 @@ run_task() {
   bench) timeout -k 10 400 python bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err ;;
   bench:*) w=${1#bench:}; timeout -k 10 300 python bench.py --workload $w --no-config-check > $O/${TAG}_bench_$w.json 2> $O/${TAG}_bench_$w.err ;;
   others) for w in cfg1 cfg2 cfg4 cfg5; do run_task bench:$w || return $?; done ;;
-  trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_trace -o bench -- $BP > $O/${TAG}_bench_under_rocprof.json 2> $O/${TAG}_trace.err ;;
+  trace) warm $BP && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_trace -o bench -- $BP > $O/${TAG}_bench_under_rocprof.json 2> $O/${TAG}_trace.err ;;
   pmc)
+    warm $BP &&
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_fetch -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_fetch.err &&
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_write -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_write.err &&
     timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/${TAG}_pmc_tcc -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_tcc.err ;;
   pmc:*)
     w=${1#pmc:}; BW="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0 --workload $w"
+    warm $BW &&
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_${w}_fetch -o bench -- $BW > /dev/null 2> $O/${TAG}_pmc_${w}_fetch.err &&
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_${w}_write -o bench -- $BW > /dev/null 2> $O/${TAG}_pmc_${w}_write.err &&
     timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/${TAG}_pmc_${w}_tcc -o bench -- $BW > /dev/null 2> $O/${TAG}_pmc_${w}_tcc.err ;;
   valu)
     B1="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0"
     mkdir -p $O/${TAG}_valu
+    warm $B1 &&
     timeout -s KILL 180 rocprofv3 --pmc VALUBusy --kernel-trace --output-format csv -d $O/${TAG}_valu/valubusy -o bench -- $B1 > /dev/null 2> $O/${TAG}_valu/valubusy.err &&
     timeout -s KILL 180 rocprofv3 --pmc VALUUtilization --kernel-trace --output-format csv -d $O/${TAG}_valu/valuutil -o bench -- $B1 > /dev/null 2> $O/${TAG}_valu/valuutil.err &&
     timeout -s KILL 180 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $O/${TAG}_valu/issue -o bench -- $B1 > /dev/null 2> $O/${TAG}_valu/issue.err ;;
@@ -69,6 +76,7 @@ run_task() {
     spec=${1#tailpmc:}; w=${spec%%:*}; l=$(lib ${spec#*:}); n=$(basename $l .so); D=$O/${TAG}_tailpmc_${w}_$n
     T1="python3 tools/tail_latency.py --workload $w --top 1"
     export FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1
+    warm $T1 &&
     timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES --kernel-trace --output-format csv -d $D/mix -o tail -- $T1 > $D.mix.log 2>&1 &&
     timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $D/wait -o tail -- $T1 > $D.wait.log 2>&1 &&
     timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 --kernel-trace --output-format csv -d $D/valu -o tail -- $T1 > $D.valu.log 2>&1
@@ -77,6 +85,7 @@ run_task() {
     spec=${1#mix:}; w=${spec%%:*}; l=$(lib ${spec#*:}); n=$(basename $l .so); D=$O/${TAG}_mix_${w}_$n
     BM="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0 --workload $w"
     export FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1
+    warm $BM &&
     timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES --kernel-trace --output-format csv -d $D/mix -o m -- $BM > $D.mix.log 2>&1 &&
     timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $D/wait -o m -- $BM > $D.wait.log 2>&1 &&
     timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $D/more -o m -- $BM > $D.more.log 2>&1

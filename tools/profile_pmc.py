@@ -22,7 +22,7 @@ import json
 import os
 import sys
 
-KERNEL = "fks_simulate_linked"
+KERNEL = "fks_simulate_shaped"
 
 
 def counters(path, kernel=KERNEL):

@@ -17,13 +17,17 @@ def main():
     extra = []
     libs = []
     for a in sys.argv[1:]:
-        # "lib.so+flag" runs that library with bench.py --flag (e.g. libfks_hip.so+segment-steps=10)
+        # "lib.so+flag" runs that library with bench.py --flag (e.g. libfks_hip.so+segment-steps=10);
+        # "lib.so+env:NAME=VALUE" with that environment variable set
         (extra if a.startswith("--") or (extra and ".so" not in a) else libs).append(a)
     for spec in libs:
         lib, _, flag = spec.partition("+")
         env = dict(os.environ, FKS_LIB_PATH=os.path.abspath(lib), FKS_VARIANT_LIB="1")
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--pipeline-batches", "0", *extra]
-        if flag:
+        if flag.startswith("env:"):
+            name, _, value = flag[4:].partition("=")
+            env[name] = value
+        elif flag:
             cmd.append("--" + flag)
         p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=900)
         if p.returncode != 0:
