@@ -217,8 +217,8 @@ constexpr inline
     o += D;
     l.real = o;
     o += D;
-    l.misc = o;
-    o += 32;
+    l.misc = o; /* tw[6], phase sums, stats, self counters, hand-over words, wave totals */
+    o += 40;
     l.ints = o; /* int32 region: perm[64], transpositions[64], 16 spare words */
     o += (2 * kMaxDofs + 16) / 2;
     /* the second FK chain's joint motion matrices (paired FK of the next free microstep) */
@@ -246,7 +246,7 @@ constexpr inline
 
 /* per-wave scratch layout (doubles) */
 struct ScratchLayout {
-    uint64_t J, b, keys, corr, flag, cand, list, cellw, dense, rstate, total;
+    uint64_t J, b, keys, corr, flag, cand, list, cellw, dense, rstate, pid, total;
 };
 constexpr inline
 #if defined(__HIPCC__)
@@ -275,6 +275,8 @@ constexpr inline
     o += (G > 1) ? self_dense_words(G) : 8;
     l.rstate = o; /* the round skip-proof cache of a lean LDS block (kRoundState per round r < 64) */
     o += (uint64_t)kRoundState * 64u;
+    l.pid = o; /* the particle's controller state: error integral [dof], last error [64 + dof] */
+    o += 2u * 64u;
     l.total = (o + 7) & ~7ull;
     return l;
 }

@@ -229,6 +229,29 @@ constexpr int kDppQuadBcast1 = 0x55;  /* quad_perm [1,1,1,1] */
 constexpr int kDppQuadBcast2 = 0xAA;  /* quad_perm [2,2,2,2] */
 constexpr int kDppQuadBcast3 = 0xFF;  /* quad_perm [3,3,3,3] */
 
+/* The cross-row steps of a wave reduction once every row of 16 lanes holds its row's
+ * value: v_permlane16_swap / v_permlane32_swap (gfx950) give every lane the value of the
+ * lower and of the upper row (half) of its pair, so the combine runs in all lanes in the
+ * order the scalar tree (r0 . r1) . (r2 . r3) uses, with no v_readlane per row; the result
+ * is then read once from lane 0 (wave-uniform, so branches on it stay scalar). */
+#ifndef FKS_PERMLANE_REDUCE
+#define FKS_PERMLANE_REDUCE 1
+#endif
+template <bool HALVES>
+__device__ __forceinline__ void row_pair_f64(double v, double* lower, double* upper) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+    const auto l = HALVES ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false) : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = HALVES ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false) : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    *lower = __longlong_as_double((long long)(((uint64_t)h[0] << 32) | l[0]));
+    *upper = __longlong_as_double((long long)(((uint64_t)h[1] << 32) | l[1]));
+}
+__device__ __forceinline__ double readfirstlane_f64(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 /* canonical 64-lane sum (oracle canon_sum): xor butterfly with offsets 1, 2, 4,
  * 8, 16, 32; every lane gets the same value.  Call with all 64 lanes active. */
 __device__ __forceinline__ double bfly_sum(double v) {
@@ -236,8 +259,15 @@ __device__ __forceinline__ double bfly_sum(double v) {
     v = v + dpp_f64<kDppXor2>(v);
     v = v + dpp_f64<kDppHalfMirror>(v);
     v = v + dpp_f64<kDppMirror>(v);
+#if FKS_PERMLANE_REDUCE
+    double a, b;
+    row_pair_f64<false>(v, &a, &b);
+    row_pair_f64<true>(a + b, &a, &b); /* r0 + r1, r2 + r3 */
+    return readfirstlane_f64(a + b);
+#else
     const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16), r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
     return (r0 + r1) + (r2 + r3);
+#endif
 }
 /* max over lanes of non-negative values (order-insensitive) */
 __device__ __forceinline__ double wave_max_nonneg(double v) {
@@ -249,9 +279,16 @@ __device__ __forceinline__ double wave_max_nonneg(double v) {
     v = (o > v) ? o : v;
     o = dpp_f64<kDppMirror>(v);
     v = (o > v) ? o : v;
+#if FKS_PERMLANE_REDUCE
+    double a, b;
+    row_pair_f64<false>(v, &a, &b);
+    row_pair_f64<true>((b > a) ? b : a, &a, &b);
+    return readfirstlane_f64((b > a) ? b : a);
+#else
     const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16), r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
     const double a = (r1 > r0) ? r1 : r0, b = (r3 > r2) ? r3 : r2;
     return (b > a) ? b : a;
+#endif
 }
 /* OR over the wave's lanes.  Error bits are rare: one ballot answers the common
  * all-zero case without the six dependent LDS-crossbar shuffles. */
@@ -370,31 +407,108 @@ __device__ __forceinline__ uint32_t grid_brick(const GridDev& g, int32_t i, int3
     return brick_cell(g.nb, (uint32_t)i, (uint32_t)j, (uint32_t)k);
 }
 
+/* The wave's state.  Wave-uniform values live in SGPRs, which the hot loops run short of
+ * (every value live across the microstep loop that does not fit is spilled to a VGPR lane
+ * and costs a v_writelane / v_readlane per use): the LDS tables' addresses are therefore
+ * derived from the two block bases at each use (constant offsets in shape builds), the
+ * per-segment counters are 32-bit, and wave totals, timestamps and the particle id are not
+ * kept live across the particle loop (simulate_particles). */
+/* a linked robot's shape build carries no register copy of the controller state (Sim::pid_state) */
+/* Where the lane index lives (Sim::lane).  Register allocation at the 96-VGPR budget is
+ * chaotic, and the two choices measured best on different robots: the lean-block kernels
+ * (LDS-bound robots with long chains, cfg5) run 3.4 % faster reading the index from the
+ * hardware at each use, which keeps it from being spilled and reloaded across the microstep
+ * loop; the others keep it in a VGPR (cfg3 2.7 % faster that way) */
+#ifndef FKS_ASM_LANE
+#if defined(FKS_SHAPE_LEAN) && FKS_SHAPE_LEAN
+#define FKS_ASM_LANE 1
+#else
+#define FKS_ASM_LANE 0
+#endif
+#endif
+#if defined(FKS_SHAPE_TYPE) && FKS_SHAPE_TYPE == 0
+#define FKS_PID_REGS 0
+#else
+#define FKS_PID_REGS 1
+#endif
+/* the dynamic LDS of every kernel here: the workgroup's robot tables at offset 0, then one
+ * block per wave (LdsLayout) */
+extern __shared__ __attribute__((aligned(16))) double fks_lds[];
+
 struct Sim {
     const SimArgs* A;
-    double* lds;    /* this wave's LDS block */
-    double* shared; /* the workgroup's robot tables */
-    int32_t* ldsi;
+    double* lds_block; /* this wave's LDS block (a pointer: cfg5 ran 3-7 % slower with it formed from an offset at each use) */
     double* scratch;
-    int lane;
-    uint64_t pid;
+    int lane_v; /* the lane index (FKS_ASM_LANE 0) */
+    /* the lane index.  FKS_ASM_LANE: read from the hardware at each use (two VALU
+     * instructions in a volatile asm the optimiser can neither hoist nor share), so no lane
+     * index stays live across the loops to be spilled and reloaded */
+    __device__ __forceinline__ int lane() const {
+#if FKS_ASM_LANE
+        int ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        return ln;
+#else
+        return lane_v;
+#endif
+    }
     uint32_t step;
     uint32_t err;          /* per-lane error bits, OR-reduced at decision points */
     uint64_t lane_bytes;   /* per-lane algorithmic SDF bytes */
-    uint64_t micro_count, resolver_count, step_count, lsq_rows;
-    uint32_t* stats; /* LDS, lane 0 updates */
-    uint64_t* phase; /* LDS, FKS_NUM_PHASES cycle sums, lane 0 updates */
-    const JointDev* joints;          /* LDS copy of R.joints */
-    const fks_dof_controller* ctrl;  /* LDS copy of R.ctrl */
-    const int32_t* dofj;             /* LDS copy of R.dof_joint */
-    const double* base;              /* LDS copy of R.base */
-    double pid_integral, pid_last; /* DOF lanes */
+    uint64_t local;        /* particle index within the call (global id: pid()) */
+    uint32_t micro_count, resolver_count, step_count, lsq_rows; /* this segment's */
+    __device__ __forceinline__ double* lds() const { return lds_block; }
+    __device__ __forceinline__ double* shared() const { return fks_lds; }         /* the workgroup's robot tables */
+    __device__ __forceinline__ uint64_t pid() const { return A->first_pid + local; }
+    __device__ __forceinline__ uint32_t* stats() const { return reinterpret_cast<uint32_t*>(lds() + LAY(*A).misc + 24); } /* 8 x u32, lane 0 */
+    __device__ __forceinline__ uint64_t* phase() const { return reinterpret_cast<uint64_t*>(lds() + LAY(*A).misc + 8); } /* FKS_NUM_PHASES x u64, lane 0 */
+    __device__ __forceinline__ uint64_t* totals() const { return reinterpret_cast<uint64_t*>(lds() + LAY(*A).misc + 32); } /* kWaveTotals x u64, lane 0 */
+    __device__ __forceinline__ const JointDev* joints() const { return reinterpret_cast<const JointDev*>(shared() + LAY(*A).joints); }
+    __device__ __forceinline__ const fks_dof_controller* ctrl() const {
+        return reinterpret_cast<const fks_dof_controller*>(shared() + LAY(*A).ctrl);
+    }
+    __device__ __forceinline__ const int32_t* dofj() const { return reinterpret_cast<const int32_t*>(shared() + LAY(*A).dofj); }
+    __device__ __forceinline__ const double* base() const { return shared() + LAY(*A).base; }
+    /* the particle's controller state (lane d < D: error integral [d], last error [kWave + d]).
+     * Linked robots keep it in the wave's workspace rather than in two VGPR pairs live across
+     * the whole step loop (it is read and written once per controller step; cfg3's and cfg5's
+     * microstep loops lose most of their spill reloads); SE(2) / SE(3) robots keep the registers
+     * (the workspace copy moved cfg4's allocation the other way) */
+    __device__ __forceinline__ double* pid_state() const { return scratch + SLAY(*A).pid; }
+#if FKS_PID_REGS
+    double pid_integral, pid_last; /* DOF lanes, SE(2) / SE(3) */
+#endif
     double* rstate;  /* the round skip-proof cache: LDS block, or scratch in the lean kernels */
     bool self_nonempty;
     bool tcur_valid; /* Tcur == FK(particle configuration) from the end of the last step */
-    uint64_t local;            /* particle index within the call (traced kernels) */
     uint32_t tr_steps, tr_cfgs; /* trace records produced so far (traced kernels) */
 };
+template <int RT>
+__device__ __forceinline__ void pid_get(const Sim& s, int ln, double* integral, double* last) {
+    if constexpr (RT == FKS_ROBOT_LINKED) {
+        *integral = s.pid_state()[ln];
+        *last = s.pid_state()[kWave + ln];
+    } else {
+#if FKS_PID_REGS
+        *integral = s.pid_integral;
+        *last = s.pid_last;
+#endif
+    }
+}
+template <int RT>
+__device__ __forceinline__ void pid_set(Sim& s, int ln, double integral, double last) {
+    if constexpr (RT == FKS_ROBOT_LINKED) {
+        s.pid_state()[ln] = integral;
+        s.pid_state()[kWave + ln] = last;
+    } else {
+#if FKS_PID_REGS
+        s.pid_integral = integral;
+        s.pid_last = last;
+#endif
+    }
+}
+/* the wave's call totals in LDS (Sim::totals), flushed once when the queue is drained */
+enum { kTotSteps = 0, kTotMicro, kTotResolver, kTotLsq, kTotErrors, kWaveTotals };
 
 /* The lane index made opaque to the optimiser at the head of the microstep and
  * resolver loops: the per-lane LDS / workspace addresses derived from it are then
@@ -407,7 +521,7 @@ __device__ __forceinline__ int opaque_lane(int ln) {
 
 /* wave totals of the self-collision branch (kCntSelfChecks, kCntSelfPoints), kept in the
  * wave's LDS block (misc + 28, + 29) rather than in registers: the branch is rare */
-__device__ __forceinline__ uint64_t* self_counters(const Sim& s) { return reinterpret_cast<uint64_t*>(s.lds + LAY(*s.A).misc + 28); }
+__device__ __forceinline__ uint64_t* self_counters(const Sim& s) { return reinterpret_cast<uint64_t*>(s.lds() + LAY(*s.A).misc + 28); }
 
 /* ForwardSimulationStepTrace records (traced kernel instantiations only) */
 template <bool TR>
@@ -417,8 +531,8 @@ __device__ __forceinline__ void trace_config(Sim& s, const double* cfg, uint32_t
         const uint32_t k = s.tr_cfgs++;
         if (k < A.tr_cfg_cap) {
             const uint64_t rec = s.local * (uint64_t)A.tr_cfg_cap + k;
-            if (s.lane < RDIM(A.R, W)) A.tr_cfg[rec * (uint64_t)RDIM(A.R, W) + s.lane] = cfg[s.lane];
-            if (s.lane == 0) {
+            if (s.lane() < RDIM(A.R, W)) A.tr_cfg[rec * (uint64_t)RDIM(A.R, W) + s.lane()] = cfg[s.lane()];
+            if (s.lane() == 0) {
                 A.tr_tags[3 * rec] = s.step;
                 A.tr_tags[3 * rec + 1] = micro;
                 A.tr_tags[3 * rec + 2] = kind;
@@ -434,11 +548,11 @@ __device__ __forceinline__ void trace_step(Sim& s, const double* u, const double
         if (k < A.tr_step_cap) {
             const int D = RDIM(A.R, D);
             const uint64_t rec = s.local * (uint64_t)A.tr_step_cap + k;
-            if (s.lane < D) {
-                A.tr_inputs[rec * 2ull * (uint64_t)D + s.lane] = u[s.lane];
-                A.tr_inputs[rec * 2ull * (uint64_t)D + D + s.lane] = ustep[s.lane];
+            if (s.lane() < D) {
+                A.tr_inputs[rec * 2ull * (uint64_t)D + s.lane()] = u[s.lane()];
+                A.tr_inputs[rec * 2ull * (uint64_t)D + D + s.lane()] = ustep[s.lane()];
             }
-            if (s.lane == 0) A.tr_micro[rec] = M;
+            if (s.lane() == 0) A.tr_micro[rec] = M;
         }
     }
 }
@@ -455,11 +569,11 @@ __device__ __forceinline__ uint64_t tick() {
 }
 __device__ __forceinline__ void tock(Sim& s, int phase, uint64_t t0) {
     if constexpr (FKS_PHASE_TIMERS)
-        if (s.lane == 0) s.phase[phase] += tick() - t0;
+        if (s.lane() == 0) s.phase()[phase] += tick() - t0;
 }
 __device__ __forceinline__ void count_event(Sim& s, int slot, uint64_t n) {
     if constexpr (FKS_PHASE_TIMERS)
-        if (s.lane == 0) s.phase[slot] += n;
+        if (s.lane() == 0) s.phase()[slot] += n;
 }
 
 __device__ __noinline__ void refill_noise_lanes(const SimArgs* __restrict__ Ap, double* lds, int ln, uint64_t pid, uint32_t step,
@@ -484,14 +598,14 @@ __device__ __noinline__ void refill_noise_lanes(const SimArgs* __restrict__ Ap, 
     wsync();
 }
 __device__ FKS_SHAPE_INLINE void refill_noise(Sim& s, uint32_t micro0, uint32_t M) {
-    refill_noise_lanes(s.A, s.lds, s.lane, s.pid, s.step, micro0, M);
+    refill_noise_lanes(s.A, s.lds(), s.lane(), s.pid(), s.step, micro0, M);
 }
 __device__ __forceinline__ double noise_sample(Sim& s, uint32_t micro) {
     const SimArgs& A = *s.A;
     const int D = RDIM(A.R, D);
-    const int slot = (int)(micro % (uint32_t)(kWave / D)) * D + s.lane;
-    s.err |= reinterpret_cast<const uint32_t*>(s.lds + LAY(A).noise_err)[slot];
-    return s.lds[LAY(A).noise + slot];
+    const int slot = (int)(micro % (uint32_t)(kWave / D)) * D + s.lane();
+    s.err |= reinterpret_cast<const uint32_t*>(s.lds() + LAY(A).noise_err)[slot];
+    return s.lds()[LAY(A).noise + slot];
 }
 
 /* sdf_tools EstimateDistance4d (same spec as oracle SDF::EstimateDistance4d) */
@@ -582,10 +696,10 @@ __device__ __forceinline__ D4 load_point(const RobotDev& R, int i) {
 template <int RT>
 __device__ FKS_SHAPE_INLINE void fk(Sim& s, const double* cfg, double* T) {
     const RobotDev& R = s.A->R;
-    const int ln = s.lane;
+    const int ln = s.lane();
     if constexpr (RT == FKS_ROBOT_LINKED) {
-        double* jm = s.lds + LAY(*s.A).jm;
-        const JointDev* JD = s.joints;
+        double* jm = s.lds() + LAY(*s.A).jm;
+        const JointDev* JD = s.joints();
         if (ln < RDIM(R, J)) {
             const JointDev& jd = JD[ln];
             if (jd.type == FKS_JOINT_REVOLUTE || jd.type == FKS_JOINT_CONTINUOUS) {
@@ -608,7 +722,7 @@ __device__ FKS_SHAPE_INLINE void fk(Sim& s, const double* cfg, double* T) {
          * the same dot3 as the oracle. */
         const int r = ln >> 2, c = ln & 3;
         const bool act = ln < 12;
-        double own = act ? s.base[4 * r + c] : 0.0;
+        double own = act ? s.base()[4 * r + c] : 0.0;
         if (act) T[4 * r + c] = own;
         double p0 = dpp_f64<kDppQuadBcast0>(own), p1 = dpp_f64<kDppQuadBcast1>(own), p2 = dpp_f64<kDppQuadBcast2>(own),
                p3 = dpp_f64<kDppQuadBcast3>(own);
@@ -668,10 +782,10 @@ __device__ FKS_SHAPE_INLINE void fk(Sim& s, const double* cfg, double* T) {
  * both, so the pair costs about one FK; each chain is the same arithmetic as fk(). */
 __device__ FKS_SHAPE_INLINE void fk_pair(Sim& s, const double* cfgA, double* TA, const double* cfgB, double* TB) {
     const RobotDev& R = s.A->R;
-    const int ln = s.lane;
-    double* jmA = s.lds + LAY(*s.A).jm;
-    double* jmB = s.lds + LAY(*s.A).jm2;
-    const JointDev* JD = s.joints;
+    const int ln = s.lane();
+    double* jmA = s.lds() + LAY(*s.A).jm;
+    double* jmB = s.lds() + LAY(*s.A).jm2;
+    const JointDev* JD = s.joints();
     {
         const int j = ln & 31;
         const bool second = ln >= 32;
@@ -700,7 +814,7 @@ __device__ FKS_SHAPE_INLINE void fk_pair(Sim& s, const double* cfgA, double* TA,
     const bool act = local < 12 && ln < 32;
     double* T = chainB ? TB : TA;
     const double* jm = chainB ? jmB : jmA;
-    double own = act ? s.base[4 * r + c] : 0.0;
+    double own = act ? s.base()[4 * r + c] : 0.0;
     if (act) T[4 * r + c] = own;
     double p0 = dpp_f64<kDppQuadBcast0>(own), p1 = dpp_f64<kDppQuadBcast1>(own), p2 = dpp_f64<kDppQuadBcast2>(own),
            p3 = dpp_f64<kDppQuadBcast3>(own);
@@ -763,14 +877,14 @@ template <int RT>
 __device__ FKS_SHAPE_INLINE void apply_input(Sim& s, const double* cfg_in, const double* input, double* cfg_out, bool noisy, uint32_t micro) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
-    const int ln = s.lane;
+    const int ln = s.lane();
     if constexpr (RT == FKS_ROBOT_LINKED) {
         if (ln < RDIM(R, D)) {
-            const fks_dof_controller& ct = s.ctrl[ln];
+            const fks_dof_controller& ct = s.ctrl()[ln];
             const double vmax = dabs(ct.velocity_limit);
             double real = clamp(input[ln], -vmax, vmax);
             if (noisy) real = actuator_noisy(s, ct, ln, real, micro);
-            const JointDev& jd = s.joints[s.dofj[ln]];
+            const JointDev& jd = s.joints()[s.dofj()[ln]];
             const double raw = cfg_in[ln] + real;
             double v;
             if (jd.type == FKS_JOINT_CONTINUOUS) {
@@ -785,7 +899,7 @@ __device__ FKS_SHAPE_INLINE void apply_input(Sim& s, const double* cfg_in, const
         wsync();
     } else if constexpr (RT == FKS_ROBOT_SE2) {
         if (ln < 3) {
-            const fks_dof_controller& ct = s.ctrl[ln];
+            const fks_dof_controller& ct = s.ctrl()[ln];
             const double vmax = dabs(ct.velocity_limit);
             double real = clamp(input[ln], -vmax, vmax);
             if (noisy) real = actuator_noisy(s, ct, ln, real, micro);
@@ -795,9 +909,9 @@ __device__ FKS_SHAPE_INLINE void apply_input(Sim& s, const double* cfg_in, const
         }
         wsync();
     } else {
-        double* tw = s.lds + LAY(*s.A).misc; /* 6 doubles */
+        double* tw = s.lds() + LAY(*s.A).misc; /* 6 doubles */
         if (ln < 6) {
-            const fks_dof_controller& ct = s.ctrl[ln];
+            const fks_dof_controller& ct = s.ctrl()[ln];
             const double vmax = dabs(ct.velocity_limit);
             double real = clamp(input[ln], -vmax, vmax);
             if (noisy) real = actuator_noisy(s, ct, ln, real, micro);
@@ -824,11 +938,11 @@ template <int RT>
 __device__ FKS_SHAPE_INLINE double control_action(Sim& s, const double* cfg, const double* target) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
-    const int ln = s.lane;
+    const int ln = s.lane();
     double err = 0.0;
     if constexpr (RT == FKS_ROBOT_LINKED) {
         if (ln < RDIM(R, D)) {
-            const JointDev& jd = s.joints[s.dofj[ln]];
+            const JointDev& jd = s.joints()[s.dofj()[ln]];
             if (jd.type == FKS_JOINT_CONTINUOUS)
                 err = fks_math::enforce_continuous_revolute_bounds(target[ln] - cfg[ln]);
             else
@@ -853,11 +967,14 @@ __device__ FKS_SHAPE_INLINE double control_action(Sim& s, const double* cfg, con
     }
     double u = 0.0;
     if (ln < RDIM(R, D)) {
-        const fks_dof_controller& ct = s.ctrl[ln];
+        const fks_dof_controller& ct = s.ctrl()[ln];
         /* SimplePIDController::ComputeFeedbackTerm (PID:122-135), gains made positive (PID:104-113),
          * then the actuator's clamp (UNC:70-75) */
+        double integral, last;
+        pid_get<RT>(s, ln, &integral, &last);
         const double term = fks_control::pid_feedback_term(dabs(ct.kp), dabs(ct.ki), dabs(ct.kd), dabs(ct.integral_clamp),
-                                                           &s.pid_integral, &s.pid_last, err, A.dt);
+                                                           &integral, &last, err, A.dt);
+        pid_set<RT>(s, ln, integral, last);
         u = fks_control::actuator_clamp(term, dabs(ct.velocity_limit));
     }
     return u;
@@ -870,7 +987,7 @@ __device__ FKS_SHAPE_INLINE double config_distance(Sim& s, const double* cfg, co
     if constexpr (RT == FKS_ROBOT_LINKED) {
         double sum = 0.0;
         for (int k = 0; k < RDIM(R, D); ++k) {
-            const JointDev& jd = s.joints[s.dofj[k]];
+            const JointDev& jd = s.joints()[s.dofj()[k]];
             const double sd = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(target[k] - cfg[k])
                                                                 : target[k] - cfg[k];
             const double d = gp(R.weights)[k] * dabs(sd);
@@ -935,9 +1052,16 @@ __device__ __forceinline__ double wave_min(double v) {
     v = (o < v) ? o : v;
     o = dpp_f64<kDppMirror>(v);
     v = (o < v) ? o : v;
+#if FKS_PERMLANE_REDUCE
+    double a, b;
+    row_pair_f64<false>(v, &a, &b);
+    row_pair_f64<true>((b < a) ? b : a, &a, &b);
+    return readfirstlane_f64((b < a) ? b : a);
+#else
     const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16), r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
     const double a = (r1 < r0) ? r1 : r0, b = (r3 < r2) ? r3 : r2;
     return (b < a) ? b : a;
+#endif
 }
 constexpr double kInvalidRound = -1.0e308;
 constexpr uint64_t kNoTicket = ~0ull;
@@ -977,9 +1101,9 @@ enum { kSkipCheck = 1, kSkipCorrections = 2 };
 /* (link, radius) of round r < 64 from the workgroup's LDS copy of R.rounds */
 __device__ __forceinline__ RoundDev lds_round(const Sim& s, int r) {
     RoundDev o;
-    o.link = (int32_t)s.shared[LAY(*s.A).rounds + 2 * r];
+    o.link = (int32_t)s.shared()[LAY(*s.A).rounds + 2 * r];
     o.npts = 0;
-    o.radius = s.shared[LAY(*s.A).rounds + 2 * r + 1];
+    o.radius = s.shared()[LAY(*s.A).rounds + 2 * r + 1];
     return o;
 }
 
@@ -990,7 +1114,7 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
     const RobotDev& R = A.R;
     if (!A.skip_enabled) return 0ull;
     bool sk = false;
-    const int ln = s.lane;
+    const int ln = s.lane();
     if (ln < RDIM(R, nrounds)) {
         const RoundDev rd = lds_round(s, ln);
         const double* st = s.rstate + kRoundState * ln;
@@ -1025,8 +1149,8 @@ __device__ __forceinline__ void round_update(Sim& s, int r, const double* T, dou
     if (rd.link < 0) return;
     const double smin = wave_min(S), gmin = wave_min(G), cmin = wave_min(C);
     double* st = s.rstate + kRoundState * r;
-    if (s.lane < 12) st[s.lane] = T[12 * rd.link + s.lane];
-    if (s.lane == 0) {
+    if (s.lane() < 12) st[s.lane()] = T[12 * rd.link + s.lane()];
+    if (s.lane() == 0) {
         st[12] = smin;
         st[13] = gmin;
         st[14] = cmin;
@@ -1046,7 +1170,7 @@ __device__ __forceinline__ double round_max_motion(const RobotDev& R, const doub
 }
 __device__ FKS_SHAPE_INLINE double max_point_motion(Sim& s, const double* TA, const double* TB) {
     const RobotDev& R = s.A->R;
-    const int ln = s.lane;
+    const int ln = s.lane();
     const int nr = RDIM(R, nrounds);
     double m = 0.0;
     if (nr <= 2 || nr > kWave) {
@@ -1138,7 +1262,7 @@ __device__ FKS_SHAPE_INLINE bool env_collision(Sim& s, const double* T) {
     if (RDIM(R, nrounds) <= kWave) {
         const uint64_t all = (RDIM(R, nrounds) == kWave) ? ~0ull : ((1ull << RDIM(R, nrounds)) - 1ull);
         if ((skip & all) == all) {
-            if (s.lane < RDIM(R, P)) s.lane_bytes += 4ull * (uint64_t)((RDIM(R, P) - s.lane + kWave - 1) / kWave);
+            if (s.lane() < RDIM(R, P)) s.lane_bytes += 4ull * (uint64_t)((RDIM(R, P) - s.lane() + kWave - 1) / kWave);
             count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (uint64_t)RDIM(R, nrounds));
             return false;
         }
@@ -1150,7 +1274,7 @@ __device__ FKS_SHAPE_INLINE bool env_collision(Sim& s, const double* T) {
         double S0 = __builtin_huge_val(), S1 = __builtin_huge_val(), G0 = __builtin_huge_val(), G1 = __builtin_huge_val();
         double C0 = __builtin_huge_val(), C1 = __builtin_huge_val();
         bool c0 = false, c1 = false;
-        const int i0 = base + s.lane, i1 = base + kWave + s.lane;
+        const int i0 = base + s.lane(), i1 = base + kWave + s.lane();
         if (sk0)
             b0 = (i0 < RDIM(R, P)) ? 4 : 0;
         else
@@ -1167,13 +1291,13 @@ __device__ FKS_SHAPE_INLINE bool env_collision(Sim& s, const double* T) {
         const uint64_t m1 = __ballot(c1);
         if (m0) {
             const int first = __ffsll((unsigned long long)m0) - 1;
-            if (s.lane <= first) s.lane_bytes += b0;
+            if (s.lane() <= first) s.lane_bytes += b0;
             return true;
         }
         s.lane_bytes += b0;
         if (m1) {
             const int first = __ffsll((unsigned long long)m1) - 1;
-            if (s.lane <= first) s.lane_bytes += b1;
+            if (s.lane() <= first) s.lane_bytes += b1;
             return true;
         }
         s.lane_bytes += b1;
@@ -1378,12 +1502,12 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
 __device__ FKS_SHAPE_INLINE bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
-    const int ln = s.lane;
+    const int ln = s.lane();
     if (!RDIM(R, self_possible)) return false;
-    double* box = s.lds + LAY(*s.A).box;
+    double* box = s.lds() + LAY(*s.A).box;
     bool bad = false;
     if (ln < RDIM(R, G)) {
-        const double* gb = s.shared + LAY(A).gbox + 8 * ln;
+        const double* gb = s.shared() + LAY(A).gbox + 8 * ln;
         const int link = (int)gb[7];
         const double* T = Tc + 12 * link;
         double lo[3], hi[3];
@@ -1422,7 +1546,7 @@ __device__ FKS_SHAPE_INLINE bool self_collisions(Sim& s, const double* Tp, const
     }
     wsync();
     bool any = false;
-    const uint32_t* lpairs = reinterpret_cast<const uint32_t*>(s.shared + LAY(A).gpairs);
+    const uint32_t* lpairs = reinterpret_cast<const uint32_t*>(s.shared() + LAY(A).gpairs);
     for (int k = ln; k < RDIM(R, npairs); k += kWave) {
         int a, b;
         if (k < kLdsPairs) {
@@ -1438,7 +1562,7 @@ __device__ FKS_SHAPE_INLINE bool self_collisions(Sim& s, const double* Tp, const
         any = any || ov;
     }
     if (!wave_any(any || bad)) return false;
-    const uint32_t r = self_collisions_exact(s.A, s.lds, s.scratch, ln, s.err, Tp, Tc);
+    const uint32_t r = self_collisions_exact(s.A, s.lds(), s.scratch, ln, s.err, Tp, Tc);
     s.err = r >> 1;
     return (r & 1u) != 0u;
 }
@@ -1622,7 +1746,7 @@ __device__ FKS_SHAPE_INLINE bool check_collision(Sim& s, const double* Tp, const
         tock(s, FKS_PHASE_SELF_CHECK, t0);
     }
     s.self_nonempty = self;
-    if (self && s.lane == 0) self_counters(s)[0]++;
+    if (self && s.lane() == 0) self_counters(s)[0]++;
     return env || self;
 }
 
@@ -1630,13 +1754,13 @@ __device__ FKS_SHAPE_INLINE bool check_collision(Sim& s, const double* Tp, const
 template <int RT>
 __device__ FKS_SHAPE_INLINE void joint_frames(Sim& s, const double* Tc) {
     const RobotDev& R = s.A->R;
-    const int ln = s.lane;
+    const int ln = s.lane();
     if (RT == FKS_ROBOT_LINKED && ln < RDIM(R, D)) {
-        const JointDev& jd = s.joints[s.dofj[ln]];
+        const JointDev& jd = s.joints()[s.dofj()[ln]];
         const double* Tch = Tc + 12 * jd.child;
         const D3 aw = rotate(Tch, D3{jd.axis[0], jd.axis[1], jd.axis[2]});
-        double* axw = s.lds + LAY(*s.A).axis_w;
-        double* orw = s.lds + LAY(*s.A).orig_w;
+        double* axw = s.lds() + LAY(*s.A).axis_w;
+        double* orw = s.lds() + LAY(*s.A).orig_w;
         axw[3 * ln + 0] = aw.x;
         axw[3 * ln + 1] = aw.y;
         axw[3 * ln + 2] = aw.z;
@@ -1652,7 +1776,7 @@ template <int RT>
 __device__ FKS_SHAPE_INLINE uint32_t collect_corrections(Sim& s, const double* Tp, const double* Tc, const double* cfg) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
-    const int ln = s.lane;
+    const int ln = s.lane();
     const int D = RDIM(R, D);
     const ScratchLayout& SL = A.SL;
     FKS_GLOBAL double* J = gpw(s.scratch) + SL.J;
@@ -1661,8 +1785,8 @@ __device__ FKS_SHAPE_INLINE uint32_t collect_corrections(Sim& s, const double* T
     const FKS_GLOBAL double* flag = gp(s.scratch) + SL.flag;
     const uint32_t rc = ROWCAP(A);
     joint_frames<RT>(s, Tc);
-    const double* axw = s.lds + LAY(*s.A).axis_w;
-    const double* orw = s.lds + LAY(*s.A).orig_w;
+    const double* axw = s.lds() + LAY(*s.A).axis_w;
+    const double* orw = s.lds() + LAY(*s.A).orig_w;
     uint32_t rows = 0;
     /* rounds that provably hold no corrected point: their EstimateDistance reads are
      * counted (28 B per point, in bounds) but not made */
@@ -1724,7 +1848,7 @@ __device__ FKS_SHAPE_INLINE uint32_t collect_corrections(Sim& s, const double* T
                     D3 col{0.0, 0.0, 0.0};
                     if ((mask >> d) & 1ull) {
                         const D3 aw{axw[3 * d], axw[3 * d + 1], axw[3 * d + 2]};
-                        const int jt = s.joints[s.dofj[d]].type;
+                        const int jt = s.joints()[s.dofj()[d]].type;
                         if (jt == FKS_JOINT_PRISMATIC) {
                             col = aw;
                         } else {
@@ -1971,9 +2095,16 @@ __device__ __forceinline__ double wave_max_any(double v) {
     v = (o > v) ? o : v;
     o = dpp_f64<kDppMirror>(v);
     v = (o > v) ? o : v;
+#if FKS_PERMLANE_REDUCE
+    double a, b;
+    row_pair_f64<false>(v, &a, &b);
+    row_pair_f64<true>((b > a) ? b : a, &a, &b);
+    return readfirstlane_f64((b > a) ? b : a);
+#else
     const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16), r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
     const double a = (r1 > r0) ? r1 : r0, b = (r3 > r2) ? r3 : r2;
     return (b > a) ? b : a;
+#endif
 }
 /* the serial scan "best = first; for i > first: if (val[i] > best) take i" over the
  * lanes first..last-1 (lane i holds val[i]), as one wave reduction: the first lane
@@ -2600,14 +2731,14 @@ __device__ __noinline__ void qr_solve(const SimArgs* __restrict__ Ap, double* ld
  * system), the steps summed in point order (the first assigned, then raw + step).
  * No corrected point: the zero step (as the stacked solve of an empty system). */
 __device__ __noinline__ void individual_jacobians_solve(Sim& s, uint32_t Rn, double* x) {
-    const int ln = s.lane;
+    const int ln = s.lane();
     const int D = RDIM(s.A->R, D);
-    double* acc = s.lds + LAY(*s.A).real;
+    double* acc = s.lds() + LAY(*s.A).real;
     for (uint32_t r0 = 0; r0 < Rn; r0 += 3u) {
         if (D < kWave)
-            qr_solve_cols<8>(s.A, s.lds, s.scratch, ln, 3u, x, r0);
+            qr_solve_cols<8>(s.A, s.lds(), s.scratch, ln, 3u, x, r0);
         else
-            qr_solve(s.A, s.lds, s.scratch, ln, 3u, x, r0);
+            qr_solve(s.A, s.lds(), s.scratch, ln, 3u, x, r0);
         if (ln < D) acc[ln] = (r0 == 0u) ? x[ln] : acc[ln] + x[ln];
         wsync();
     }
@@ -2625,25 +2756,25 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                             bool* out_failed, double*& Tcur, double*& Tprev) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
-    const int ln = s.lane;
+    const int ln = s.lane();
     const int W = RDIM(R, W), D = RDIM(R, D);
-    double* u = s.lds + LAY(*s.A).u;
-    double* ustep = s.lds + LAY(*s.A).ustep;
-    double* cfg_tmp = s.lds + LAY(*s.A).cfg_tmp;
-    double* cfg_prev = s.lds + LAY(*s.A).cfg_prev;
-    double* cfg_act = s.lds + LAY(*s.A).cfg_act;
-    double* x = s.lds + LAY(*s.A).x;
-    double* real = s.lds + LAY(*s.A).real;
+    double* u = s.lds() + LAY(*s.A).u;
+    double* ustep = s.lds() + LAY(*s.A).ustep;
+    double* cfg_tmp = s.lds() + LAY(*s.A).cfg_tmp;
+    double* cfg_prev = s.lds() + LAY(*s.A).cfg_prev;
+    double* cfg_act = s.lds() + LAY(*s.A).cfg_act;
+    double* x = s.lds() + LAY(*s.A).x;
+    double* real = s.lds() + LAY(*s.A).real;
     /* the trial transforms live in whichever of the three transform buffers is neither
      * Tcur nor Tprev (the paired FK below rotates all three) */
     double* Ttmp;
     {
-        double* b0 = s.lds + LAY(*s.A).Tcur;
-        double* b1 = s.lds + LAY(*s.A).Tprev;
-        double* b2 = s.lds + LAY(*s.A).Ttmp;
+        double* b0 = s.lds() + LAY(*s.A).Tcur;
+        double* b1 = s.lds() + LAY(*s.A).Tprev;
+        double* b2 = s.lds() + LAY(*s.A).Ttmp;
         Ttmp = (b0 != Tcur && b0 != Tprev) ? b0 : ((b1 != Tcur && b1 != Tprev) ? b1 : b2);
     }
-    double* cfg = s.lds + LAY(*s.A).cfg_work; /* robot(immutable_robot->Clone()) SPCS:1548 */
+    double* cfg = s.lds() + LAY(*s.A).cfg_work; /* robot(immutable_robot->Clone()) SPCS:1548 */
     *out_collided = false;
     *out_failed = false;
     uint64_t t0 = tick();
@@ -2699,8 +2830,8 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
     bool pair_ready = false; /* Ttmp holds FK(cfg_tmp), cfg_tmp = the predicted configuration */
     uint32_t pair_err = 0;   /* the predicted configuration's actuator error bits (per lane) */
     for (uint32_t micro = 0; micro < M; ++micro) {
-        s.lane = opaque_lane(s.lane);
-        const int ln = s.lane;
+        s.lane_v = opaque_lane(s.lane_v);
+        const int ln = s.lane();
         s.micro_count++;
         if (ln < W) cfg_prev[ln] = cfg[ln];
         wsync();
@@ -2768,8 +2899,8 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
             uint32_t iters = 0;
             double scaling = A.S.resolve_correction_initial_step_size;
             while (in_collision) {
-                s.lane = opaque_lane(s.lane);
-                const int ln = s.lane;
+                s.lane_v = opaque_lane(s.lane_v);
+                const int ln = s.lane();
                 s.resolver_count++;
                 t0 = tick();
                 uint32_t Rn = collect_corrections<RT>(s, Tprev, Tcur, cfg_act);
@@ -2781,15 +2912,15 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                 if (IND || (TR && A.individual_jacobians)) {
                     individual_jacobians_solve(s, Rn, x);
                 } else if (Rn <= 8u && RDIM(R, D) < kWave)
-                    qr_solve_cols<8>(s.A, s.lds, s.scratch, ln, Rn, x);
+                    qr_solve_cols<8>(s.A, s.lds(), s.scratch, ln, Rn, x);
                 else if (Rn <= 16u && RDIM(R, D) < kWave)
-                    qr_solve_cols<16>(s.A, s.lds, s.scratch, ln, Rn, x);
+                    qr_solve_cols<16>(s.A, s.lds(), s.scratch, ln, Rn, x);
                 else if (Rn <= (uint32_t)kWave && RDIM(R, D) <= 8)
-                    qr_solve_regs<8>(s.A, s.lds, s.scratch, ln, Rn, x);
+                    qr_solve_regs<8>(s.A, s.lds(), s.scratch, ln, Rn, x);
                 else if (RT == FKS_ROBOT_LINKED && Rn <= (uint32_t)kWave && RDIM(R, D) <= 16)
-                    qr_solve_regs<RT == FKS_ROBOT_LINKED ? 16 : 8>(s.A, s.lds, s.scratch, ln, Rn, x);
+                    qr_solve_regs<RT == FKS_ROBOT_LINKED ? 16 : 8>(s.A, s.lds(), s.scratch, ln, Rn, x);
                 else
-                    qr_solve(s.A, s.lds, s.scratch, ln, Rn, x);
+                    qr_solve(s.A, s.lds(), s.scratch, ln, Rn, x);
                 tock(s, FKS_PHASE_SOLVE, t0);
                 t0 = tick();
                 apply_input<RT>(s, cfg_act, x, cfg_tmp, false, 0);
@@ -2818,8 +2949,8 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                 if (iters > A.S.max_resolver_iterations) {
                     trace_config<TR>(s, cfg_prev, micro, FKS_TRACE_RESOLVE_FAILED);
                     if (ln == 0) {
-                        s.stats[kCntUnsuccessful]++;
-                        s.stats[s.self_nonempty ? kCntUnsuccessfulSelf : kCntUnsuccessfulEnv]++;
+                        s.stats()[kCntUnsuccessful]++;
+                        s.stats()[s.self_nonempty ? kCntUnsuccessfulSelf : kCntUnsuccessfulEnv]++;
                     }
                     if (ln < W) res_cfg[ln] = cfg_prev[ln];
                     wsync();
@@ -2841,7 +2972,7 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
             /* the resolved configuration's check came back free (Tcur = FK(cfg)) */
         } else if (in_collision && !allow_contacts) {
             trace_config<TR>(s, cfg_prev, micro, FKS_TRACE_CONTACT_STOP);
-            if (s.lane == 0) s.stats[kCntSuccessful]++;
+            if (s.lane() == 0) s.stats()[kCntSuccessful]++;
             if (ln < W) res_cfg[ln] = cfg_prev[ln];
             wsync();
             *out_collided = true;
@@ -2849,8 +2980,8 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
         }
     }
     if (ln == 0) {
-        s.stats[kCntSuccessful]++;
-        s.stats[collided ? kCntCollision : kCntFree]++;
+        s.stats()[kCntSuccessful]++;
+        s.stats()[collided ? kCntCollision : kCntFree]++;
     }
     if (ln < W) res_cfg[ln] = cfg[ln];
     wsync();
@@ -2897,18 +3028,10 @@ __device__ __forceinline__ void setup_wave(const SimArgs* __restrict__ args, dou
         __syncthreads();
     }
     s.A = args;
-    s.shared = shared;
-    s.lds = lds_mem + LAY(A).shared_total + (uint64_t)wave * LAY(A).total;
-    s.ldsi = reinterpret_cast<int32_t*>(s.lds + LAY(A).ints);
+    s.lds_block = lds_mem + LAY(A).shared_total + (uint64_t)wave * LAY(A).total;
     s.scratch = A.scratch + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)wave) * A.scratch_per_wave;
-    s.lane = lane_id();
-    s.stats = reinterpret_cast<uint32_t*>(s.lds + LAY(*s.A).misc + 24);
-    s.phase = reinterpret_cast<uint64_t*>(s.lds + LAY(*s.A).misc + 8);
-    s.joints = reinterpret_cast<const JointDev*>(shared + LAY(A).joints);
-    s.ctrl = reinterpret_cast<const fks_dof_controller*>(shared + LAY(A).ctrl);
-    s.dofj = reinterpret_cast<const int32_t*>(shared + LAY(A).dofj);
-    s.base = shared + LAY(A).base;
-    s.rstate = s.lds + LAY(A).rstate; /* (the check / kinematics kernels keep no skip-proof cache) */
+    s.lane_v = lane_id();
+    s.rstate = s.lds() + LAY(A).rstate; /* (the check / kinematics kernels keep no skip-proof cache) */
     s.err = 0;
     s.lane_bytes = 0;
     s.self_nonempty = false;
@@ -2918,10 +3041,10 @@ __device__ __forceinline__ void setup_wave(const SimArgs* __restrict__ args, dou
 /* SetPosition(src) into cfg (LDS): joint limits / angle wrap as SetConfig does */
 template <int RT>
 __device__ __forceinline__ void set_position(Sim& s, const double* src, double* cfg) {
-    const int ln = s.lane;
+    const int ln = s.lane();
     if constexpr (RT == FKS_ROBOT_LINKED) {
         if (ln < RDIM(s.A->R, D)) {
-            const JointDev& jd = s.joints[s.dofj[ln]];
+            const JointDev& jd = s.joints()[s.dofj()[ln]];
             cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(src[ln])
                                                         : clamp(src[ln], jd.lo, jd.hi);
         }
@@ -3030,9 +3153,9 @@ __device__ __forceinline__ void check_configs(const SimArgs* __restrict__ args, 
     setup_wave<RT>(args, lds_mem, s);
     const SimArgs& A = *args;
     const RobotDev& R = A.R;
-    const int ln = s.lane;
-    double* cfg = s.lds + LAY(A).cfg;
-    double* T = s.lds + LAY(A).Tcur;
+    const int ln = s.lane();
+    double* cfg = s.lds() + LAY(A).cfg;
+    double* T = s.lds() + LAY(A).Tcur;
     const uint64_t stride = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint64_t bytes_total = 0;
     for (uint64_t c = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < A.n; c += stride) {
@@ -3063,7 +3186,7 @@ __device__ __forceinline__ void check_configs(const SimArgs* __restrict__ args, 
         }
         uint32_t r = 0;
         if constexpr (RT == FKS_ROBOT_LINKED) {
-            if (RDIM(R, self_possible)) r = config_self_collision(args, s.shared, s.lds, s.scratch, ln, T, A.self_res);
+            if (RDIM(R, self_possible)) r = config_self_collision(args, s.shared(), s.lds(), s.scratch, ln, T, A.self_res);
         }
         const uint64_t bytes = wave_sum_u64(lane_bytes);
         if (ln == 0) {
@@ -3086,15 +3209,15 @@ __device__ __forceinline__ void kinematics(const SimArgs* __restrict__ args, dou
     setup_wave<RT>(args, lds_mem, s);
     const SimArgs& A = *args;
     const RobotDev& R = A.R;
-    const int ln = s.lane;
-    double* cfg = s.lds + LAY(A).cfg;
-    double* out_cfg = s.lds + LAY(A).cfg_tmp;
-    double* T = s.lds + LAY(A).Tcur;
+    const int ln = s.lane();
+    double* cfg = s.lds() + LAY(A).cfg;
+    double* out_cfg = s.lds() + LAY(A).cfg_tmp;
+    double* T = s.lds() + LAY(A).Tcur;
     const uint64_t stride = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t c = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < A.n; c += stride) {
         set_position<RT>(s, A.starts + c * (uint64_t)RDIM(R, W), cfg);
         if (A.kin_mode == FKS_KIN_APPLY_CONTROL_INPUT) {
-            double* in = s.lds + LAY(A).u;
+            double* in = s.lds() + LAY(A).u;
             if (ln < RDIM(R, D)) in[ln] = A.targets[c * (uint64_t)RDIM(R, D) + ln];
             wsync();
             apply_input<RT>(s, cfg, in, out_cfg, false, 0);
@@ -3151,41 +3274,35 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     }
     Sim s;
     s.A = args;
-    s.shared = shared;
-    s.lds = lds_mem + LAY(A).shared_total + (uint64_t)wave * LAY(A).total;
-    s.ldsi = reinterpret_cast<int32_t*>(s.lds + LAY(A).ints);
+    s.lds_block = lds_mem + LAY(A).shared_total + (uint64_t)wave * LAY(A).total;
     s.scratch = A.scratch + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)wave) * A.scratch_per_wave;
-    s.lane = lane_id();
-    s.stats = reinterpret_cast<uint32_t*>(s.lds + LAY(*s.A).misc + 24); /* 8 x u32 */
-    s.phase = reinterpret_cast<uint64_t*>(s.lds + LAY(*s.A).misc + 8); /* FKS_NUM_PHASES x u64 */
-    s.joints = reinterpret_cast<const JointDev*>(shared + LAY(A).joints);
-    s.ctrl = reinterpret_cast<const fks_dof_controller*>(shared + LAY(A).ctrl);
-    s.dofj = reinterpret_cast<const int32_t*>(shared + LAY(A).dofj);
-    s.base = shared + LAY(A).base;
+    s.lane_v = lane_id();
     /* skip-proof cache of the first 64 rounds (the skip masks are 64-bit; later rounds are always
      * read): in the wave's LDS block, or in its scratch for a lean block (fixed per kernel, so
      * each instantiation addresses it with one kind of load) */
-    s.rstate = LEAN ? s.scratch + SLAY(A).rstate : s.lds + LAY(A).rstate;
-    if (s.lane < RDIM(R, nrounds)) s.rstate[kRoundState * s.lane + 12] = kInvalidRound;
+    s.rstate = LEAN ? s.scratch + SLAY(A).rstate : s.lds() + LAY(A).rstate;
+    if (s.lane() < RDIM(R, nrounds)) s.rstate[kRoundState * s.lane() + 12] = kInvalidRound;
     wsync();
-    const int ln = s.lane;
+    const int ln = s.lane();
     const int W = RDIM(R, W), D = RDIM(R, D);
-    double* cfg = s.lds + LAY(*s.A).cfg;
-    double* res_cfg = s.lds + LAY(*s.A).cfg_res;
-    double* u = s.lds + LAY(*s.A).u;
-    unsigned long long* next_particle = reinterpret_cast<unsigned long long*>(s.lds + LAY(*s.A).misc + 31);
-    uint32_t* seg_seen = reinterpret_cast<uint32_t*>(s.lds + LAY(*s.A).misc + 30);
-    const uint64_t t_resident = __builtin_amdgcn_s_memrealtime();
+    double* cfg = s.lds() + LAY(*s.A).cfg;
+    double* res_cfg = s.lds() + LAY(*s.A).cfg_res;
+    double* u = s.lds() + LAY(*s.A).u;
+    unsigned long long* next_particle = reinterpret_cast<unsigned long long*>(s.lds() + LAY(*s.A).misc + 31);
+    uint32_t* seg_seen = reinterpret_cast<uint32_t*>(s.lds() + LAY(*s.A).misc + 30);
     const uint32_t nseg = A.nseg;
     uint64_t carry = kNoTicket; /* the next segment of the particle just run, claimed by this wave */
     bool carry_heavy = false;   /* ... and whether the segment just run was contact-heavy */
     /* call counters are summed per wave and flushed once when the queue is drained
      * (per-segment device atomics on a handful of shared addresses would serialise) */
-    if (ln < 8) s.stats[ln] = 0;
-    if (ln < FKS_NUM_PHASES) s.phase[ln] = 0;
+    if (ln < 8) s.stats()[ln] = 0;
+    if (ln < FKS_NUM_PHASES) s.phase()[ln] = 0;
+    if (ln < kWaveTotals) s.totals()[ln] = 0;
     s.lane_bytes = 0;
-    uint64_t w_steps = 0, w_micro = 0, w_resolver = 0, w_lsq = 0, w_errors = 0;
     if (ln < 2) self_counters(s)[ln] = 0;
+    /* timestamps are folded into their LDS sums at once (end - start = (0 - start) + end),
+     * so none stays live across the particle loop */
+    if (ln == 0) s.phase()[FKS_PHASE_WAVE_RESIDENCY] = 0ull - __builtin_amdgcn_s_memrealtime();
     wsync();
     while (true) {
         /* ticket t: segment t / n of particle t % n, so every particle's first segment is
@@ -3227,20 +3344,21 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                 /* the queue is drained: this wave slot idles from here to the kernel's end */
                 const uint64_t bytes = wave_sum_u64(s.lane_bytes);
                 if (ln == 0) {
-                    s.phase[FKS_PHASE_WAVE_RESIDENCY] += __builtin_amdgcn_s_memrealtime() - t_resident;
+                    s.phase()[FKS_PHASE_WAVE_RESIDENCY] += __builtin_amdgcn_s_memrealtime();
                     for (int k = 0; k < 8; ++k)
-                        if (s.stats[k]) atomicAdd(A.counters + k, (unsigned long long)s.stats[k]);
-                    if (w_steps) atomicAdd(A.counters + kCntSteps, (unsigned long long)w_steps);
-                    if (w_micro) atomicAdd(A.counters + kCntMicrosteps, (unsigned long long)w_micro);
-                    if (w_resolver) atomicAdd(A.counters + kCntResolver, (unsigned long long)w_resolver);
-                    if (w_lsq) atomicAdd(A.counters + kCntLsqRows, (unsigned long long)w_lsq);
+                        if (s.stats()[k]) atomicAdd(A.counters + k, (unsigned long long)s.stats()[k]);
+                    const uint64_t* wt = s.totals();
+                    if (wt[kTotSteps]) atomicAdd(A.counters + kCntSteps, (unsigned long long)wt[kTotSteps]);
+                    if (wt[kTotMicro]) atomicAdd(A.counters + kCntMicrosteps, (unsigned long long)wt[kTotMicro]);
+                    if (wt[kTotResolver]) atomicAdd(A.counters + kCntResolver, (unsigned long long)wt[kTotResolver]);
+                    if (wt[kTotLsq]) atomicAdd(A.counters + kCntLsqRows, (unsigned long long)wt[kTotLsq]);
                     if (bytes) atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes);
-                    if (w_errors) atomicAdd(A.counters + kCntErrorParticles, (unsigned long long)w_errors);
+                    if (wt[kTotErrors]) atomicAdd(A.counters + kCntErrorParticles, (unsigned long long)wt[kTotErrors]);
                     const uint64_t* sc = self_counters(s);
                     if (sc[0]) atomicAdd(A.counters + kCntSelfChecks, (unsigned long long)sc[0]);
                     if (sc[1]) atomicAdd(A.counters + kCntSelfPoints, (unsigned long long)sc[1]);
                     for (int k = 0; k < FKS_NUM_PHASES; ++k)
-                        if (s.phase[k]) atomicAdd(A.counters + kPhaseBase + k, (unsigned long long)s.phase[k]);
+                        if (s.phase()[k]) atomicAdd(A.counters + kPhaseBase + k, (unsigned long long)s.phase()[k]);
                 }
                 break;
             }
@@ -3261,7 +3379,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         const uint32_t step_begin = (uint32_t)seg * A.seg_steps;
         const uint32_t step_end = (seg + 1 == (uint64_t)nseg) ? A.T : step_begin + A.seg_steps;
         double* st = A.seg_state + local * (uint64_t)A.seg_stride; /* nseg > 1 only */
-        s.pid = A.first_pid + local;
         s.local = local;
         s.tr_steps = 0;
         s.tr_cfgs = 0;
@@ -3270,23 +3387,23 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         s.resolver_count = 0;
         s.lsq_rows = 0;
         s.step_count = 0;
-        const uint64_t t_particle = __builtin_amdgcn_s_memtime();
+        if (ln == 0) s.phase()[FKS_PHASE_PARTICLE] -= __builtin_amdgcn_s_memtime();
         s.self_nonempty = false;
         s.tcur_valid = false;
         const double* start = A.starts + local * (uint64_t)W;
         const double* target = (A.num_targets == A.n) ? A.targets + local * (uint64_t)W : A.targets;
         bool collided = false;
         bool any_failed = false;
-        uint64_t micro_before = 0, resolver_before = 0;
         if (seg == 0) {
             /* ResetPosition zeroes the controllers (TNUVA:524-536); ForwardSimulateMutableRobot
              * continues the robot's own (SPCS:843-919, fks_forward_simulate_mutable) */
-            s.pid_integral = (A.pid_io && ln < D) ? A.pid_io[local * 2ull * (uint64_t)D + ln] : 0.0;
-            s.pid_last = (A.pid_io && ln < D) ? A.pid_io[local * 2ull * (uint64_t)D + D + ln] : 0.0;
+            if (ln < D)
+                pid_set<RT>(s, ln, A.pid_io ? A.pid_io[local * 2ull * (uint64_t)D + ln] : 0.0,
+                            A.pid_io ? A.pid_io[local * 2ull * (uint64_t)D + D + ln] : 0.0);
             /* ResetPosition(start): SetPosition enforces joint limits / angle wrap */
             if constexpr (RT == FKS_ROBOT_LINKED) {
                 if (ln < D) {
-                    const JointDev& jd = s.joints[s.dofj[ln]];
+                    const JointDev& jd = s.joints()[s.dofj()[ln]];
                     cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(start[ln])
                                                                 : clamp(start[ln], jd.lo, jd.hi);
                 }
@@ -3299,29 +3416,27 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             /* resume: configuration from out_q, controller state and per-particle totals
              * from seg_state (bit-exact: the step loop below recomputes FK at its start) */
             if (ln < W) cfg[ln] = load_coherent(A.out_q + local * (uint64_t)W + ln);
-            s.pid_integral = (ln < D) ? load_coherent(st + ln) : 0.0;
-            s.pid_last = (ln < D) ? load_coherent(st + D + ln) : 0.0;
+            if (ln < D) pid_set<RT>(s, ln, load_coherent(st + ln), load_coherent(st + D + ln));
             const uint64_t* sw = reinterpret_cast<const uint64_t*>(st + 2 * D);
             const uint64_t flags = load_coherent_u64(sw);
             collided = (flags & 1ull) != 0;
             any_failed = (flags & 2ull) != 0;
-            micro_before = load_coherent_u64(sw + 1);
-            resolver_before = load_coherent_u64(sw + 2);
+            /* the particle's totals so far (sw + 1, + 2) are read again at the segment's end */
             /* the particle's own skip-proof cache (the rounds' last full evaluations) */
             const int nrc = kRoundState * (RDIM(R, nrounds) < kWave ? RDIM(R, nrounds) : kWave);
             for (int e = ln; e < nrc; e += kWave) s.rstate[e] = load_coherent(st + 2 * D + 4 + e);
         }
         wsync();
-        double* Tcur = s.lds + LAY(*s.A).Tcur;
-        double* Tprev = s.lds + LAY(*s.A).Tprev;
+        double* Tcur = s.lds() + LAY(*s.A).Tcur;
+        double* Tprev = s.lds() + LAY(*s.A).Tprev;
         bool ended = false;
         /* ForwardSimulateMutableRobot (SPCS:843-919) */
         for (uint32_t step = step_begin; step < step_end; ++step) {
-            s.lane = opaque_lane(s.lane);
-            const int ln = s.lane;
+            s.lane_v = opaque_lane(s.lane_v);
+            const int ln = s.lane();
             s.step = step;
             s.step_count++;
-            double* tgt_lds = s.lds + LAY(*s.A).tgt;
+            double* tgt_lds = s.lds() + LAY(*s.A).tgt;
             const uint64_t t0 = tick();
             const double uc = control_action<RT>(s, cfg, target);
             if (ln < D) u[ln] = uc * A.dt;
@@ -3345,7 +3460,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                     }
                     any_failed = true;
                 } else if (any_failed) {
-                    if (s.lane == 0) s.stats[kCntRecovered]++;
+                    if (s.lane() == 0) s.stats()[kCntRecovered]++;
                 }
                 if (A.S.simulation_shortcut_distance > 0.0 || A.S.simulation_shortcut_distance != A.S.simulation_shortcut_distance) {
                     if (ln < W) tgt_lds[ln] = target[ln];
@@ -3366,12 +3481,18 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         /* outputs (the configuration doubles as the resting state between segments) */
         const uint64_t t_out = __builtin_amdgcn_s_memtime();
         if (ln < W) store_coherent(A.out_q + local * (uint64_t)W + ln, cfg[ln]);
-        const uint64_t micro_total = micro_before + s.micro_count;
-        const uint64_t resolver_total = resolver_before + s.resolver_count;
+        uint64_t micro_total = s.micro_count, resolver_total = s.resolver_count;
+        if (seg > 0) {
+            const uint64_t* sw = reinterpret_cast<const uint64_t*>(st + 2 * D);
+            micro_total += load_coherent_u64(sw + 1);
+            resolver_total += load_coherent_u64(sw + 2);
+        }
         if (!ended) {
             if (ln < D) {
-                store_coherent(st + ln, s.pid_integral);
-                store_coherent(st + D + ln, s.pid_last);
+                double integral, last;
+                pid_get<RT>(s, ln, &integral, &last);
+                store_coherent(st + ln, integral);
+                store_coherent(st + D + ln, last);
             }
             if (ln == 0) {
                 uint64_t* sw = reinterpret_cast<uint64_t*>(st + 2 * D);
@@ -3382,14 +3503,19 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             const int nrc = kRoundState * (RDIM(R, nrounds) < kWave ? RDIM(R, nrounds) : kWave);
             for (int e = ln; e < nrc; e += kWave) store_coherent(st + 2 * D + 4 + e, s.rstate[e]);
         }
-        w_steps += s.step_count;
-        w_micro += s.micro_count;
-        w_resolver += s.resolver_count;
-        w_lsq += s.lsq_rows;
-        if (s.err) w_errors++;
+        if (ln == 0) {
+            uint64_t* wt = s.totals();
+            wt[kTotSteps] += s.step_count;
+            wt[kTotMicro] += s.micro_count;
+            wt[kTotResolver] += s.resolver_count;
+            wt[kTotLsq] += s.lsq_rows;
+            if (s.err) wt[kTotErrors]++;
+        }
         if (ended && A.pid_io && ln < D) {
-            A.pid_io[local * 2ull * (uint64_t)D + ln] = s.pid_integral;
-            A.pid_io[local * 2ull * (uint64_t)D + D + ln] = s.pid_last;
+            double integral, last;
+            pid_get<RT>(s, ln, &integral, &last);
+            A.pid_io[local * 2ull * (uint64_t)D + ln] = integral;
+            A.pid_io[local * 2ull * (uint64_t)D + D + ln] = last;
         }
         if (ln == 0) {
             if (ended) {
@@ -3403,8 +3529,8 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                 }
             }
             const uint64_t t_end = __builtin_amdgcn_s_memtime();
-            s.phase[FKS_PHASE_OUTPUT] += t_end - t_out;
-            s.phase[FKS_PHASE_PARTICLE] += t_end - t_particle;
+            s.phase()[FKS_PHASE_OUTPUT] += t_end - t_out;
+            s.phase()[FKS_PHASE_PARTICLE] += t_end;
         }
         if (nseg > 1) {
             /* publish the resting state; if the next segment's ticket is already out, claim

@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import loop_spills as L  # noqa: E402
 
 path = sys.argv[1]
-lines = L.kernel_lines(path, 'fks_simulate_linked')
+lines = L.kernel_lines(path, sys.argv[2] if len(sys.argv) > 2 else 'fks_simulate_shaped')
 blocks, loops = L.analyse(lines)
 def calls(body, pat):
     return any(pat in l for k in body for l in lines[blocks[k][1]:blocks[k][2]] if "rel32@lo" in l)
