@@ -1141,13 +1141,42 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
     return __ballot(sk);
 }
 
-/* cache the state of round r after a full evaluation at T (uniform call) */
+/* minimum over the wave of a float (all 64 lanes active): DPP steps inside rows of 16 (folded
+ * into v_min_f32), then the row pairs by v_permlane16/32_swap, read once from lane 0 */
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_min_f32(float v) {
+    v = fminf(v, dpp_f32<kDppXor1>(v));
+    v = fminf(v, dpp_f32<kDppXor2>(v));
+    v = fminf(v, dpp_f32<kDppHalfMirror>(v));
+    v = fminf(v, dpp_f32<kDppMirror>(v));
+    const uint32_t b = (uint32_t)__float_as_int(v);
+    const auto p16 = __builtin_amdgcn_permlane16_swap(b, b, false, false);
+    v = fminf(__int_as_float((int)p16[0]), __int_as_float((int)p16[1]));
+    const uint32_t c = (uint32_t)__float_as_int(v);
+    const auto p32 = __builtin_amdgcn_permlane32_swap(c, c, false, false);
+    v = fminf(__int_as_float((int)p32[0]), __int_as_float((int)p32[1]));
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+/* a float no larger than x (x finite >= kInvalidRound, or +inf): the proofs use the cached
+ * margins as lower bounds, so they are rounded down (by far more than the conversion's error) */
+__device__ __forceinline__ float lower_f32(double x) {
+    return (x < 3.0e38) ? (float)(x - (dabs(x) * 0x1p-20 + 0x1p-20)) : (float)x;
+}
+
+/* cache the state of round r after a full evaluation at T (uniform call).  The three minima
+ * are taken in single precision: S is a float SDF value (exact; kInvalidRound becomes -inf,
+ * which the validity tests treat alike), G and C are rounded down first.  Only skip decisions
+ * read them, and those never change a result or a byte count (parity tests, counters). */
 __device__ __forceinline__ void round_update(Sim& s, int r, const double* T, double S, double G, double C) {
     const SimArgs& A = *s.A;
     if (!A.skip_enabled || r >= kWave || r >= RDIM(A.R, nrounds)) return;
     const RoundDev rd = lds_round(s, r);
     if (rd.link < 0) return;
-    const double smin = wave_min(S), gmin = wave_min(G), cmin = wave_min(C);
+    const double smin = (double)wave_min_f32((float)S), gmin = (double)wave_min_f32(lower_f32(G)),
+                 cmin = (double)wave_min_f32(lower_f32(C));
     double* st = s.rstate + kRoundState * r;
     if (s.lane() < 12) st[s.lane()] = T[12 * rd.link + s.lane()];
     if (s.lane() == 0) {
