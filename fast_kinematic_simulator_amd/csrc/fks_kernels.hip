@@ -1119,18 +1119,24 @@ __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, in
         const RoundDev rd = lds_round(s, ln);
         const double* st = s.rstate + kRoundState * ln;
         if (rd.link >= 0 && st[12] > kInvalidRound) {
-            const double b = rigid_motion_bound(T + 12 * rd.link, st, rd.radius) * A.sdf_g.inv_res; /* cells */
+            const double bm = rigid_motion_bound(T + 12 * rd.link, st, rd.radius);
+            const double b = bm * A.sdf_g.inv_res; /* cells */
             const double K = 1.7320508075688773 * b + 3.0;
             const double Sr = st[12] * A.sdf_g.inv_res;
             const double lp = A.skip_lplus;
             const bool inb = st[13] - b > 1e-6;
-            /* every point still in the cell it was evaluated in: nearest values unchanged
-             * (always true for a link that has not moved at all, e.g. a fixed base) */
-            const double* Tl = T + 12 * rd.link;
-            bool still = true;
+            /* every point still in the cell it was evaluated in: nearest values unchanged.  The
+             * bound says so unless a point sits within 1e-9 cells of a face; then only a link
+             * that has not moved at all (e.g. a fixed base) keeps it there — which needs every
+             * difference zero, so the bound is at its floor (1e-12) and only then is compared */
+            bool same_cell = b < st[14] - 1e-9;
+            if (!same_cell && bm <= 1e-12) {
+                const double* Tl = T + 12 * rd.link;
+                bool still = true;
 #pragma unroll
-            for (int e = 0; e < 12; ++e) still = still && (Tl[e] == st[e]);
-            const bool same_cell = still || b < st[14] - 1e-9;
+                for (int e = 0; e < 12; ++e) still = still && (Tl[e] == st[e]);
+                same_cell = still;
+            }
             if (what == kSkipCheck)
                 sk = (inb && (Sr - A.skip_cmax) > (K - 1.0) * lp + 1e-9) || (same_cell && st[12] >= A.thr_env);
             else
