@@ -49,6 +49,8 @@ def test_full_batch_blocks_match_oracle(fks_lib, oracle_lib, name, scale, nblock
         sim.set_call_index(5)
         g = sim.forward_simulate_arrays(wl.robot, wl.starts, wl.targets, True)
         c = sim.last_call_counters()
+        # the library's default path for a full batch: the robot's shape-specialised kernel
+        assert sim.launch_info()["last_kernel"] == "shaped", (sim.launch_info(), sim.specialization())
         sim.set_call_index(5)
         g2 = sim.forward_simulate_arrays(wl.robot, wl.starts, wl.targets, True)
         # the batch outnumbers the resident waves, so the launches above ran in
