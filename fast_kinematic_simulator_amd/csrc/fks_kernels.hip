@@ -2958,19 +2958,37 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                     qr_solve(s.A, s.lds(), s.scratch, ln, Rn, x);
                 tock(s, FKS_PHASE_SOLVE, t0);
                 t0 = tick();
-                apply_input<RT>(s, cfg_act, x, cfg_tmp, false, 0);
-                fk<RT>(s, cfg_tmp, Ttmp);
-                const double est = max_point_motion(s, Tcur, Ttmp);
-                const double step_fraction = dmax(est / A.allowed_micro, 1.0);
-                if (step_fraction == 1.0 && dabs(scaling) == 1.0) {
-                    /* real_correction_step = (x / 1) * 1 == x bit for bit (SPCS:1681-1682): the
-                     * corrected configuration is cfg_tmp and its transforms are Ttmp */
-                    if (ln < W) cfg_act[ln] = cfg_tmp[ln];
-                    for (int e = ln; e < 12 * RDIM(R, L); e += kWave) Tcur[e] = Ttmp[e];
-                    wsync();
+                /* SPCS:1663-1682: the correction's workspace motion est decides
+                 * step_fraction = max(est / allowed, 1).  For a linked robot the lever-arm
+                 * bound sum_d |x_d| * lever_d (clamping and wrapping only shorten joint
+                 * motion) often proves est <= allowed, i.e. step_fraction == 1 exactly; the
+                 * trial FK and the motion estimate are then not needed and the real step
+                 * (x / 1) * |scaling| == x * |scaling| is applied directly */
+                bool fraction_one = false;
+                if constexpr (RT == FKS_ROBOT_LINKED) {
+                    const double term = (ln < D) ? dabs(x[ln]) * gp(R.dof_lever)[ln] : 0.0;
+                    fraction_one = bfly_sum(0.0 + term) * (1.0 + 1e-6) + 1e-12 < A.allowed_micro;
+                }
+                bool applied = false; /* cfg_act and Tcur already hold the corrected state */
+                if (fraction_one) {
+                    if (ln < D) real[ln] = x[ln] * dabs(scaling);
                 } else {
-                    if (ln < D) real[ln] = (x[ln] / step_fraction) * dabs(scaling);
-                    wsync();
+                    apply_input<RT>(s, cfg_act, x, cfg_tmp, false, 0);
+                    fk<RT>(s, cfg_tmp, Ttmp);
+                    const double est = max_point_motion(s, Tcur, Ttmp);
+                    const double step_fraction = dmax(est / A.allowed_micro, 1.0);
+                    if (step_fraction == 1.0 && dabs(scaling) == 1.0) {
+                        /* real_correction_step = (x / 1) * 1 == x bit for bit (SPCS:1681-1682): the
+                         * corrected configuration is cfg_tmp and its transforms are Ttmp */
+                        if (ln < W) cfg_act[ln] = cfg_tmp[ln];
+                        for (int e = ln; e < 12 * RDIM(R, L); e += kWave) Tcur[e] = Ttmp[e];
+                        applied = true;
+                    } else if (ln < D) {
+                        real[ln] = (x[ln] / step_fraction) * dabs(scaling);
+                    }
+                }
+                wsync();
+                if (!applied) {
                     apply_input<RT>(s, cfg_act, real, cfg_tmp, false, 0);
                     if (ln < W) cfg_act[ln] = cfg_tmp[ln];
                     wsync();

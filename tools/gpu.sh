@@ -92,7 +92,8 @@ run_task() {
     rc=$?; unset FKS_LIB_PATH FKS_VARIANT_LIB; return $rc ;;
   sched:*)
     spec=${1#sched:}; w=${spec%%:*}; rest=${spec#*:}; seg=${rest%%:*}; heavy=${rest#*:}
-    timeout -k 10 600 python tools/sched_sweep.py --workload $w --segments $seg --heavy $heavy --prio 1 --json $O/${TAG}_sched_$w.json > $O/${TAG}_sched_$w.log 2>&1 ;;
+    np=""; [ "$w" = cfg4 -o "$w" = cfg5 ] && np="--particles 131072"
+    timeout -k 10 600 python tools/sched_sweep.py --workload $w $np --segments $seg --heavy $heavy --prio 1 --json $O/${TAG}_sched_$w.json > $O/${TAG}_sched_$w.log 2>&1 ;;
   torchrun1) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_torchrun_w1.json 2> $O/${TAG}_torchrun_w1.err ;;
   round) for t in suite smoke bench trace pmc others; do run_task $t || return $?; done ;;
   *) echo "unknown task $1" >&2; return 2 ;;

@@ -29,9 +29,13 @@ def main():
     ap.add_argument("--heavy", default="1,2,4,65536")
     ap.add_argument("--prio", default="0,1,2")
     ap.add_argument("--json", default="")
+    ap.add_argument("--particles", type=int, default=0, help="batch size (default: the workload's base count)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     wl = W.WORKLOADS[a.workload]()
+    if a.particles:
+        wl = W.WORKLOADS[a.workload](scale=a.particles / float(wl.num_particles))
+    wl._env = W.SCENES[a.workload](device=0)  # the GPU build (same bytes as the host's)
     sim = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
     sim.set_robot(wl.robot)
     n = wl.num_particles
