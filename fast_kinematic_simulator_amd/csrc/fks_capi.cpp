@@ -927,6 +927,22 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
             /* AngleAxis with a non-unit axis is not a rotation: no bound */
             lever[k] = (std::fabs(an - 1.0) < 1e-12 && std::isfinite(worst)) ? worst * (1.0 + 1e-9) + 1e-12 : HUGE_VAL;
         }
+    } else {
+        /* SE(2) (x, y, theta, applied additively) and SE(3) (body twist v, w: P * exp(twist)):
+         * a point p of the body moves by at most |dt| + |rotation angle| * |p|, the angle at most
+         * the sum of the angular components' magnitudes and |V v| <= |v| (exp's V has operator
+         * norm <= 1), so translation components get lever 1, rotation components max |p| */
+        bool w_one = true;
+        double rmax = 0.0;
+        for (uint32_t i = 0; i < P; ++i) {
+            const double* p = d->points + 4 * (size_t)i;
+            w_one = w_one && p[3] == 1.0;
+            rmax = std::max(rmax, std::sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]));
+        }
+        if (w_one && std::isfinite(rmax)) {
+            const int nt = d->robot_type == FKS_ROBOT_SE2 ? 2 : 3; /* translation components first */
+            for (int k = 0; k < R.D; ++k) lever[k] = (k < nt) ? 1.0 + 1e-9 : rmax * (1.0 + 1e-9) + 1e-12;
+        }
     }
     std::vector<double> weights;
     if (d->robot_type == FKS_ROBOT_LINKED) {

@@ -2832,11 +2832,12 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
     if (ln < D) ustep[ln] = u[ln] / (double)M;
     wsync();
     /* SPCS:1563-1575: the motion of one clean microstep must not exceed the allowed
-     * distance.  Linked robots: sum_d |u_d / M| * lever_d bounds it (clamping only
-     * shortens joint motion), so the check is evaluated only when the bound does not
-     * already prove it. */
+     * distance.  sum_d |u_d / M| * lever_d bounds it (clamping only shortens the
+     * motion), so the check is evaluated only when the bound does not already prove it. */
     bool proven = false;
-    if constexpr (RT == FKS_ROBOT_LINKED) {
+    {
+        /* per-dof lever arms (fks_set_robot): linked joints' reach, SE(2) / SE(3) 1 for
+         * translation and max |p| for rotation components; +inf where no bound holds */
         const double term = (ln < D) ? dabs(ustep[ln]) * gp(R.dof_lever)[ln] : 0.0;
         const double bound = bfly_sum(0.0 + term);
         proven = bound * (1.0 + 1e-6) + 1e-12 < A.allowed_micro;
@@ -2959,13 +2960,14 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                 tock(s, FKS_PHASE_SOLVE, t0);
                 t0 = tick();
                 /* SPCS:1663-1682: the correction's workspace motion est decides
-                 * step_fraction = max(est / allowed, 1).  For a linked robot the lever-arm
-                 * bound sum_d |x_d| * lever_d (clamping and wrapping only shorten joint
-                 * motion) often proves est <= allowed, i.e. step_fraction == 1 exactly; the
+                 * step_fraction = max(est / allowed, 1).  The lever-arm bound
+                 * sum_d |x_d| * lever_d (clamping and wrapping only shorten the motion; SE(2) /
+                 * SE(3) levers in fks_set_robot) often proves est <= allowed, i.e.
+                 * step_fraction == 1 exactly; the
                  * trial FK and the motion estimate are then not needed and the real step
                  * (x / 1) * |scaling| == x * |scaling| is applied directly */
-                bool fraction_one = false;
-                if constexpr (RT == FKS_ROBOT_LINKED) {
+                bool fraction_one;
+                {
                     const double term = (ln < D) ? dabs(x[ln]) * gp(R.dof_lever)[ln] : 0.0;
                     fraction_one = bfly_sum(0.0 + term) * (1.0 + 1e-6) + 1e-12 < A.allowed_micro;
                 }
