@@ -2933,7 +2933,17 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
             if (ln < W) cfg_act[ln] = cfg[ln];
             wsync();
             uint32_t iters = 0;
-            double scaling = A.S.resolve_correction_initial_step_size;
+            /* the correction step scaling: a linked robot keeps it in the wave's LDS block
+             * (misc + 38), one uniform double fewer live across the resolver loop (fewer spill
+             * reloads on cfg3 / cfg5); SE(2) / SE(3) keep the register (cfg4's allocation
+             * went the other way) */
+            constexpr bool kScalingLds = RT == FKS_ROBOT_LINKED;
+            double* scaling_p = s.lds() + LAY(*s.A).misc + 38;
+            double scaling_reg = A.S.resolve_correction_initial_step_size;
+            if (kScalingLds) {
+                if (ln == 0) *scaling_p = scaling_reg;
+                wsync();
+            }
             while (in_collision) {
                 s.lane_v = opaque_lane(s.lane_v);
                 const int ln = s.lane();
@@ -2971,26 +2981,25 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                     const double term = (ln < D) ? dabs(x[ln]) * gp(R.dof_lever)[ln] : 0.0;
                     fraction_one = bfly_sum(0.0 + term) * (1.0 + 1e-6) + 1e-12 < A.allowed_micro;
                 }
+                double step_fraction = 1.0;
                 bool applied = false; /* cfg_act and Tcur already hold the corrected state */
-                if (fraction_one) {
-                    if (ln < D) real[ln] = x[ln] * dabs(scaling);
-                } else {
+                if (!fraction_one) {
                     apply_input<RT>(s, cfg_act, x, cfg_tmp, false, 0);
                     fk<RT>(s, cfg_tmp, Ttmp);
                     const double est = max_point_motion(s, Tcur, Ttmp);
-                    const double step_fraction = dmax(est / A.allowed_micro, 1.0);
-                    if (step_fraction == 1.0 && dabs(scaling) == 1.0) {
+                    step_fraction = dmax(est / A.allowed_micro, 1.0);
+                    applied = step_fraction == 1.0 && dabs(kScalingLds ? *scaling_p : scaling_reg) == 1.0;
+                    if (applied) {
                         /* real_correction_step = (x / 1) * 1 == x bit for bit (SPCS:1681-1682): the
                          * corrected configuration is cfg_tmp and its transforms are Ttmp */
                         if (ln < W) cfg_act[ln] = cfg_tmp[ln];
                         for (int e = ln; e < 12 * RDIM(R, L); e += kWave) Tcur[e] = Ttmp[e];
-                        applied = true;
-                    } else if (ln < D) {
-                        real[ln] = (x[ln] / step_fraction) * dabs(scaling);
+                        wsync();
                     }
                 }
-                wsync();
                 if (!applied) {
+                    if (ln < D) real[ln] = (x[ln] / step_fraction) * dabs(kScalingLds ? *scaling_p : scaling_reg);
+                    wsync();
                     apply_input<RT>(s, cfg_act, real, cfg_tmp, false, 0);
                     if (ln < W) cfg_act[ln] = cfg_tmp[ln];
                     wsync();
@@ -3014,11 +3023,18 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                     return 0;
                 }
                 if ((iters % A.S.resolve_correction_step_scaling_decay_iterations) == 0u) {
+                    double scaling = kScalingLds ? *scaling_p : scaling_reg;
                     if (scaling >= 0.0) {
                         scaling = scaling * A.S.resolve_correction_step_scaling_decay_rate;
                         if (scaling < A.S.resolve_correction_min_step_scaling) scaling = -A.S.resolve_correction_min_step_scaling;
                     } else {
                         scaling = -A.S.resolve_correction_min_step_scaling;
+                    }
+                    if (kScalingLds) {
+                        if (ln == 0) *scaling_p = scaling;
+                        wsync();
+                    } else {
+                        scaling_reg = scaling;
                     }
                 }
             }
