@@ -944,6 +944,43 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
             for (int k = 0; k < R.D; ++k) lever[k] = (k < nt) ? 1.0 + 1e-9 : rmax * (1.0 + 1e-9) + 1e-12;
         }
     }
+    /* the same bound over the geometries' local boxes (corner distance <= |centre| + |half
+     * extents|): the self-collision boxes are built from them */
+    std::vector<double> lever_box(std::max(1, R.D), HUGE_VAL);
+    if (d->robot_type == FKS_ROBOT_LINKED) {
+        for (int k = 0; k < R.D; ++k) {
+            const int jd = dof_joint[k];
+            if (joints[jd].type == FKS_JOINT_PRISMATIC) {
+                lever_box[k] = lever[k];
+                continue;
+            }
+            const double* ax = joints[jd].axis;
+            const double an = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+            double worst = 0.0;
+            bool ok = std::fabs(an - 1.0) < 1e-12;
+            for (int g = 0; g < G && ok; ++g) {
+                const int l = d->geometry_link[g];
+                if (!((link_mask[l] >> k) & 1ull)) continue;
+                const double* b = box.data() + 7 * (size_t)g;
+                if (b[6] == 0.0) {
+                    ok = false; /* no box (a point with w != 1): the box test never skips anyway */
+                    break;
+                }
+                double reach = 0.0;
+                for (int cur = l; cur != joints[jd].child;) {
+                    const JointDev& jp = joints[link_parent_joint[cur]];
+                    reach += std::sqrt(jp.origin[3] * jp.origin[3] + jp.origin[7] * jp.origin[7] + jp.origin[11] * jp.origin[11]);
+                    if (jp.type == FKS_JOINT_PRISMATIC)
+                        reach += std::max(std::fabs(jp.lo), std::fabs(jp.hi)) *
+                                 std::sqrt(jp.axis[0] * jp.axis[0] + jp.axis[1] * jp.axis[1] + jp.axis[2] * jp.axis[2]);
+                    cur = jp.parent;
+                }
+                worst = std::max(worst, reach + std::sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]) +
+                                            std::sqrt(b[3] * b[3] + b[4] * b[4] + b[5] * b[5]));
+            }
+            lever_box[k] = (ok && std::isfinite(worst)) ? worst * (1.0 + 1e-9) + 1e-12 : HUGE_VAL;
+        }
+    }
     std::vector<double> weights;
     if (d->robot_type == FKS_ROBOT_LINKED) {
         for (int k = 0; k < R.D; ++k) weights.push_back(d->distance_weights ? d->distance_weights[k] : 1.0);
@@ -996,6 +1033,8 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     HIP_TRY(ctx, up(&drounds, rounds.data(), rounds.size()));
     double* dlever = nullptr;
     HIP_TRY(ctx, up(&dlever, lever.data(), lever.size()));
+    double* dlever_box = nullptr;
+    HIP_TRY(ctx, up(&dlever_box, lever_box.data(), lever_box.size()));
     R.joints = dj;
     R.geom_link = dgl;
     R.geom_off = dgo;
@@ -1012,6 +1051,7 @@ fks_status fks_set_robot(fks_context* ctx, const fks_robot_desc* d) {
     R.weights = dw;
     R.rounds = drounds;
     R.dof_lever = dlever;
+    R.dof_lever_box = dlever_box;
     R.sampled_mask = 0;
     R.sampled = nullptr;
     if (d->sampled_actuators) {

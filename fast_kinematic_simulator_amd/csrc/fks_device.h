@@ -113,6 +113,9 @@ struct RobotDev {
      * unknown.  Lets the microstep-motion check of SPCS:1570-1575 be proven instead
      * of recomputed. */
     const double* dof_lever;
+    /* the same for every point of the geometries' local boxes (their corners reach past the
+     * points): bounds how far a self-collision box moves (the self-collision skip proof) */
+    const double* dof_lever_box;
     /* dofs whose actuator is a SampledUncertainVelocityActuator (bit d), their tables */
     uint64_t sampled_mask;
     const SampledDev* sampled;
@@ -134,7 +137,7 @@ constexpr int kThroughputWavesPerEU = 5;
 struct LdsLayout {
     uint32_t joints, ctrl, base, dofj, gbox, gpairs, rounds, shared_total;
     uint32_t rstate, noise, noise_err, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u,
-        ustep, x, real, axis_w, orig_w, colsq, hcoef, box, misc, ints, jm2, total;
+        ustep, x, real, axis_w, orig_w, colsq, hcoef, box, misc, ints, selfref, jm2, total;
     uint32_t fk_pair; /* 1: the free-motion microsteps pair their FK chains (jm2 allocated) */
     uint32_t lean;    /* 1: no rstate here: the skip-proof cache is ScratchLayout.rstate (lean kernels) */
 };
@@ -221,6 +224,11 @@ constexpr inline
     o += 40;
     l.ints = o; /* int32 region: perm[64], transpositions[64], 16 spare words */
     o += (2 * kMaxDofs + 16) / 2;
+    /* the self-collision skip proof's reference: the configuration of the last full box
+     * evaluation [D] and the boxes' smallest gap then (cells) [D]; a lean block keeps it in
+     * the wave's scratch (ScratchLayout.selfref) */
+    l.selfref = o;
+    if (!lean) o += (uint32_t)(D + 2) & ~1u;
     /* the second FK chain's joint motion matrices (paired FK of the next free microstep) */
     l.fk_pair = fk_pair ? 1u : 0u;
     l.jm2 = o;
@@ -246,7 +254,7 @@ constexpr inline
 
 /* per-wave scratch layout (doubles) */
 struct ScratchLayout {
-    uint64_t J, b, keys, corr, flag, cand, list, cellw, dense, rstate, pid, total;
+    uint64_t J, b, keys, corr, flag, cand, list, cellw, dense, rstate, pid, selfref, total;
 };
 constexpr inline
 #if defined(__HIPCC__)
@@ -277,6 +285,8 @@ constexpr inline
     o += (uint64_t)kRoundState * 64u;
     l.pid = o; /* the particle's controller state: error integral [dof], last error [64 + dof] */
     o += 2u * 64u;
+    l.selfref = o; /* a lean block's self-collision proof reference (LdsLayout.selfref) */
+    o += 66u;
     l.total = (o + 7) & ~7ull;
     return l;
 }

@@ -479,6 +479,7 @@ struct Sim {
     double pid_integral, pid_last; /* DOF lanes, SE(2) / SE(3) */
 #endif
     double* rstate;  /* the round skip-proof cache: LDS block, or scratch in the lean kernels */
+    double* selfref; /* the self-collision proof's reference (LdsLayout / ScratchLayout selfref) */
     bool self_nonempty;
     bool tcur_valid; /* Tcur == FK(particle configuration) from the end of the last step */
     uint32_t tr_steps, tr_cfgs; /* trace records produced so far (traced kernels) */
@@ -1534,11 +1535,30 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
                                                        uint32_t err, const double* Tp, const double* Tc);
 
 /* CollectSelfCollisions: returns whether the self-collision map is non-empty */
-__device__ FKS_SHAPE_INLINE bool self_collisions(Sim& s, const double* Tp, const double* Tc) {
+__device__ FKS_SHAPE_INLINE bool self_collisions(Sim& s, const double* Tp, const double* Tc, const double* q) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const int ln = s.lane();
     if (!RDIM(R, self_possible)) return false;
+#if defined(FKS_PROBE_NO_SELF)
+    return false; /* A/B probe only: what the self-collision check costs (results may change) */
+#endif
+    /* Skip proof (a cheaper route to the fast path's "no box pair overlaps").  At the last full
+     * evaluation, with configuration qref, every disallowed pair was separated along some axis
+     * by gap >= 1 cells.  Since then every point of every geometry's local box has moved by at
+     * most mu = sum_d |q_d - qref_d| * lever_box_d (joint motion along the straight path in
+     * joint space; wrapping and clamping only shorten it); the world AABB of a moved box lies in
+     * the old one grown by mu per side, the grid transform is rigid, and truncation moves each
+     * integer bound by at most mu / res + 2 cells.  So gap - 2 mu / res - 4 >= 1 keeps every
+     * pair apart: the fast path's answer (no self-collision) without building the boxes. */
+    double* ref = s.selfref;
+    const int D = RDIM(R, D);
+    const double gap = readfirstlane_f64(ref[D]);
+    if (gap >= 6.0) {
+        const double term = (ln < D) ? dabs(q[ln] - ref[ln]) * gp(R.dof_lever_box)[ln] : 0.0;
+        const double mu = bfly_sum(0.0 + term) * (1.0 + 1e-6) + 1e-12;
+        if (2.0 * mu * A.env_g.inv_res + 5.0 <= gap) return false;
+    }
     double* box = s.lds() + LAY(*s.A).box;
     bool bad = false;
     if (ln < RDIM(R, G)) {
@@ -1581,6 +1601,7 @@ __device__ FKS_SHAPE_INLINE bool self_collisions(Sim& s, const double* Tp, const
     }
     wsync();
     bool any = false;
+    double gmin = __builtin_huge_val();
     const uint32_t* lpairs = reinterpret_cast<const uint32_t*>(s.shared() + LAY(A).gpairs);
     for (int k = ln; k < RDIM(R, npairs); k += kWave) {
         int a, b;
@@ -1593,9 +1614,21 @@ __device__ FKS_SHAPE_INLINE bool self_collisions(Sim& s, const double* Tp, const
             b = gp(R.pairs)[2 * k + 1];
         }
         bool ov = true;
-        for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
+        double sep = -__builtin_huge_val(); /* the pair's largest separation over the axes (cells) */
+        for (int i = 0; i < 3; ++i) {
+            const double la = box[6 * a + i], ha = box[6 * a + 3 + i], lb = box[6 * b + i], hb = box[6 * b + 3 + i];
+            ov = ov && (la <= hb) && (lb <= ha);
+            sep = dmax(sep, dmax(lb - ha, la - hb));
+        }
         any = any || ov;
+        gmin = dmin(gmin, sep);
     }
+    /* the new reference: this configuration and the smallest separation (-inf if a box was not
+     * finite: no proof until the next full evaluation) */
+    const float gw = wave_min_f32(wave_any(bad) ? -__builtin_inff() : lower_f32(gmin));
+    if (ln < D) ref[ln] = q[ln];
+    if (ln == 0) ref[D] = (double)gw;
+    wsync();
     if (!wave_any(any || bad)) return false;
     const uint32_t r = self_collisions_exact(s.A, s.lds(), s.scratch, ln, s.err, Tp, Tc);
     s.err = r >> 1;
@@ -1770,14 +1803,14 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
 
 /* CheckCollision (SPCS:1418-1436) */
 template <int RT>
-__device__ FKS_SHAPE_INLINE bool check_collision(Sim& s, const double* Tp, const double* Tc) {
+__device__ FKS_SHAPE_INLINE bool check_collision(Sim& s, const double* Tp, const double* Tc, const double* q) {
     uint64_t t0 = tick();
     const bool env = env_collision(s, Tc);
     tock(s, FKS_PHASE_ENV_CHECK, t0);
     bool self = false;
     if constexpr (RT == FKS_ROBOT_LINKED) {
         t0 = tick();
-        self = self_collisions(s, Tp, Tc);
+        self = self_collisions(s, Tp, Tc, q);
         tock(s, FKS_PHASE_SELF_CHECK, t0);
     }
     s.self_nonempty = self;
@@ -2924,7 +2957,7 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                 fk<RT>(s, cfg, Tcur);
         }
         tock(s, FKS_PHASE_MICRO_FK, t0);
-        bool in_collision = check_collision<RT>(s, Tprev, Tcur);
+        bool in_collision = check_collision<RT>(s, Tprev, Tcur, cfg);
         if (s.err) return 1;
         if (in_collision) pair_ready = false; /* the resolver reuses cfg_tmp / Ttmp */
         trace_config<TR>(s, cfg, micro, FKS_TRACE_POST_ACTION);
@@ -3006,7 +3039,7 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                     fk<RT>(s, cfg_act, Tcur);
                 }
                 tock(s, FKS_PHASE_RESOLVE_APPLY, t0);
-                in_collision = check_collision<RT>(s, Tprev, Tcur);
+                in_collision = check_collision<RT>(s, Tprev, Tcur, cfg_act);
                 if (s.err) return 1;
                 trace_config<TR>(s, cfg_act, micro, FKS_TRACE_RESOLVER_STEP);
                 iters++;
@@ -3352,6 +3385,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
      * read): in the wave's LDS block, or in its scratch for a lean block (fixed per kernel, so
      * each instantiation addresses it with one kind of load) */
     s.rstate = LEAN ? s.scratch + SLAY(A).rstate : s.lds() + LAY(A).rstate;
+    s.selfref = LEAN ? s.scratch + SLAY(A).selfref : s.lds() + LAY(A).selfref;
     if (s.lane() < RDIM(R, nrounds)) s.rstate[kRoundState * s.lane() + 12] = kInvalidRound;
     wsync();
     const int ln = s.lane();
@@ -3461,6 +3495,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
         if (ln == 0) s.phase()[FKS_PHASE_PARTICLE] -= __builtin_amdgcn_s_memtime();
         s.self_nonempty = false;
         s.tcur_valid = false;
+        if (ln == 0) s.selfref[RDIM(R, D)] = -1.0; /* no self-collision proof reference for this particle yet */
         const double* start = A.starts + local * (uint64_t)W;
         const double* target = (A.num_targets == A.n) ? A.targets + local * (uint64_t)W : A.targets;
         bool collided = false;
