@@ -431,6 +431,9 @@ __device__ __forceinline__ uint32_t grid_brick(const GridDev& g, int32_t i, int3
 #else
 #define FKS_PID_REGS 1
 #endif
+#ifndef FKS_PAR_PROOF
+#define FKS_PAR_PROOF 1
+#endif
 /* the dynamic LDS of every kernel here: the workgroup's robot tables at offset 0, then one
  * block per wave (LdsLayout) */
 extern __shared__ __attribute__((aligned(16))) double fks_lds[];
@@ -1108,12 +1111,70 @@ __device__ __forceinline__ RoundDev lds_round(const Sim& s, int r) {
     return o;
 }
 
+/* the proof's verdict for one round from its motion bound bm (meters) and cached state st */
+__device__ __forceinline__ bool round_proof(const SimArgs& A, const double* st, double bm, bool still_if_floor, int what) {
+    const double b = bm * A.sdf_g.inv_res; /* cells */
+    const double K = 1.7320508075688773 * b + 3.0;
+    const double Sr = st[12] * A.sdf_g.inv_res;
+    const double lp = A.skip_lplus;
+    const bool inb = st[13] - b > 1e-6;
+    const bool same_cell = (b < st[14] - 1e-9) || (bm <= 1e-12 && still_if_floor);
+    if (what == kSkipCheck) return (inb && (Sr - A.skip_cmax) > (K - 1.0) * lp + 1e-9) || (same_cell && st[12] >= A.thr_env);
+    return (inb && (Sr - A.skip_cmax) > K * lp + 1e-9 && (Sr - K * lp) > 0.5 + 1.5 * lp + 1e-6) ||
+           (same_cell && Sr > A.skip_cmax + 1e-9 && Sr > 0.5 + 1.5 * lp + 1e-6);
+}
+
+/* skippable_rounds for robots of at most 8 rounds: eight lanes per round, each taking one or
+ * two of the twelve transform differences, summed inside the group by DPP (the same bound as
+ * rigid_motion_bound, in another order: a bound either way), so a round's proof costs a few
+ * instructions instead of the serial 3x4 difference on one lane */
+__device__ __forceinline__ uint64_t skippable_rounds8(Sim& s, const double* T, int what) {
+    const SimArgs& A = *s.A;
+    const RobotDev& R = A.R;
+    const int ln = s.lane();
+    const int r = ln >> 3, e = ln & 7;
+    const bool valid_r = r < RDIM(R, nrounds);
+    const RoundDev rd = lds_round(s, valid_r ? r : 0);
+    const double* st = s.rstate + kRoundState * (valid_r ? r : 0);
+    const bool usable = valid_r && rd.link >= 0 && st[12] > kInvalidRound;
+    const double* Tl = T + 12 * (rd.link >= 0 ? rd.link : 0);
+    /* lane e: rotation entry kRot[e] (lane 0 also the ninth), translation entry e < 3 */
+    const int ia = (e < 3) ? e : (e < 6 ? e + 1 : e + 2); /* 0 1 2 4 5 6 8 9 */
+    const double da = Tl[ia] - st[ia];
+    const double d9 = Tl[10] - st[10];
+    const int it = 4 * (e < 3 ? e : 0) + 3;
+    const double dt = Tl[it] - st[it];
+    double f = da * da;
+    if (e == 0) f = f + d9 * d9;
+    double t = (e < 3) ? dt * dt : 0.0;
+    f = f + dpp_f64<kDppXor1>(f);
+    t = t + dpp_f64<kDppXor1>(t);
+    f = f + dpp_f64<kDppXor2>(f);
+    t = t + dpp_f64<kDppXor2>(t);
+    f = f + dpp_f64<kDppHalfMirror>(f);
+    t = t + dpp_f64<kDppHalfMirror>(t);
+    const double bm = (sqrt_upper(t) + sqrt_upper(f) * rd.radius) * (1.0 + 1e-9) + 1e-12;
+    /* an unmoved link: every difference exactly zero in the group (only looked at when the
+     * bound is at its floor) */
+    const bool eq = (da == 0.0) && (e != 0 || d9 == 0.0) && (e >= 3 || dt == 0.0);
+    const uint64_t neq = __ballot(!eq);
+    const bool still = ((neq >> (8 * r)) & 0xffull) == 0ull;
+    const bool sk = usable && round_proof(A, st, bm, still, what);
+    const uint64_t m = __ballot(sk && e == 0) & 0x0101010101010101ull;
+    return (m * 0x0102040810204080ull) >> 56;
+}
+
 /* which rounds (bit r, r < 64) may skip the env check / the correction estimate at
  * transforms T; lane r evaluates round r */
 __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, int what) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     if (!A.skip_enabled) return 0ull;
+#if FKS_PAR_PROOF && defined(FKS_SHAPE_P) && FKS_SHAPE_TYPE == 0
+    /* linked-robot shape builds of at most 8 rounds (cfg3: wave time -2.4 %; the SE(3) shape of
+     * cfg4 ran 1.4 % slower with it, and generic builds keep one proof for every robot) */
+    if constexpr ((FKS_SHAPE_P + kWave - 1) / kWave <= 8) return skippable_rounds8(s, T, what);
+#endif
     bool sk = false;
     const int ln = s.lane();
     if (ln < RDIM(R, nrounds)) {
@@ -1292,7 +1353,14 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
 __device__ FKS_SHAPE_INLINE bool env_collision(Sim& s, const double* T) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
+#if defined(FKS_PROBE_PROOF_TWICE)
+    /* A/B probe only: the proof evaluated twice (same answer), to measure what one costs */
+    uint64_t skip = skippable_rounds(s, T, kSkipCheck);
+    asm volatile("" ::: "memory");
+    skip &= skippable_rounds(s, T, kSkipCheck) | skip;
+#else
     const uint64_t skip = skippable_rounds(s, T, kSkipCheck);
+#endif
     /* every round proven free (the common microstep): the reference reads 4 bytes per
      * point and finds nothing; account those reads without walking the rounds */
     if (RDIM(R, nrounds) <= kWave) {
