@@ -892,8 +892,8 @@ __device__ FKS_SHAPE_INLINE void apply_input(Sim& s, const double* cfg_in, const
             const double raw = cfg_in[ln] + real;
             double v;
             if (jd.type == FKS_JOINT_CONTINUOUS) {
-                v = fks_math::enforce_continuous_revolute_bounds(raw);
-                v = fks_math::enforce_continuous_revolute_bounds(v);
+                v = fks_math::wrap_revolute(raw);
+                v = fks_math::wrap_revolute(v);
             } else {
                 v = clamp(raw, jd.lo, jd.hi);
                 v = clamp(v, jd.lo, jd.hi);
@@ -908,7 +908,7 @@ __device__ FKS_SHAPE_INLINE void apply_input(Sim& s, const double* cfg_in, const
             double real = clamp(input[ln], -vmax, vmax);
             if (noisy) real = actuator_noisy(s, ct, ln, real, micro);
             double v = cfg_in[ln] + real;
-            if (ln == 2) v = fks_math::enforce_continuous_revolute_bounds(v);
+            if (ln == 2) v = fks_math::wrap_revolute(v);
             cfg_out[ln] = v;
         }
         wsync();
@@ -948,13 +948,13 @@ __device__ FKS_SHAPE_INLINE double control_action(Sim& s, const double* cfg, con
         if (ln < RDIM(R, D)) {
             const JointDev& jd = s.joints()[s.dofj()[ln]];
             if (jd.type == FKS_JOINT_CONTINUOUS)
-                err = fks_math::enforce_continuous_revolute_bounds(target[ln] - cfg[ln]);
+                err = fks_math::wrap_revolute(target[ln] - cfg[ln]);
             else
                 err = target[ln] - cfg[ln];
         }
     } else if constexpr (RT == FKS_ROBOT_SE2) {
         if (ln < 2) err = target[ln] - cfg[ln];
-        if (ln == 2) err = fks_math::enforce_continuous_revolute_bounds(target[2] - cfg[2]);
+        if (ln == 2) err = fks_math::wrap_revolute(target[2] - cfg[2]);
     } else {
         double P[12], Pi[12], Tg[12], Dm[12], tw[6];
         for (int k = 0; k < 12; ++k) {
@@ -992,7 +992,7 @@ __device__ FKS_SHAPE_INLINE double config_distance(Sim& s, const double* cfg, co
         double sum = 0.0;
         for (int k = 0; k < RDIM(R, D); ++k) {
             const JointDev& jd = s.joints()[s.dofj()[k]];
-            const double sd = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(target[k] - cfg[k])
+            const double sd = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::wrap_revolute(target[k] - cfg[k])
                                                                 : target[k] - cfg[k];
             const double d = gp(R.weights)[k] * dabs(sd);
             sum = sum + d * d;
@@ -1001,7 +1001,7 @@ __device__ FKS_SHAPE_INLINE double config_distance(Sim& s, const double* cfg, co
     } else if constexpr (RT == FKS_ROBOT_SE2) {
         const double dx = target[0] - cfg[0];
         const double dy = target[1] - cfg[1];
-        const double dr = fks_math::enforce_continuous_revolute_bounds(target[2] - cfg[2]);
+        const double dr = fks_math::wrap_revolute(target[2] - cfg[2]);
         return gp(R.weights)[0] * dsqrt(dx * dx + dy * dy) + gp(R.weights)[1] * dabs(dr);
     } else {
         double P[12], Pi[12], Tg[12], Dm[12], tw[6];
@@ -3217,11 +3217,11 @@ __device__ __forceinline__ void set_position(Sim& s, const double* src, double* 
     if constexpr (RT == FKS_ROBOT_LINKED) {
         if (ln < RDIM(s.A->R, D)) {
             const JointDev& jd = s.joints()[s.dofj()[ln]];
-            cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(src[ln])
+            cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::wrap_revolute(src[ln])
                                                         : clamp(src[ln], jd.lo, jd.hi);
         }
     } else if constexpr (RT == FKS_ROBOT_SE2) {
-        if (ln < 3) cfg[ln] = (ln == 2) ? fks_math::enforce_continuous_revolute_bounds(src[2]) : src[ln];
+        if (ln < 3) cfg[ln] = (ln == 2) ? fks_math::wrap_revolute(src[2]) : src[ln];
     } else {
         if (ln < 12) cfg[ln] = src[ln];
     }
@@ -3578,11 +3578,11 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             if constexpr (RT == FKS_ROBOT_LINKED) {
                 if (ln < D) {
                     const JointDev& jd = s.joints()[s.dofj()[ln]];
-                    cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::enforce_continuous_revolute_bounds(start[ln])
+                    cfg[ln] = (jd.type == FKS_JOINT_CONTINUOUS) ? fks_math::wrap_revolute(start[ln])
                                                                 : clamp(start[ln], jd.lo, jd.hi);
                 }
             } else if constexpr (RT == FKS_ROBOT_SE2) {
-                if (ln < 3) cfg[ln] = (ln == 2) ? fks_math::enforce_continuous_revolute_bounds(start[2]) : start[ln];
+                if (ln < 3) cfg[ln] = (ln == 2) ? fks_math::wrap_revolute(start[2]) : start[ln];
             } else {
                 if (ln < 12) cfg[ln] = start[ln];
             }
@@ -3874,7 +3874,7 @@ extern "C" __global__ void fks_math_probe(const double* a, const double* b, doub
     out[8 * i + 3] = fks_math::atan2(x, y);
     out[8 * i + 4] = fks_math::dsqrt(fks_math::dabs(y));
     out[8 * i + 5] = x / y;
-    out[8 * i + 6] = fks_math::enforce_continuous_revolute_bounds(x);
+    out[8 * i + 6] = fks_math::wrap_revolute(x);
     out[8 * i + 7] = (x * y + x) * y - x * x;
 }
 #endif

@@ -365,6 +365,38 @@ FKS_HD inline double atan2(double y, double x) {
     }
 }
 
+/* fmod(x, 2*pi) without a libm call, for the kernel's continuous-joint wrap: binary long
+ * division of |x| by 2*pi.  Each step subtracts s = 2*pi*2^m with s <= r < 2*s, which is exact
+ * (Sterbenz), so the result is the exact remainder fmod returns, with the sign of x; a
+ * non-finite x gives the quiet NaN.  At most one step per binade of |x| / (2*pi).  Pinned
+ * against glibc's fmod by tests/test_portable_math.py. */
+FKS_HD inline double fmod_two_pi(double x) {
+    const double y = 2.0 * 3.14159265358979323846;
+    const uint64_t yb = bits(y);
+    double r = dabs(x);
+    if (!(r <= 1.7976931348623157e308)) return from_bits(0x7ff8000000000000ull);
+    while (r >= y) {
+        const uint64_t shift = (uint64_t)((hi_word(r) >> 20) - (uint32_t)(yb >> 52)) << 52;
+        double s = from_bits(yb + shift);
+        if (s > r) s = from_bits(yb + shift - (1ull << 52));
+        r = r - s;
+    }
+    return from_bits(bits(r) | (bits(x) & 0x8000000000000000ull));
+}
+
+/* the same wrap as enforce_continuous_revolute_bounds below, through fmod_two_pi: the kernel's
+ * form (ocml's fmod is a large inlined loop that costs the hot loops registers) */
+FKS_HD inline double wrap_revolute(double value) {
+    const double kPi = 3.14159265358979323846;
+    if ((value <= -kPi) || (value > kPi)) {
+        const double remainder = fmod_two_pi(value);
+        if (remainder <= -kPi) return remainder + (2.0 * kPi);
+        if (remainder > kPi) return remainder - (2.0 * kPi);
+        return remainder;
+    }
+    return value;
+}
+
 /* arc_utilities EigenHelpers::EnforceContinuousRevoluteBounds restated:
  * wrap into (-pi, pi]; fmod is exact on both glibc and ocml. */
 FKS_HD inline double enforce_continuous_revolute_bounds(double value) {

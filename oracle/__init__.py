@@ -354,7 +354,8 @@ def se3_log(pose):
 
 
 def portable_math(fn, x, y=None):
-    """fn: 0 sin, 1 cos, 2 log, 3 atan, 4 atan2(x, y), 5 wrap (include/fks_portable_math.h)."""
+    """fn: 0 sin, 1 cos, 2 log, 3 atan, 4 atan2(x, y), 5 wrap, 6 fmod_two_pi, 7 wrap_revolute
+    (include/fks_portable_math.h)."""
     x = np.ascontiguousarray(x, dtype=np.float64)
     y = np.ascontiguousarray(y if y is not None else np.zeros_like(x), dtype=np.float64)
     o = np.zeros_like(x)

@@ -1330,7 +1330,8 @@ int oracle_max_threads(void) { return omp_get_max_threads(); }
 
 extern "C" {
 /* evaluate the shared portable libm (include/fks_portable_math.h) for tests:
- * fn 0 sin, 1 cos, 2 log, 3 atan, 4 atan2(x, y), 5 wrap */
+ * fn 0 sin, 1 cos, 2 log, 3 atan, 4 atan2(x, y), 5 wrap, 6 fmod_two_pi and 7 wrap_revolute
+ * (the kernel's libm-free wrap, checked against 5 and glibc) */
 void oracle_portable_math(int32_t fn, const double* x, const double* y, uint64_t n, double* out) {
     for (uint64_t i = 0; i < n; ++i) {
         switch (fn) {
@@ -1339,6 +1340,8 @@ void oracle_portable_math(int32_t fn, const double* x, const double* y, uint64_t
             case 2: out[i] = fks_math::log(x[i]); break;
             case 3: out[i] = fks_math::atan(x[i]); break;
             case 4: out[i] = fks_math::atan2(x[i], y[i]); break;
+            case 6: out[i] = fks_math::fmod_two_pi(x[i]); break;
+            case 7: out[i] = fks_math::wrap_revolute(x[i]); break;
             default: out[i] = fks_math::enforce_continuous_revolute_bounds(x[i]); break;
         }
     }

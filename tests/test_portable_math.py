@@ -63,3 +63,24 @@ def test_continuous_wrap(oracle_lib):
     assert np.all(w <= math.pi) and np.all(w > -math.pi)
     assert w[1] == math.pi and w[2] == math.pi
     assert np.allclose(np.cos(w), np.cos(x)) and np.allclose(np.sin(w), np.sin(x))
+
+
+def test_fmod_two_pi_matches_glibc_bit_for_bit(oracle_lib):
+    """fks_math::fmod_two_pi (the kernel's continuous-joint wrap, no libm call) returns glibc's
+    fmod(x, 2*pi) bit for bit, over every binade and at the multiples of 2*pi; wrap_revolute
+    equals enforce_continuous_revolute_bounds."""
+    import oracle
+
+    rng = np.random.default_rng(6)
+    two_pi = 2.0 * math.pi
+    x = rng.uniform(-1, 1, 400000) * 10.0 ** rng.uniform(-3, 20, 400000)
+    k = rng.integers(-10**6, 10**6, 20000).astype(np.float64)
+    near = np.concatenate([k * two_pi, np.nextafter(k * two_pi, np.inf), np.nextafter(k * two_pi, -np.inf)])
+    edge = np.array([0.0, -0.0, two_pi, -two_pi, math.pi, -math.pi, 1e308, -1e308, 5e-324,
+                     np.finfo(float).max, -np.finfo(float).max, 2.0**53, 3 * two_pi])
+    x = np.concatenate([x, near, edge, rng.uniform(-1e300, 1e300, 2000)])
+    got = oracle.portable_math(6, x)
+    want = np.fmod(x, two_pi)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+    assert np.array_equal(oracle.portable_math(7, x).view(np.uint64), oracle.portable_math(5, x).view(np.uint64))
+    assert np.isnan(oracle.portable_math(6, np.array([np.inf, -np.inf, np.nan]))).all()
