@@ -1837,7 +1837,7 @@ fks_status fks_selftest_math(int32_t device, uint64_t n, uint64_t* out_mismatche
         host[8 * i + 3] = fks_math::atan2(x, y);
         host[8 * i + 4] = fks_math::dsqrt(fks_math::dabs(y));
         host[8 * i + 5] = x / y;
-        host[8 * i + 6] = fks_math::enforce_continuous_revolute_bounds(x);
+        host[8 * i + 6] = fks_math::enforce_continuous_revolute_bounds(x / y); /* glibc fmod vs the kernel's wrap */
         host[8 * i + 7] = (x * y + x) * y - x * x;
     }
     double *da = nullptr, *db = nullptr, *dout = nullptr;

@@ -3874,7 +3874,7 @@ extern "C" __global__ void fks_math_probe(const double* a, const double* b, doub
     out[8 * i + 3] = fks_math::atan2(x, y);
     out[8 * i + 4] = fks_math::dsqrt(fks_math::dabs(y));
     out[8 * i + 5] = x / y;
-    out[8 * i + 6] = fks_math::wrap_revolute(x);
+    out[8 * i + 6] = fks_math::wrap_revolute(x / y); /* |x / y| from 1e-7 to beyond 1e9: the long division's every length */
     out[8 * i + 7] = (x * y + x) * y - x * x;
 }
 #endif
