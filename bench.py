@@ -150,17 +150,48 @@ def config_check_bench(sim, wl, dev, n=1 << 20, reps=3, cpu_sample=16384, thread
     return out
 
 
-def load_traffic():
+def kernel_name(kind: str, robot_type: int, spec) -> str:
+    """The simulation kernel the last timed launch ran (fks_get_launch_info's last_kernel),
+    not the one the flags asked for."""
+    if kind == "shaped":
+        return "fks_simulate_shaped (" + (spec["shape"] if spec else "?") + ")"
+    base = KERNELS.get(robot_type, "fks_simulate")
+    return {"throughput": base, "small_batch": base + "_small"}.get(kind, f"{base} ({kind})")
+
+
+def kernel_source_sha16() -> str:
+    """The hash tools/profile_pmc.py records: the kernel source and the headers it includes."""
+    import hashlib
+
+    from fast_kinematic_simulator_amd import build
+
+    h = hashlib.sha256()
+    for name, rel in build.EMBEDDED:
+        h.update(name.encode() + b"\0")
+        with open(os.path.join(build.PKG, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def load_traffic(kernel: str):
     """HBM bytes per launch of the simulation kernel and the L2 hit rate from the committed
     rocprofv3 PMC summary (profiles/latest_pmc.json, written by tools/profile_pmc.py from
     separate FETCH_SIZE / WRITE_SIZE / TCC_HIT+MISS passes of this bench), or Nones.  It is
-    the builder's profile of the same command, not a measurement of this run."""
+    the builder's profile of the same command, not a measurement of this run, so it is used
+    only when the profile names the kernel (and shape) this run's timed launches ran."""
     path = os.path.join(ROOT, "profiles", "latest_pmc.json")
     if not os.path.exists(path):
         return None, None, None
     try:
         with open(path) as f:
             d = json.load(f)
+        if d.get("kernel") != kernel:
+            return None, None, (f"profiles/latest_pmc.json profiles {d.get('kernel')!r}, this run ran {kernel!r}: "
+                                "traffic not quoted")
+        sha = kernel_source_sha16()
+        if d.get("kernel_source_sha16") != sha:
+            return None, None, (f"profiles/latest_pmc.json profiles kernel sources {d.get('kernel_source_sha16')}, this tree's "
+                                f"are {sha}: traffic not quoted")
         src = d.get("source", "profiles/latest_pmc.json")
         if d.get("note"):
             src = src + "; " + d["note"]
@@ -195,6 +226,8 @@ def main():
                          "ForwardSimulateRobots call gets it; no launcher, no collective")
     ap.add_argument("--devices", default=None, help="--in-process: comma-separated device ids (default 0..gpus-1; "
                                                       "a device may repeat)")
+    ap.add_argument("--no-projection", action="store_true",
+                    help="skip the strong-scaling projection (the batch's 2/4/8-way shards timed alone on this GPU)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous / shard / gather check without a GPU (gloo): no simulation, value null")
     args = ap.parse_args()
@@ -262,6 +295,10 @@ def main():
         log(f"[rank {rank}] shape-specialised kernel {spec['shape']}: "
             + (f"compiled in {spec['compile_seconds']:.1f}s" if not spec["from_cache"] else "from the kernel cache")
             + f" ({time.perf_counter() - t0:.1f}s setup)")
+    else:
+        # the library specialises by default (lazily, at the first throughput launch): the
+        # generic-kernel A/B leg has to switch it off, or it would time the shaped kernel
+        sim.set_specialization(False)
     Wd = wl.robot.config_width
     dev = torch.device("cuda", local_rank)
     starts = torch.from_numpy(np.ascontiguousarray(wl.starts[lo:lo + n_local])).to(dev)
@@ -311,6 +348,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     kernel_ms = [a.elapsed_time(b) for a, b in events]
+    ran_kernel = sim.launch_info()["last_kernel"]  # what the last timed launch actually ran
     tot = sim.total_counters()
     spec_launches = (sim.specialization()["launches"] - spec_before) if spec else 0
     phases = sim.phase_cycles(total=True)
@@ -338,7 +376,8 @@ def main():
         avg_kernel_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3
         bytes_per_launch = tot["sdf_bytes"] / calls
         achieved = bytes_per_launch / avg_kernel_s / 1e9
-        traffic, l2_hit, traffic_src = load_traffic() if args.workload == "cfg3" else (None, None, None)  # cfg3 profile
+        traffic, l2_hit, traffic_src = (load_traffic(kernel_name(ran_kernel, wl.robot.robot_type, spec))
+                                        if args.workload == "cfg3" else (None, None, None))  # cfg3 profile
         per_launch = {k: tot[k] / calls for k in ("microsteps", "controller_steps", "resolver_iterations", "least_squares_rows")}
         flops = fp64_algorithmic_flops(wl.robot, per_launch)
         cpu = None
@@ -366,6 +405,14 @@ def main():
                 pipe = {"value": None, "error": f"{type(e).__name__}: {e}"}
         if pipe and pipe.get("value"):
             log(f"pipelined: {pipe['value']:.4e} {UNIT}, {pipe['ms_per_batch']:.1f} ms per batch, identical={pipe['identical_to_sequential']}")
+        proj = None
+        if world == 1 and not args.no_contacts and not args.no_projection:
+            try:
+                proj = strong_scaling_projection(sim, wl, dev, n_local, lo)
+                log("strong-scaling projection: " + ", ".join(f"{r['devices']} dev {r['slowest_shard_ms']:.1f} ms "
+                                                               f"(x{r['projected_speedup']:.2f})" for r in proj["rows"]))
+            except Exception as e:  # a side figure: never costs the headline line
+                proj = {"error": f"{type(e).__name__}: {e}"}
         cc = None
         if not args.no_config_check and args.workload == "cfg3":
             if not args.no_cpu_baseline:
@@ -410,7 +457,8 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "l2_hit_rate": l2_hit,
-                "kernel": ("fks_simulate_shaped (" + spec["shape"] + ")") if spec else KERNELS[wl.robot.robot_type],
+                "kernel": kernel_name(ran_kernel, wl.robot.robot_type, spec),
+                "kernel_kind": ran_kernel,
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 # second entry: the kernel is FP64-VALU- and latency-bound, not HBM-bound
@@ -432,6 +480,8 @@ def main():
             "config_check": cc,
             "pcie_inclusive": pcie,
             "pipelined": pipe,
+            # a fixed batch split over G devices, each shard timed alone on this GPU
+            "strong_scaling_projection": proj,
             # share of wave time per phase of the hot path (s_memtime cycle sums, rank 0)
             # (only in profiling builds of the library: -DFKS_PHASE_TIMERS=1, see tools/variant_bench.py)
             "kernel_phases": ({k: (v if k in PHASE_COUNTS else round(v / max(1, phases["particle"]), 4))
@@ -462,8 +512,8 @@ def pipelined_batches(sim, denv, wl, dev, starts, targets, n, first_id, batches)
 
     sim2 = make_linked_simulator(denv, wl.solver, wl.controller_frequency, wl.seed, device=dev.index)
     sim2.set_robot(wl.robot)
-    if sim.specialization()["active"]:
-        sim2.set_specialization(True)  # the process cache holds the code object
+    # the same kernel as the first context (the process cache holds the shaped code object)
+    sim2.set_specialization(bool(sim.specialization()["active"]))
     sims = (sim, sim2)
     streams = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
     W = wl.robot.config_width
@@ -511,6 +561,52 @@ def pipelined_batches(sim, denv, wl, dev, starts, targets, n, first_id, batches)
             "contexts": 2, "streams": 2, "identical_to_sequential": same,
             "note": "throughput of back-to-back batches whose tails overlap the next batch's start (two contexts, two "
                     "streams, fks_forward_simulate_device without synchronisation); `value` above is the one-stream figure"}
+
+
+def strong_scaling_projection(sim, wl, dev, n, first_id=0, groups=(1, 2, 4, 8), call_index=0):
+    """What one GPU can say about strong scaling a fixed batch (the planner's regime: one
+    ForwardSimulateRobots call of n particles, SPCS:795-802) over G devices: the batch split as
+    fks_shard_bounds splits it, every shard run alone on this GPU with its own first particle
+    id (so each shard's particles are exactly those of the whole batch, the same trajectories),
+    and the projected time on G devices = the slowest shard's kernel time.  speedup = T(n) /
+    that.  A projection, not a measurement: it leaves out the per-device host staging and any
+    interference between devices, and no multi-GPU run backs it."""
+    import numpy as np
+    import torch
+
+    from fast_kinematic_simulator_amd.sharding import shard_bounds
+
+    W = wl.robot.config_width
+    d_starts = torch.from_numpy(np.ascontiguousarray(wl.starts[first_id:first_id + n])).to(dev)
+    d_targets = torch.from_numpy(np.ascontiguousarray(wl.targets)).to(dev)
+    out = torch.empty((n, W), dtype=torch.float64, device=dev)
+    micro = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def shard_ms(lo, hi):
+        k = hi - lo
+        sim.set_call_index(call_index)
+        sim.forward_simulate_device(wl.robot, d_starts[lo:].data_ptr(), k, d_targets.data_ptr(), 1, first_id + lo, True,
+                                    out[lo:].data_ptr(), d_out_microsteps=micro[lo:].data_ptr(), synchronize=True)
+        return sim.last_call_counters()["kernel_ms"], sim.launch_info()["last_kernel"]
+
+    rows = []
+    t1 = None
+    for G in groups:
+        times, kinds = [], set()
+        for g in range(G):
+            lo, hi = shard_bounds(n, G, g)
+            ms, kind = shard_ms(lo, hi)
+            times.append(ms)
+            kinds.add(kind)
+        t = max(times)
+        if G == 1:
+            t1 = t
+        rows.append({"devices": G, "particles_per_device": n // G, "slowest_shard_ms": t, "mean_shard_ms": sum(times) / G,
+                     "projected_speedup": t1 / t, "projected_efficiency": t1 / t / G, "kernels": sorted(kinds)})
+    return {"particles": n, "rows": rows,
+            "note": "each shard of the batch run alone on one GPU (same particle ids, same trajectories); projected time on G "
+                    "devices = the slowest shard's kernel time; excludes host staging and inter-device effects; no multi-GPU "
+                    "run measured it"}
 
 
 def in_process(args) -> int:
@@ -565,6 +661,17 @@ def in_process(args) -> int:
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     bytes_per_device_launch = totals["sdf_bytes"] / totals["calls"] / ndev
     achieved = bytes_per_device_launch / avg_kernel_s / 1e9
+    proj = None
+    if not args.no_projection and not args.no_contacts:
+        # the planner's fixed batch of one device's size, split as the multi-device path would
+        # split it, every shard timed alone on devices[0]
+        from fast_kinematic_simulator_amd import make_linked_simulator
+
+        one = make_linked_simulator(henv, wl.solver, wl.controller_frequency, wl.seed, device=devices[0])
+        one.set_robot(wl.robot)
+        one.set_specialization(True)
+        proj = strong_scaling_projection(one, wl, torch.device("cuda", devices[0]), n_total // ndev, 0)
+        one.close()
     cpu = None
     if not args.no_cpu_baseline:
         sample = min(args.cpu_sample, n_total)
@@ -592,6 +699,8 @@ def in_process(args) -> int:
                      "note": "per device: algorithmic bytes of one shard's launch / the slowest shard's kernel time"},
         "statistics": sim.get_statistics(),
         "cpu_baseline": cpu,
+        "strong_scaling_projection": proj,
+        "active_devices": sim.active_devices(),
     }
     print(json.dumps(line), flush=True)
     sim.close()

@@ -172,8 +172,11 @@ class CallCounters(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+SPECIALIZE_OFF, SPECIALIZE_ON, SPECIALIZE_NO_PROOFS = 0, 1, 2  # fks_specialization_mode (ABI 9)
+
+
 class SpecializationInfo(ctypes.Structure):
-    """fks_specialization_info (ABI 8)"""
+    """fks_specialization_info (ABI 9)"""
     _fields_ = [
         ("enabled", c_int32),
         ("active", c_int32),
@@ -182,11 +185,15 @@ class SpecializationInfo(ctypes.Structure):
         ("compile_seconds", c_double),
         ("launches", c_uint64),
         ("shape", ctypes.c_char * 64),
+        ("failed", c_int32),
+        ("reserved", c_int32),
+        ("message", ctypes.c_char * 512),
     ]
 
     def as_dict(self):
-        d = {name: getattr(self, name) for name, _ in self._fields_ if name not in ("reserved", "shape")}
+        d = {name: getattr(self, name) for name, _ in self._fields_ if name not in ("reserved", "shape", "message")}
         d["shape"] = self.shape.decode()
+        d["message"] = self.message.decode(errors="replace")
         return d
 
 
@@ -351,6 +358,8 @@ PROTOTYPES = [
     ("fks_multi_reset_statistics", c_int32, [c_void_p]),
     ("fks_multi_get_last_call_counters", c_int32, [c_void_p, POINTER(CallCounters)]),
     ("fks_multi_set_call_index", c_int32, [c_void_p, c_uint64]),
+    ("fks_multi_set_active_devices", c_int32, [c_void_p, c_int32]),
+    ("fks_multi_active_devices", c_int32, [c_void_p]),
     ("fks_multi_check_config_collision", c_int32, [c_void_p, POINTER(c_double), c_uint64, c_double, POINTER(c_uint8), POINTER(c_uint32)]),
     ("fks_device_count", c_int32, []),
 ]

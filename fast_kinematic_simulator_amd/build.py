@@ -56,11 +56,21 @@ def write_embedded_sources(directory: str = GENERATED, defines=()) -> str:
     return out
 
 
+def generated_dir(output: str) -> str:
+    """Where the embedded-sources include of the library at `output` is written: the product's
+    under build/generated, each variant's in a directory of its own (concurrent variant builds
+    must not embed each other's defines)."""
+    if os.path.basename(output) in ("libfks_hip.so", "libfks_hip.so.tmp"):
+        return GENERATED
+    return os.path.join(GENERATED, "variant-" + os.path.basename(output).replace(".tmp", ""))
+
+
 def build_command(output: str, defines=(), flags=()) -> list:
-    write_embedded_sources(defines=defines)
+    gen = generated_dir(output)
+    write_embedded_sources(gen, defines=defines)
     return [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
             *[f"-D{d}" for d in defines], *flags,
-            f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(PKG, 'csrc')}", f"-I{GENERATED}", "-x", "hip",
+            f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(PKG, 'csrc')}", f"-I{gen}", "-x", "hip",
             *[os.path.join(PKG, s) for s in SOURCES], "-o", output]
 
 
@@ -109,7 +119,10 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
 def build_variant(output: str, defines=(), flags=()) -> str:
     """Build a tuning or diagnostic variant (e.g. FKS_WAVES_PER_EU=3, FKS_PHASE_TIMERS=1, or
     extra compiler flags) to a separate path; load it with FKS_LIB_PATH=<output> and
-    FKS_VARIANT_LIB=1 (tools/variant_bench.py).  A variant never takes the product's name."""
+    FKS_VARIANT_LIB=1 (tools/variant_bench.py).  A variant never takes the product's name.
+    Its defines reach its shape-specialised kernels (they are prepended to the embedded kernel
+    source, and a source-defined FKS_WAVES_PER_EU wins over the layout's budget); extra
+    `flags` do not (hiprtc compiles with the library's fixed options)."""
     output = os.path.abspath(output)
     if os.path.basename(output) == "libfks_hip.so":
         raise ValueError("a build variant must not be named libfks_hip.so (the product library)")

@@ -293,6 +293,8 @@ struct fks_context {
     double spec_seconds = 0.0;
     int32_t spec_from_cache = 0;
     uint64_t spec_launches = 0;
+    bool spec_failed = false;  /* the current robot's build failed (its calls run the generic kernel) */
+    std::string spec_message;  /* why (fks_specialization_info.message) */
 };
 
 template <typename T>
@@ -356,14 +358,31 @@ static void spec_release(fks_context* ctx) {
     ctx->spec_seconds = 0.0;
     ctx->spec_from_cache = 0;
     ctx->spec_launches = 0;
+    ctx->spec_failed = false;
+    ctx->spec_message.clear();
 }
+
+static fks_status spec_build(fks_context* ctx);
 
 /* the shape-specialised throughput kernel of the current robot: compiled (or taken from a
  * cache), loaded on the context's device, and used only if it keeps the generic kernel's
- * occupancy (the persistent grid is sized for that) */
+ * occupancy (the persistent grid is sized for that).  A failure leaves the generic kernel
+ * in place and is recorded (fks_specialization_info.failed / message) */
 static fks_status spec_prepare(fks_context* ctx) {
     spec_release(ctx);
     if (!ctx->specialize || !ctx->has_robot) return FKS_OK;
+    const fks_status st = spec_build(ctx);
+    if (st != FKS_OK) {
+        ctx->spec_failed = true;
+        ctx->spec_message = ctx->last_error;
+        /* a failed module load can leave the runtime's per-thread error set; the generic
+         * launch that follows checks hipGetLastError and must not pick it up */
+        (void)hipGetLastError();
+    }
+    return st;
+}
+
+static fks_status spec_build(fks_context* ctx) {
     fks_spec::Shape sh;
     sh.type = ctx->R.type;
     sh.L = ctx->R.L;
@@ -374,6 +393,7 @@ static fks_status spec_prepare(fks_context* ctx) {
     sh.P = ctx->R.P;
     sh.pair = ctx->fk_pair ? 1 : 0;
     sh.lean = ctx->lean ? 1 : 0;
+    sh.no_proofs = ctx->specialize == FKS_SPECIALIZE_NO_PROOFS ? 1 : 0;
     /* the waves a SIMD holds at this layout (4 SIMDs per CU): when the LDS block keeps fewer
      * resident than the register budget allows (cfg5's lean blocks: 16 per CU), the
      * specialised kernel is compiled for that many and may use their registers */
@@ -387,13 +407,22 @@ static fks_status spec_prepare(fks_context* ctx) {
         else if (n >= per_simd && n <= 8) sh.waves_per_eu = n;
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    ctx->spec_shape = fks_spec::shape_key(sh); /* named in the report even when the build fails */
     std::string log;
     bool compiled = false;
-    const std::shared_ptr<const fks_spec::CodeObject> co = fks_spec::code_object(sh, &log, &compiled);
+    std::shared_ptr<const fks_spec::CodeObject> co = fks_spec::code_object(sh, &log, &compiled);
     if (!co) return fail(ctx, FKS_ERR_UNSUPPORTED, "shape specialisation: " + log);
     hipModule_t m = nullptr;
     hipFunction_t f = nullptr;
     hipError_t e = hipModuleLoadData(&m, co->bytes.data());
+    if (e != hipSuccess && !compiled) {
+        /* a cached code object the runtime refuses (truncated, or from another toolchain):
+         * dropped from both caches and compiled afresh, once */
+        (void)hipGetLastError();
+        co = fks_spec::code_object(sh, &log, &compiled, /*refresh=*/true);
+        if (!co) return fail(ctx, FKS_ERR_UNSUPPORTED, "shape specialisation (after an unloadable cached code object): " + log);
+        e = hipModuleLoadData(&m, co->bytes.data());
+    }
     if (e != hipSuccess) return hip_fail(ctx, e, "hipModuleLoadData (shape-specialised kernel)");
     e = hipModuleGetFunction(&f, m, "fks_simulate_shaped");
     if (e != hipSuccess) {
@@ -1770,12 +1799,12 @@ fks_status fks_set_individual_jacobians(fks_context* ctx, int32_t simulate_with_
     return FKS_OK;
 }
 
-fks_status fks_set_specialization(fks_context* ctx, int32_t enabled) {
-    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+fks_status fks_set_specialization(fks_context* ctx, int32_t mode) {
+    if (!ctx || mode < FKS_SPECIALIZE_OFF || mode > FKS_SPECIALIZE_NO_PROOFS) return FKS_ERR_INVALID_ARGUMENT;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     fks_status st = settle(ctx);
     if (st != FKS_OK) return st;
-    ctx->specialize = enabled ? 1 : 0;
+    ctx->specialize = mode;
     ctx->spec_pending = false;
     return spec_prepare(ctx); /* now, for the current robot (releases it when disabled) */
 }
@@ -1790,6 +1819,8 @@ fks_status fks_get_specialization(const fks_context* ctx, fks_specialization_inf
     out->compile_seconds = ctx->spec_seconds;
     out->launches = ctx->spec_launches;
     std::snprintf(out->shape, sizeof(out->shape), "%s", ctx->spec_shape.c_str());
+    out->failed = ctx->spec_failed ? 1 : 0;
+    std::snprintf(out->message, sizeof(out->message), "%s", ctx->spec_message.c_str());
     return FKS_OK;
 }
 

@@ -434,6 +434,16 @@ __device__ __forceinline__ uint32_t grid_brick(const GridDev& g, int32_t i, int3
 #ifndef FKS_PAR_PROOF
 #define FKS_PAR_PROOF 1
 #endif
+/* FKS_NO_SKIP_PROOFS (validation builds only: fks_set_specialization(ctx,
+ * FKS_SPECIALIZE_NO_PROOFS), tests/test_proof_free.py): every shortcut that rests on a cached
+ * state and a floating-point margin is compiled out, so each check is evaluated as the
+ * reference evaluates it — the environment / correction round proofs (skippable_rounds), the
+ * motion estimate's round pruning (max_point_motion), the self-collision gap proof
+ * (self_collisions) and the two lever-arm shortcuts of the resolver (resolve_step).  The
+ * product's results must equal this build's on every particle, byte for byte. */
+#ifndef FKS_NO_SKIP_PROOFS
+#define FKS_NO_SKIP_PROOFS 0
+#endif
 /* the dynamic LDS of every kernel here: the workgroup's robot tables at offset 0, then one
  * block per wave (LdsLayout) */
 extern __shared__ __attribute__((aligned(16))) double fks_lds[];
@@ -1169,7 +1179,7 @@ __device__ __forceinline__ uint64_t skippable_rounds8(Sim& s, const double* T, i
 __device__ __forceinline__ uint64_t skippable_rounds(Sim& s, const double* T, int what) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
-    if (!A.skip_enabled) return 0ull;
+    if (FKS_NO_SKIP_PROOFS || !A.skip_enabled) return 0ull;
 #if FKS_PAR_PROOF && defined(FKS_SHAPE_P) && FKS_SHAPE_TYPE == 0
     /* linked-robot shape builds of at most 8 rounds (cfg3: wave time -2.4 %; the SE(3) shape of
      * cfg4 ran 1.4 % slower with it, and generic builds keep one proof for every robot) */
@@ -1270,7 +1280,7 @@ __device__ FKS_SHAPE_INLINE double max_point_motion(Sim& s, const double* TA, co
     const int ln = s.lane();
     const int nr = RDIM(R, nrounds);
     double m = 0.0;
-    if (nr <= 2 || nr > kWave) {
+    if (FKS_NO_SKIP_PROOFS || nr <= 2 || nr > kWave) {
 #pragma unroll 2
         for (int r = 0; r < nr; ++r) {
             const double sq = round_max_motion(R, TA, TB, r, ln);
@@ -1622,7 +1632,7 @@ __device__ FKS_SHAPE_INLINE bool self_collisions(Sim& s, const double* Tp, const
     double* ref = s.selfref;
     const int D = RDIM(R, D);
     const double gap = readfirstlane_f64(ref[D]);
-    if (gap >= 6.0) {
+    if (!FKS_NO_SKIP_PROOFS && gap >= 6.0) {
         const double term = (ln < D) ? dabs(q[ln] - ref[ln]) * gp(R.dof_lever_box)[ln] : 0.0;
         const double mu = bfly_sum(0.0 + term) * (1.0 + 1e-6) + 1e-12;
         if (2.0 * mu * A.env_g.inv_res + 5.0 <= gap) return false;
@@ -2941,7 +2951,7 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
          * translation and max |p| for rotation components; +inf where no bound holds */
         const double term = (ln < D) ? dabs(ustep[ln]) * gp(R.dof_lever)[ln] : 0.0;
         const double bound = bfly_sum(0.0 + term);
-        proven = bound * (1.0 + 1e-6) + 1e-12 < A.allowed_micro;
+        proven = !FKS_NO_SKIP_PROOFS && bound * (1.0 + 1e-6) + 1e-12 < A.allowed_micro;
     }
     if (!proven) {
         apply_input<RT>(s, cfg, ustep, cfg_tmp, false, 0);
@@ -3080,7 +3090,7 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                 bool fraction_one;
                 {
                     const double term = (ln < D) ? dabs(x[ln]) * gp(R.dof_lever)[ln] : 0.0;
-                    fraction_one = bfly_sum(0.0 + term) * (1.0 + 1e-6) + 1e-12 < A.allowed_micro;
+                    fraction_one = !FKS_NO_SKIP_PROOFS && bfly_sum(0.0 + term) * (1.0 + 1e-6) + 1e-12 < A.allowed_micro;
                 }
                 double step_fraction = 1.0;
                 bool applied = false; /* cfg_act and Tcur already hold the corrected state */

@@ -14,6 +14,12 @@
  * which is where the planner consumes them; the statistics and call counters are
  * summed over the devices (kernel_ms is the slowest device's).  Device-resident
  * multi-process use (one rank per GPU, RCCL gather) is bench.py / sharding.py.
+ *
+ * Host side of a call: one std::thread per active device runs that device's whole pipeline
+ * (copy of its shard into its own pinned staging buffer, H2D, kernel, D2H into pinned memory,
+ * copy out to the caller), so no device's copies or host memcpys wait for another device's
+ * (a pageable hipMemcpyAsync blocks its caller until the copy is done, which serialised the
+ * devices' copies in device order before ABI 9).
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -23,6 +29,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fks_capi.h"
@@ -40,11 +47,20 @@ struct fks_multi_context {
         uint32_t* d_res = nullptr;
         uint32_t* d_err = nullptr;
         size_t cap = 0, cap_targets = 0;
+        /* pinned host staging of the shard: inputs (starts, targets), outputs (positions,
+         * then collided bytes, microsteps, resolver iterations, error bits) */
+        unsigned char* h_in = nullptr;
+        unsigned char* h_out = nullptr;
+        size_t cap_h_in = 0, cap_h_out = 0;
+        fks_status status = FKS_OK; /* the device thread's outcome */
+        std::string error;
+        fks_call_counters counters{};
     };
     std::vector<Device> devices;
     std::string last_error;
     uint64_t call_index = 0;
     int32_t width = 0;
+    int32_t active = 0; /* devices the batches are sharded over (0 = all) */
     fks_call_counters last{};
 };
 
@@ -54,17 +70,9 @@ fks_status mfail(fks_multi_context* m, fks_status st, const std::string& msg) {
     if (m) m->last_error = msg;
     return st;
 }
-fks_status mhip(fks_multi_context* m, hipError_t e, const char* where) {
-    return mfail(m, FKS_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
-}
 fks_status mctx(fks_multi_context* m, fks_status st, const fks_context* ctx, const char* where) {
     return mfail(m, st, std::string(where) + ": " + fks_status_string(st) + " (" + fks_get_last_error(ctx) + ")");
 }
-#define MHIP(m, expr)                                       \
-    do {                                                    \
-        hipError_t _e = (expr);                             \
-        if (_e != hipSuccess) return mhip((m), _e, #expr);  \
-    } while (0)
 
 template <typename T>
 hipError_t grow(T** p, size_t count) {
@@ -72,15 +80,72 @@ hipError_t grow(T** p, size_t count) {
     *p = nullptr;
     return hipMalloc((void**)p, (count > 0 ? count : 1) * sizeof(T));
 }
+hipError_t grow_pinned(unsigned char** p, size_t* cap, size_t bytes) {
+    if (bytes <= *cap && *p) return hipSuccess;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const hipError_t e = hipHostMalloc((void**)p, bytes > 0 ? bytes : 1, hipHostMallocDefault);
+    if (e == hipSuccess) *cap = bytes;
+    return e;
+}
 
 void free_device(fks_multi_context::Device& d) {
     (void)hipSetDevice(d.device);
     void* ptrs[] = {d.d_starts, d.d_targets, d.d_out, d.d_coll, d.d_micro, d.d_res, d.d_err};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (d.h_in) (void)hipHostFree(d.h_in);
+    if (d.h_out) (void)hipHostFree(d.h_out);
     if (d.stream) (void)hipStreamDestroy(d.stream);
     if (d.ctx) fks_destroy(d.ctx);
     d = fks_multi_context::Device();
+}
+
+int32_t active_count(const fks_multi_context* m) {
+    const int32_t n = (int32_t)m->devices.size();
+    return (m->active > 0 && m->active < n) ? m->active : n;
+}
+
+/* run f(device index) on one host thread per device (inline when there is one) */
+template <typename F>
+void on_device_threads(int32_t ndev, F f) {
+    if (ndev == 1) {
+        f(0);
+        return;
+    }
+    std::vector<std::thread> threads;
+    threads.reserve((size_t)ndev);
+    for (int32_t g = 0; g < ndev; ++g) threads.emplace_back(f, g);
+    for (auto& t : threads) t.join();
+}
+
+#define DHIP(d, expr)                                                                              \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess) {                                                                    \
+            (d).status = FKS_ERR_HIP;                                                              \
+            (d).error = std::string(#expr) + ": " + hipGetErrorString(_e);                         \
+            return;                                                                                \
+        }                                                                                          \
+    } while (0)
+#define DCTX(d, st, what)                                                                          \
+    do {                                                                                           \
+        const fks_status _s = (st);                                                                \
+        if (_s != FKS_OK) {                                                                        \
+            (d).status = _s;                                                                       \
+            (d).error = std::string(what) + ": " + fks_status_string(_s) + " (" + fks_get_last_error((d).ctx) + ")"; \
+            return;                                                                                \
+        }                                                                                          \
+    } while (0)
+
+/* the first failing device's error, in device order */
+fks_status collect_status(fks_multi_context* m, int32_t ndev) {
+    for (int32_t g = 0; g < ndev; ++g) {
+        const auto& d = m->devices[(size_t)g];
+        if (d.status != FKS_OK) return mfail(m, d.status, "device " + std::to_string(d.device) + ": " + d.error);
+    }
+    return FKS_OK;
 }
 
 }  // namespace
@@ -155,61 +220,74 @@ fks_status fks_multi_forward_simulate(fks_multi_context* m, const double* starts
     if (n > 0 && num_targets != 1 && num_targets != n) return mfail(m, FKS_ERR_INVALID_ARGUMENT, "targets must be 1 or n (SPCS:792)");
     const auto t0 = std::chrono::steady_clock::now();
     const size_t W = (size_t)m->width;
-    const int32_t ndev = (int32_t)m->devices.size();
+    const int32_t ndev = active_count(m);
     const uint64_t call = m->call_index++;
-    /* enqueue every shard, then collect: the devices run concurrently */
-    for (int32_t g = 0; g < ndev; ++g) {
+    /* one host thread per device: stage in, launch, stage out (the devices run concurrently) */
+    on_device_threads(ndev, [&](int32_t g) {
         auto& d = m->devices[(size_t)g];
+        d.status = FKS_OK;
+        d.error.clear();
+        std::memset(&d.counters, 0, sizeof(d.counters));
         uint64_t lo = 0, hi = 0;
         fks_shard_bounds(n, ndev, g, &lo, &hi);
         const uint64_t k = hi - lo;
-        fks_status st = fks_set_call_index(d.ctx, call);
-        if (st != FKS_OK) return mctx(m, st, d.ctx, "fks_set_call_index");
-        MHIP(m, hipSetDevice(d.device));
+        DCTX(d, fks_set_call_index(d.ctx, call), "fks_set_call_index");
+        DHIP(d, hipSetDevice(d.device));
         if (k > d.cap) {
-            MHIP(m, grow(&d.d_starts, k * W));
-            MHIP(m, grow(&d.d_out, k * W));
-            MHIP(m, grow(&d.d_coll, k));
-            MHIP(m, grow(&d.d_micro, k));
-            MHIP(m, grow(&d.d_res, k));
-            MHIP(m, grow(&d.d_err, k));
+            DHIP(d, grow(&d.d_starts, k * W));
+            DHIP(d, grow(&d.d_out, k * W));
+            DHIP(d, grow(&d.d_coll, k));
+            DHIP(d, grow(&d.d_micro, k));
+            DHIP(d, grow(&d.d_res, k));
+            DHIP(d, grow(&d.d_err, k));
             d.cap = k;
         }
         const uint64_t nt = (num_targets == n) ? k : 1;
         if (nt > d.cap_targets) {
-            MHIP(m, grow(&d.d_targets, nt * W));
+            DHIP(d, grow(&d.d_targets, nt * W));
             d.cap_targets = nt;
         }
-        if (k == 0) continue;
-        MHIP(m, hipMemcpyAsync(d.d_starts, starts + lo * W, k * W * sizeof(double), hipMemcpyHostToDevice, d.stream));
-        MHIP(m, hipMemcpyAsync(d.d_targets, targets + (num_targets == n ? lo * W : 0), nt * W * sizeof(double),
-                               hipMemcpyHostToDevice, d.stream));
-        st = fks_forward_simulate_device(d.ctx, d.d_starts, k, d.d_targets, nt, lo, allow_contacts, d.d_out, d.d_coll, d.d_micro,
-                                         d.d_res, d.d_err, d.stream, 0);
-        if (st != FKS_OK) return mctx(m, st, d.ctx, "fks_forward_simulate_device");
-    }
+        if (k == 0) {
+            DCTX(d, fks_get_last_call_counters(d.ctx, &d.counters), "fks_get_last_call_counters"); /* settles */
+            std::memset(&d.counters, 0, sizeof(d.counters));
+            return;
+        }
+        const size_t in_bytes = (k + nt) * W * sizeof(double);
+        const size_t out_bytes = k * W * sizeof(double) + k * (1 + 3 * sizeof(uint32_t));
+        DHIP(d, grow_pinned(&d.h_in, &d.cap_h_in, in_bytes));
+        DHIP(d, grow_pinned(&d.h_out, &d.cap_h_out, out_bytes));
+        double* h_starts = reinterpret_cast<double*>(d.h_in);
+        double* h_targets = h_starts + k * W;
+        std::memcpy(h_starts, starts + lo * W, k * W * sizeof(double));
+        std::memcpy(h_targets, targets + (num_targets == n ? lo * W : 0), nt * W * sizeof(double));
+        DHIP(d, hipMemcpyAsync(d.d_starts, h_starts, k * W * sizeof(double), hipMemcpyHostToDevice, d.stream));
+        DHIP(d, hipMemcpyAsync(d.d_targets, h_targets, nt * W * sizeof(double), hipMemcpyHostToDevice, d.stream));
+        DCTX(d, fks_forward_simulate_device(d.ctx, d.d_starts, k, d.d_targets, nt, lo, allow_contacts, d.d_out, d.d_coll, d.d_micro,
+                                            d.d_res, d.d_err, d.stream, 0),
+             "fks_forward_simulate_device");
+        double* h_q = reinterpret_cast<double*>(d.h_out);
+        uint32_t* h_micro = reinterpret_cast<uint32_t*>(h_q + k * W);
+        uint32_t* h_res = h_micro + k;
+        uint32_t* h_err = h_res + k;
+        uint8_t* h_coll = reinterpret_cast<uint8_t*>(h_err + k);
+        DHIP(d, hipMemcpyAsync(h_q, d.d_out, k * W * sizeof(double), hipMemcpyDeviceToHost, d.stream));
+        DHIP(d, hipMemcpyAsync(h_micro, d.d_micro, k * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
+        DHIP(d, hipMemcpyAsync(h_res, d.d_res, k * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
+        DHIP(d, hipMemcpyAsync(h_err, d.d_err, k * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
+        DHIP(d, hipMemcpyAsync(h_coll, d.d_coll, k, hipMemcpyDeviceToHost, d.stream));
+        DHIP(d, hipStreamSynchronize(d.stream));
+        std::memcpy(out_positions + lo * W, h_q, k * W * sizeof(double));
+        if (out_collided) std::memcpy(out_collided + lo, h_coll, k);
+        if (out_microsteps) std::memcpy(out_microsteps + lo, h_micro, k * sizeof(uint32_t));
+        if (out_resolver_iterations) std::memcpy(out_resolver_iterations + lo, h_res, k * sizeof(uint32_t));
+        if (out_error_flags) std::memcpy(out_error_flags + lo, h_err, k * sizeof(uint32_t));
+        DCTX(d, fks_get_last_call_counters(d.ctx, &d.counters), "fks_get_last_call_counters"); /* settles the launch */
+    });
+    const fks_status st = collect_status(m, ndev);
+    if (st != FKS_OK) return st;
     std::memset(&m->last, 0, sizeof(m->last));
     for (int32_t g = 0; g < ndev; ++g) {
-        auto& d = m->devices[(size_t)g];
-        uint64_t lo = 0, hi = 0;
-        fks_shard_bounds(n, ndev, g, &lo, &hi);
-        const uint64_t k = hi - lo;
-        MHIP(m, hipSetDevice(d.device));
-        if (k > 0) {
-            MHIP(m, hipMemcpyAsync(out_positions + lo * W, d.d_out, k * W * sizeof(double), hipMemcpyDeviceToHost, d.stream));
-            if (out_collided) MHIP(m, hipMemcpyAsync(out_collided + lo, d.d_coll, k, hipMemcpyDeviceToHost, d.stream));
-            if (out_microsteps)
-                MHIP(m, hipMemcpyAsync(out_microsteps + lo, d.d_micro, k * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
-            if (out_resolver_iterations)
-                MHIP(m, hipMemcpyAsync(out_resolver_iterations + lo, d.d_res, k * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
-            if (out_error_flags)
-                MHIP(m, hipMemcpyAsync(out_error_flags + lo, d.d_err, k * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
-            MHIP(m, hipStreamSynchronize(d.stream));
-        }
-        fks_call_counters c;
-        const fks_status st = fks_get_last_call_counters(d.ctx, &c); /* settles the device's launch */
-        if (st != FKS_OK) return mctx(m, st, d.ctx, "fks_get_last_call_counters");
-        if (k == 0) continue;
+        const fks_call_counters& c = m->devices[(size_t)g].counters;
         m->last.particles += c.particles;
         m->last.controller_steps += c.controller_steps;
         m->last.microsteps += c.microsteps;
@@ -225,6 +303,14 @@ fks_status fks_multi_forward_simulate(fks_multi_context* m, const double* starts
     m->last.call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return FKS_OK;
 }
+
+fks_status fks_multi_set_active_devices(fks_multi_context* m, int32_t count) {
+    if (!m || count < 0 || count > (int32_t)m->devices.size()) return FKS_ERR_INVALID_ARGUMENT;
+    m->active = count;
+    return FKS_OK;
+}
+
+int32_t fks_multi_active_devices(const fks_multi_context* m) { return m ? active_count(m) : 0; }
 
 fks_status fks_multi_get_statistics(const fks_multi_context* m, fks_statistics* out) {
     if (!m || !out) return FKS_ERR_INVALID_ARGUMENT;
@@ -272,45 +358,43 @@ fks_status fks_multi_check_config_collision(fks_multi_context* m, const double* 
     if (m->width <= 0) return mfail(m, FKS_ERR_NO_ROBOT, "fks_multi_set_robot has not been called");
     if (n > 0 && (!configs || !out_collided)) return mfail(m, FKS_ERR_INVALID_ARGUMENT, "null host buffer");
     const size_t W = (size_t)m->width;
-    const int32_t ndev = (int32_t)m->devices.size();
+    const int32_t ndev = active_count(m);
     /* the configurations and flags reuse the simulation buffers (starts, collided, errors) */
-    for (int32_t g = 0; g < ndev; ++g) {
+    on_device_threads(ndev, [&](int32_t g) {
         auto& d = m->devices[(size_t)g];
+        d.status = FKS_OK;
+        d.error.clear();
         uint64_t lo = 0, hi = 0;
         fks_shard_bounds(n, ndev, g, &lo, &hi);
         const uint64_t k = hi - lo;
-        MHIP(m, hipSetDevice(d.device));
+        DHIP(d, hipSetDevice(d.device));
         if (k > d.cap) {
-            MHIP(m, grow(&d.d_starts, k * W));
-            MHIP(m, grow(&d.d_out, k * W));
-            MHIP(m, grow(&d.d_coll, k));
-            MHIP(m, grow(&d.d_micro, k));
-            MHIP(m, grow(&d.d_res, k));
-            MHIP(m, grow(&d.d_err, k));
+            DHIP(d, grow(&d.d_starts, k * W));
+            DHIP(d, grow(&d.d_out, k * W));
+            DHIP(d, grow(&d.d_coll, k));
+            DHIP(d, grow(&d.d_micro, k));
+            DHIP(d, grow(&d.d_res, k));
+            DHIP(d, grow(&d.d_err, k));
             d.cap = k;
         }
-        if (k == 0) continue;
-        MHIP(m, hipMemcpyAsync(d.d_starts, configs + lo * W, k * W * sizeof(double), hipMemcpyHostToDevice, d.stream));
-        const fks_status st =
-            fks_check_config_collision_device(d.ctx, d.d_starts, k, inflation_ratio, d.d_coll, d.d_err, d.stream, 0);
-        if (st != FKS_OK) return mctx(m, st, d.ctx, "fks_check_config_collision_device");
-    }
-    for (int32_t g = 0; g < ndev; ++g) {
-        auto& d = m->devices[(size_t)g];
-        uint64_t lo = 0, hi = 0;
-        fks_shard_bounds(n, ndev, g, &lo, &hi);
-        const uint64_t k = hi - lo;
-        if (k == 0) continue;
-        MHIP(m, hipSetDevice(d.device));
-        MHIP(m, hipMemcpyAsync(out_collided + lo, d.d_coll, k, hipMemcpyDeviceToHost, d.stream));
-        if (out_error_flags)
-            MHIP(m, hipMemcpyAsync(out_error_flags + lo, d.d_err, k * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
-        MHIP(m, hipStreamSynchronize(d.stream));
+        if (k == 0) return;
+        DHIP(d, grow_pinned(&d.h_in, &d.cap_h_in, k * W * sizeof(double)));
+        DHIP(d, grow_pinned(&d.h_out, &d.cap_h_out, k * (1 + sizeof(uint32_t))));
+        std::memcpy(d.h_in, configs + lo * W, k * W * sizeof(double));
+        DHIP(d, hipMemcpyAsync(d.d_starts, d.h_in, k * W * sizeof(double), hipMemcpyHostToDevice, d.stream));
+        DCTX(d, fks_check_config_collision_device(d.ctx, d.d_starts, k, inflation_ratio, d.d_coll, d.d_err, d.stream, 0),
+             "fks_check_config_collision_device");
+        uint32_t* h_err = reinterpret_cast<uint32_t*>(d.h_out);
+        uint8_t* h_coll = reinterpret_cast<uint8_t*>(h_err + k);
+        DHIP(d, hipMemcpyAsync(h_coll, d.d_coll, k, hipMemcpyDeviceToHost, d.stream));
+        DHIP(d, hipMemcpyAsync(h_err, d.d_err, k * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
+        DHIP(d, hipStreamSynchronize(d.stream));
+        std::memcpy(out_collided + lo, h_coll, k);
+        if (out_error_flags) std::memcpy(out_error_flags + lo, h_err, k * sizeof(uint32_t));
         fks_call_counters c;
-        const fks_status st = fks_get_last_check_counters(d.ctx, &c); /* settles the device's check */
-        if (st != FKS_OK) return mctx(m, st, d.ctx, "fks_get_last_check_counters");
-    }
-    return FKS_OK;
+        DCTX(d, fks_get_last_check_counters(d.ctx, &c), "fks_get_last_check_counters"); /* settles the device's check */
+    });
+    return collect_status(m, ndev);
 }
 
 int32_t fks_device_count(void) {

@@ -32,9 +32,11 @@ struct Shape {
     int32_t waves_per_eu = 0; /* 0: the library's register budget (fksd::kThroughputWavesPerEU waves
                                * per SIMD); fewer when the LDS block caps the resident waves lower,
                                * so the kernel may use the registers those absent waves leave */
+    int32_t no_proofs = 0;    /* validation build: every skip proof compiled out (FKS_NO_SKIP_PROOFS) */
 };
 
-/* "t0-L8-J7-D7-W7-G8-P512-p1-l0" (+ "-w4" for a raised register budget): names the shape in logs and cache files */
+/* "t0-L8-J7-D7-W7-G8-P512-p1-l0" (+ "-w4" for a raised register budget, "-np" for the
+ * validation build without skip proofs): names the shape in logs and cache files */
 std::string shape_key(const Shape& s);
 
 struct CodeObject {
@@ -45,8 +47,11 @@ struct CodeObject {
 
 /* The code object of `fks_simulate_shaped` for shape `s`: from the process cache, the disk
  * cache, or a hiprtc compile (seconds; one compile at a time per process; *compiled says
- * which).  On failure returns null and sets *log. */
-std::shared_ptr<const CodeObject> code_object(const Shape& s, std::string* log, bool* compiled);
+ * which).  refresh: drop the cached copies and compile.  On failure returns null and sets
+ * *log.  The disk cache is used only when its directory belongs to this user and is not
+ * writable by others; the key covers every source byte, every option, the device
+ * architecture and the identity (size, mtime) of the fks_shapec binary that compiles. */
+std::shared_ptr<const CodeObject> code_object(const Shape& s, std::string* log, bool* compiled, bool refresh = false);
 
 /* an unsigned field of the (single) kernel's entry in a code object's AMDGPU metadata note
  * (MessagePack: the key string followed by a positive integer), e.g. ".vgpr_count"; -1 if

@@ -162,13 +162,17 @@ class HipParticleContactSimulator:
         (fks_set_small_batch_kernel; default on).  Results do not depend on it."""
         _capi.check(self._lib.fks_set_small_batch_kernel(self._ctx, 1 if enabled else 0), self._ctx, "small batch kernel")
 
-    def set_specialization(self, enabled: bool = True):
+    def set_specialization(self, enabled=True):
         """Run the plain throughput simulation of this robot (and of every robot set later) on a
         kernel compiled at run time for its shape (fks_set_specialization: hiprtc, cached per
         process and on disk).  On by default, built at the first call that runs it; enabling
         it builds the current robot's kernel now.  Results do not depend on it; raises FksError
-        with the compiler log when the current robot's kernel cannot be built."""
-        _capi.check(self._lib.fks_set_specialization(self._ctx, 1 if enabled else 0), self._ctx, "specialization")
+        with the compiler log when the current robot's kernel cannot be built (the calls then
+        keep the generic kernel, and specialization()["failed"] says so).  enabled may also be
+        an fks_specialization_mode: _capi.SPECIALIZE_NO_PROOFS builds the validation kernel with
+        every skip proof compiled out (same results, slower)."""
+        mode = int(enabled) if not isinstance(enabled, bool) else (_capi.SPECIALIZE_ON if enabled else _capi.SPECIALIZE_OFF)
+        _capi.check(self._lib.fks_set_specialization(self._ctx, mode), self._ctx, "specialization")
 
     def launch_info(self) -> dict:
         """fks_get_launch_info: the layout fks_set_robot chose and the kernel of the last call."""
@@ -177,7 +181,8 @@ class HipParticleContactSimulator:
         return info.as_dict()
 
     def specialization(self) -> dict:
-        """fks_get_specialization: enabled, active, pending, from_cache, compile_seconds, launches, shape"""
+        """fks_get_specialization: enabled (mode), active, pending, from_cache, compile_seconds, launches,
+        shape, failed, message"""
         info = _capi.SpecializationInfo()
         _capi.check(self._lib.fks_get_specialization(self._ctx, ctypes.byref(info)), self._ctx, "specialization")
         return info.as_dict()
@@ -515,6 +520,21 @@ class MultiDeviceSimulator:
 
     def num_devices(self) -> int:
         return int(self._lib.fks_multi_num_devices(self._ctx))
+
+    def set_active_devices(self, count: int = 0):
+        """Shard the batches that follow over the first `count` listed devices (0 = all;
+        fks_multi_set_active_devices).  Results do not depend on it."""
+        self._check(self._lib.fks_multi_set_active_devices(self._ctx, int(count)), "fks_multi_set_active_devices")
+
+    def active_devices(self) -> int:
+        return int(self._lib.fks_multi_active_devices(self._ctx))
+
+    def device_simulator_specialization(self, shard: int = 0) -> dict:
+        """fks_get_specialization of one device's context."""
+        info = _capi.SpecializationInfo()
+        ctx = self._lib.fks_multi_device_context(self._ctx, int(shard))
+        _capi.check(self._lib.fks_get_specialization(ctx, ctypes.byref(info)), ctx, "specialization")
+        return info.as_dict()
 
     def set_robot(self, robot: RobotDescription):
         if self._robot is robot:

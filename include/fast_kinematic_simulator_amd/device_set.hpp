@@ -3,13 +3,16 @@
  *
  * The reference runs every batch over the host's cores (`#pragma omp parallel for` over
  * particles, SPCS:795-802).  A DeviceSet runs it over a list of devices: one fks_context
- * for a single device, an fks_multi_context (fks_multi.cpp) for several.  Batches of at
- * least shard_threshold() particles are split into contiguous shards by global particle
- * id, one per device, each simulated with first_particle_id = the shard's start and the
- * call index the first device would have used, so the counter RNG streams and therefore
- * the results are bit-identical to one device.  Smaller batches and every
- * single-particle call (mutable robots, traced runs, kinematics) run on devices[0], whose
- * call index is the simulator's.  Statistics are summed over the devices.
+ * for a single device, an fks_multi_context (fks_multi.cpp) for several.  A batch is split
+ * into contiguous shards by global particle id over the first devices_for(n) devices — as
+ * many as keep at least shard_threshold() particles each — each simulated with
+ * first_particle_id = the shard's start and the call index the first device would have used,
+ * so the counter RNG streams and therefore the results are bit-identical to one device
+ * (DESIGN.md §6).  A launch lasts at least as long as its slowest particle's chain, so a shard
+ * smaller than a few times one device's resident waves gains little from another device
+ * (the strong-scaling projection in DESIGN.md §6 sets the default).  Batches that keep one
+ * device and every single-particle call (mutable robots, traced runs, kinematics) run on
+ * devices[0], whose call index is the simulator's.  Statistics are summed over the devices.
  *
  * Used by the planner-facing HipParticleContactSimulator (fast_kinematic_simulator.hpp) and
  * the plain C++ wrapper (hip_particle_contact_simulator.hpp).
@@ -35,6 +38,18 @@ class SimulatorError : public std::runtime_error {
 
   private:
     fks_status status_;
+};
+
+/* The robot-shape-specialised kernel of the current robot on every device
+ * (fks_get_specialization): whether all of them run it, and why not when a build failed (the
+ * calls then run the generic kernel: same results, 10-20 % slower). */
+struct SpecializationStatus {
+    bool active = false;  /* every device runs the shaped kernel for the current robot */
+    bool pending = false; /* some device builds it at its first throughput call */
+    bool failed = false;  /* some device's build failed */
+    std::string shape;    /* the shape key */
+    std::string message;  /* the first failure's log, else empty */
+    std::vector<fks_specialization_info> per_device;
 };
 
 /* every device visible to the process (HIP_VISIBLE_DEVICES applies), {0} when there is none
@@ -89,30 +104,40 @@ class DeviceSet {
             Check(fks_set_robot(ctx_, &d), ctx_, "fks_set_robot");
     }
 
-    /* batches of at least this many particles are sharded (0: automatic = the resident waves
-     * of devices[0] for the current robot, so a batch one device runs with one wave per
-     * particle pays no fan-out; 1 shards every batch) */
-    void set_shard_threshold(uint64_t particles) { shard_threshold_ = particles; }
+    /* the particles each device must get before a batch takes it on (0: automatic =
+     * kShardWavesPerDevice x the resident waves of devices[0] for the current robot; 1 shards
+     * every batch of at least as many particles as devices over all of them) */
+    static constexpr uint64_t kShardWavesPerDevice = 2;
+    void set_shard_threshold(uint64_t particles_per_device) { shard_threshold_ = particles_per_device; }
     uint64_t shard_threshold() const {
         if (shard_threshold_ > 0) return shard_threshold_;
         uint32_t waves = 0;
         uint64_t lds = 0;
         Check(fks_get_launch_geometry(ctx_, &waves, &lds), ctx_, "fks_get_launch_geometry");
-        return waves > 0 ? waves : 1;
+        return waves > 0 ? kShardWavesPerDevice * waves : 1;
     }
-    bool shards(uint64_t n) const { return multi_ && n > 0 && n >= shard_threshold(); }
-    /* whether the last batch ran sharded over every device */
-    bool last_sharded() const { return last_sharded_; }
+    /* the devices a batch of n particles is sharded over: min(devices, n / shard_threshold()), >= 1 */
+    int32_t devices_for(uint64_t n) const {
+        if (!multi_ || n == 0) return 1;
+        const uint64_t g = n / shard_threshold();
+        const uint64_t nd = (uint64_t)fks_multi_num_devices(multi_.get());
+        return (int32_t)(g < 1 ? 1 : (g > nd ? nd : g));
+    }
+    bool shards(uint64_t n) const { return devices_for(n) >= 2; }
+    /* how many devices the last batch ran on (1: devices[0] alone) */
+    int32_t last_devices() const { return last_devices_; }
+    bool last_sharded() const { return last_devices_ >= 2; }
 
     /* ForwardSimulateRobots / ReverseSimulateRobots (SPCS:788-822) over host buffers; the
      * arguments are those of fks_forward_simulate */
     void simulate(bool reverse, const double* starts, uint64_t n, const double* targets, uint64_t num_targets, bool allow_contacts,
                   double* out_positions, uint8_t* out_collided, uint32_t* out_microsteps, uint32_t* out_resolver_iterations,
                   uint32_t* out_error_flags, const char* what) {
-        last_sharded_ = shards(n);
-        if (last_sharded_) {
+        last_devices_ = devices_for(n);
+        if (last_devices_ >= 2) {
             /* every device uses the call index devices[0] would have used */
             const uint64_t call = fks_get_call_index(ctx_);
+            MultiCheck(fks_multi_set_active_devices(multi_.get(), last_devices_), what);
             MultiCheck(fks_multi_set_call_index(multi_.get(), call), what);
             MultiCheck(fks_multi_forward_simulate(multi_.get(), starts, n, targets, num_targets, allow_contacts ? 1 : 0, out_positions,
                                                   out_collided, out_microsteps, out_resolver_iterations, out_error_flags),
@@ -129,9 +154,11 @@ class DeviceSet {
     /* batched CheckConfigCollision (SPCS:1398-1416) */
     void check_configs(const double* configs, uint64_t n, double inflation_ratio, uint8_t* out_collided, uint32_t* out_error_flags,
                        const char* what) const {
-        if (shards(n))
+        const int32_t g = devices_for(n);
+        if (g >= 2) {
+            MultiCheck(fks_multi_set_active_devices(multi_.get(), g), what);
             MultiCheck(fks_multi_check_config_collision(multi_.get(), configs, n, inflation_ratio, out_collided, out_error_flags), what);
-        else
+        } else
             Check(fks_check_config_collision(ctx_, configs, n, inflation_ratio, out_collided, out_error_flags), ctx_, what);
     }
 
@@ -158,6 +185,33 @@ class DeviceSet {
     }
     void set_individual_jacobians(bool on) const {
         for_each([&](fks_context* c) { Check(fks_set_individual_jacobians(c, on ? 1 : 0), c, "fks_set_individual_jacobians"); });
+    }
+
+    /* build the current robot's shape-specialised kernel on every device now (construction
+     * time, where a planner expects setup cost) instead of inside the first large batch.  A
+     * failed build is not an error: the calls keep the generic kernel and the returned status
+     * says why.  mode: FKS_SPECIALIZE_OFF / _ON / _NO_PROOFS */
+    SpecializationStatus prepare_kernels(int32_t mode = FKS_SPECIALIZE_ON) const {
+        for_each([&](fks_context* c) {
+            const fks_status st = fks_set_specialization(c, mode);
+            if (st != FKS_OK && st != FKS_ERR_UNSUPPORTED) Check(st, c, "fks_set_specialization");
+        });
+        return specialization_status();
+    }
+    SpecializationStatus specialization_status() const {
+        SpecializationStatus s;
+        s.active = true;
+        for_each([&](fks_context* c) {
+            fks_specialization_info i{};
+            Check(fks_get_specialization(c, &i), c, "fks_get_specialization");
+            s.active = s.active && i.active != 0;
+            s.pending = s.pending || i.pending != 0;
+            if (i.failed && !s.failed) s.message = i.message;
+            s.failed = s.failed || i.failed != 0;
+            if (s.shape.empty()) s.shape = i.shape;
+            s.per_device.push_back(i);
+        });
+        return s;
     }
 
     static void Check(fks_status st, const fks_context* ctx, const char* what) {
@@ -187,7 +241,7 @@ class DeviceSet {
     std::unique_ptr<fks_multi_context, DestroyMulti> multi_;
     fks_context* ctx_ = nullptr;
     uint64_t shard_threshold_ = 0;
-    bool last_sharded_ = false;
+    int32_t last_devices_ = 1;
 };
 
 }  // namespace fks

@@ -97,11 +97,11 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
     typedef fks_planner_types::ColorRGBA ColorRGBA;
 
     /* SPCS:420-444.  `devices` lists the MI355X devices the simulator runs on (no reference
-     * counterpart; the reference's batch loop runs over the host's cores, SPCS:795): batches
-     * of at least ShardThreshold() particles are split into contiguous shards by global
-     * particle id, one per listed device (fks_create_multi), bit-identical to one device;
-     * smaller batches and single-particle calls run on devices[0].  The same device may be
-     * listed more than once. */
+     * counterpart; the reference's batch loop runs over the host's cores, SPCS:795): a batch
+     * is split into contiguous shards by global particle id over as many of the listed devices
+     * as keep at least ShardThreshold() particles each (fks_create_multi), bit-identical to
+     * one device; batches that keep one device and single-particle calls run on devices[0].
+     * The same device may be listed more than once. */
     HipParticleContactSimulator(const sdf_tools::TaggedObjectCollisionMapGrid& environment,
                                 const sdf_tools::SignedDistanceField& environment_sdf,
                                 const SurfaceNormalGrid& surface_normals_grid, const SimulatorSolverParameters& solver_config,
@@ -345,16 +345,18 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
     const std::vector<uint32_t>& LastParticleErrors() const { return last_errors_; }
     const std::vector<uint32_t>& LastMicrosteps() const { return last_micro_; }
     const std::vector<uint32_t>& LastResolverIterations() const { return last_resolver_; }
-    /* the context of devices[0] (single-particle calls and batches below ShardThreshold()) */
+    /* the context of devices[0] (single-particle calls and batches that keep one device) */
     fks_context* Context() const { return ctx_; }
     const std::vector<int32_t>& Devices() const { return dev_->devices(); }
-    /* batches of at least this many particles are sharded over Devices() (0: automatic = the
-     * resident waves of devices[0] for the current robot, so that a batch one device runs in
-     * a single wave per particle pays no fan-out); 1 shards every batch */
-    void SetShardThreshold(uint64_t particles) { dev_->set_shard_threshold(particles); }
+    /* the particles each listed device must get before a batch is sharded over it (0:
+     * automatic = twice the resident waves of devices[0] for the current robot: a smaller shard
+     * is bounded by its slowest particle's chain); 1 shards every batch over all
+     * of Devices() */
+    void SetShardThreshold(uint64_t particles_per_device) { dev_->set_shard_threshold(particles_per_device); }
     uint64_t ShardThreshold() const { return dev_->shard_threshold(); }
-    /* whether the last batch call ran sharded over every listed device */
+    /* whether the last batch call ran sharded, and over how many of Devices() */
     bool LastBatchSharded() const { return dev_->last_sharded(); }
+    int32_t LastBatchDevices() const { return dev_->last_devices(); }
     /* batched CheckConfigCollision (SPCS:1398-1416, one configuration per call there),
      * sharded like the simulation batches */
     std::vector<uint8_t> CheckConfigCollisions(const std::shared_ptr<BaseRobotType>& immutable_robot,
@@ -370,6 +372,17 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
         dev_->check_configs(c.data(), configs.size(), inflation_ratio, collided.data(), nullptr, "CheckConfigCollisions");
         return collided;
     }
+    /* Robot-shape specialisation (fks_set_specialization; no reference counterpart, results are
+     * identical either way).  PrepareKernels builds `robot`'s kernel on every device now, so the
+     * compile (2-20 s the first time on a machine, then from the disk cache) lands at setup and
+     * not inside the first large ForwardSimulateRobots; SpecializationStatus reports whether the
+     * calls run it, and the compiler log when its build failed (they then run the generic
+     * kernel).  Neither throws on a failed build. */
+    fks::SpecializationStatus PrepareKernels(const std::shared_ptr<BaseRobotType>& robot) {
+        SetRobot(Derived(robot));
+        return dev_->prepare_kernels(FKS_SPECIALIZE_ON);
+    }
+    fks::SpecializationStatus SpecializationStatus() const { return dev_->specialization_status(); }
     /* the configuration capacity a traced call starts with (a longer trace is re-run once with
      * the exact size); RetriedTraces() counts those re-runs */
     void SetTraceCapacityHint(uint32_t configs) { trace_capacity_hint_ = configs > 0 ? configs : 1; }

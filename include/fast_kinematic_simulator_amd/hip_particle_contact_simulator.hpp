@@ -203,9 +203,9 @@ class RobotDescription {
     }
 };
 
-/* SimpleParticleContactSimulator on one or several MI355X devices (DeviceSet: batches of
- * at least ShardThreshold() particles are sharded by particle id, bit-identical to one
- * device).  The stacked-Jacobian resolver is always used, as the reference factories
+/* SimpleParticleContactSimulator on one or several MI355X devices (DeviceSet: a batch is
+ * sharded by particle id over as many devices as keep at least ShardThreshold() particles
+ * each, bit-identical to one device).  The stacked-Jacobian resolver is always used, as the reference factories
  * hard-wire (FKS.cpp:22,45,68). */
 class HipParticleContactSimulator {
   public:
@@ -230,9 +230,17 @@ class HipParticleContactSimulator {
                                       std::vector<int32_t>{device}) {}
 
     const std::vector<int32_t>& Devices() const { return dev_.devices(); }
-    void SetShardThreshold(uint64_t particles) { dev_.set_shard_threshold(particles); }
+    void SetShardThreshold(uint64_t particles_per_device) { dev_.set_shard_threshold(particles_per_device); }
     uint64_t ShardThreshold() const { return dev_.shard_threshold(); }
     bool LastBatchSharded() const { return dev_.last_sharded(); }
+    int32_t LastBatchDevices() const { return dev_.last_devices(); }
+    /* build `robot`'s shape-specialised kernel on every device now (see
+     * fast_kinematic_simulator.hpp PrepareKernels); never throws on a failed build */
+    fks::SpecializationStatus PrepareKernels(const RobotDescription& robot) {
+        SetRobot(robot);
+        return dev_.prepare_kernels(FKS_SPECIALIZE_ON);
+    }
+    fks::SpecializationStatus SpecializationStatus() const { return dev_.specialization_status(); }
 
     /* GetFrame (SPCS:517-520) */
     std::string GetFrame() const { return frame_; }

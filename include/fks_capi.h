@@ -64,8 +64,12 @@ extern "C" {
  * 6: host robot control (fks_robot_control_action, fks_robot_apply_control_input), the
  * environment builder's public steps (fks_env_discretize_obstacle, fks_env_build_normals,
  * fks_env_cell_objects), fks_set_statistics / fks_set_total_counters.
- * 7: fks_set_small_batch_kernel */
-#define FKS_ABI_VERSION 8
+ * 7: fks_set_small_batch_kernel
+ * 8: shape specialisation, launch info
+ * 9: specialisation modes (FKS_SPECIALIZE_NO_PROOFS validation kernel), build failures in
+ *    fks_specialization_info (failed, message), fks_multi_set_active_devices, pinned per-device
+ *    staging in fks_multi_* */
+#define FKS_ABI_VERSION 9
 
 typedef enum {
     FKS_OK = 0,
@@ -499,18 +503,32 @@ fks_status fks_set_individual_jacobians(fks_context* ctx, int32_t simulate_with_
  * the first robot of a shape on a machine costs one compile (2-20 s in the calling thread),
  * later ones come from the per-process cache or the disk cache (FKS_KERNEL_CACHE=<dir>,
  * default ~/.cache/fast_kinematic_simulator_amd; "off" disables it).  When the kernel cannot
- * be built the calls keep the generic kernel and fks_get_last_error holds the compiler log;
- * fks_set_specialization(ctx, 1) then returns FKS_ERR_UNSUPPORTED.  0 = generic kernels only
- * (also the default when the environment variable FKS_SPECIALIZE=0 is set at fks_create). */
-fks_status fks_set_specialization(fks_context* ctx, int32_t enabled);
+ * be built the calls keep the generic kernel (same results), fks_get_specialization reports
+ * failed = 1 with the compiler log in `message`, and so does fks_get_last_error;
+ * fks_set_specialization(ctx, FKS_SPECIALIZE_ON) then returns FKS_ERR_UNSUPPORTED.
+ * FKS_SPECIALIZE_OFF = generic kernels only (also the default when the environment variable
+ * FKS_SPECIALIZE=0 is set at fks_create).  FKS_SPECIALIZE_NO_PROOFS (ABI 9, validation only)
+ * builds the same shaped kernel with every skip proof compiled out (FKS_NO_SKIP_PROOFS: the
+ * environment / correction round proofs, the motion-estimate pruning, the self-collision gap
+ * proof and both lever-arm shortcuts): the results must not change, only the
+ * time, which is what tests/test_proof_free.py checks on full batches. */
+typedef enum {
+    FKS_SPECIALIZE_OFF = 0,
+    FKS_SPECIALIZE_ON = 1,
+    FKS_SPECIALIZE_NO_PROOFS = 2
+} fks_specialization_mode;
+fks_status fks_set_specialization(fks_context* ctx, int32_t mode);
 typedef struct fks_specialization_info {
-    int32_t enabled;         /* fks_set_specialization */
+    int32_t enabled;         /* fks_set_specialization's mode (fks_specialization_mode) */
     int32_t active;          /* the current robot's plain simulation calls run the shape-specialised kernel */
     int32_t from_cache;      /* its code object came from the process or disk cache */
     int32_t pending;         /* enabled, robot set, kernel to be built at the first call that runs it */
     double compile_seconds;  /* hiprtc time of that code object (0 when it came from a cache) */
     uint64_t launches;       /* launches of the specialised kernel since the robot was set */
     char shape[64];          /* the shape key, e.g. "t0-L8-J7-D7-W7-G8-P512-p1-l0" */
+    int32_t failed;          /* ABI 9: the current robot's build failed; its calls run the generic kernel */
+    int32_t reserved;
+    char message[512];       /* ABI 9: why it failed (the start of the compiler log), else empty */
 } fks_specialization_info;
 fks_status fks_get_specialization(const fks_context* ctx, fks_specialization_info* out);
 
@@ -609,10 +627,11 @@ void fks_env_free(fks_env_handle* env);
  * over particles, SPCS:795); a multi context runs one fks_context per listed device and
  * splits every batch into contiguous shards, particle i on the device whose
  * fks_shard_bounds range holds it, simulated with first_particle_id = the range start
- * (bit-identical results for any device list).  Inputs go to each device by its own H2D
- * copy, the devices run concurrently on their own streams, and each copies its outcomes
- * into the caller's buffers at its offset; statistics and call counters are summed over
- * the devices (kernel_ms: the slowest).  The same device may be listed more than once. */
+ * (bit-identical results for any device list).  Each device has a host thread of its own for
+ * the call: it stages its shard through pinned buffers of its own (H2D, kernel, D2H on the
+ * device's stream, so no device's copies wait for another's), and copies its outcomes into
+ * the caller's buffers at its offset; statistics and call counters are summed over the
+ * devices (kernel_ms: the slowest).  The same device may be listed more than once. */
 typedef struct fks_multi_context fks_multi_context;
 /* [begin, end) of shard `shard` of n particles over ndev devices: balanced contiguous ranges,
  * the first n % ndev shards one particle longer */
@@ -626,7 +645,13 @@ int32_t fks_multi_num_devices(const fks_multi_context* m);
 /* the per-device context of shard `shard` (for per-device settings such as fks_set_segment_steps) */
 fks_context* fks_multi_device_context(fks_multi_context* m, int32_t shard);
 fks_status fks_multi_set_robot(fks_multi_context* m, const fks_robot_desc* robot);
-/* ForwardSimulateRobots (SPCS:788-804) over all devices; arguments as fks_forward_simulate */
+/* ABI 9: the batches that follow are sharded over the first `count` listed devices only
+ * (1 <= count <= fks_multi_num_devices; 0 = all).  A batch too small to keep every device
+ * busy for longer than its slowest particle runs no faster on more devices, so
+ * the planner-facing DeviceSet picks the count per batch from the particles per device. */
+fks_status fks_multi_set_active_devices(fks_multi_context* m, int32_t count);
+int32_t fks_multi_active_devices(const fks_multi_context* m);
+/* ForwardSimulateRobots (SPCS:788-804) over the active devices; arguments as fks_forward_simulate */
 fks_status fks_multi_forward_simulate(fks_multi_context* m, const double* starts, uint64_t n, const double* targets,
                                       uint64_t num_targets, int32_t allow_contacts, double* out_positions, uint8_t* out_collided,
                                       uint32_t* out_microsteps, uint32_t* out_resolver_iterations, uint32_t* out_error_flags);

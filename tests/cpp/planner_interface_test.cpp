@@ -407,9 +407,18 @@ static int exercise(const Scene& s, const std::shared_ptr<simple_simulator_inter
     auto* hip = dynamic_cast<simple_particle_contact_simulator::HipParticleContactSimulator<Robot, Config, upc::PRNG, Alloc>*>(sim.get());
     if (!hip) throw std::runtime_error("the factory did not return the HIP simulator");
     apply_shard_threshold(hip);
+    /* the shape-specialised kernel built at setup, on every device (PrepareKernels), so the
+     * first batch does not pay the compile; a failed build would only fall back (same bytes) */
+    {
+        const fks::SpecializationStatus st = hip->PrepareKernels(base);
+        std::fprintf(stderr, "kernels %s active %d failed %d%s%s\n", st.shape.c_str(), st.active ? 1 : 0, st.failed ? 1 : 0,
+                     st.failed ? ": " : "", st.message.c_str());
+        if (st.per_device.size() != hip->Devices().size()) throw std::runtime_error("one specialisation status per device");
+    }
     /* call index 0: ForwardSimulateRobots (SPCS:788) */
     const auto fwd = sim->ForwardSimulateRobots(base, starts, targets, s.allow, [](const fks_planner_types::MarkerArray&) {});
-    std::fprintf(stderr, "devices %zu sharded %d\n", hip->Devices().size(), hip->LastBatchSharded() ? 1 : 0);
+    std::fprintf(stderr, "devices %zu sharded %d over %d\n", hip->Devices().size(), hip->LastBatchSharded() ? 1 : 0,
+                 hip->LastBatchDevices());
     for (size_t i = 0; i < fwd.size(); ++i) print("fwd", i, fwd[i]);
     for (const auto& kv : sim->GetStatistics()) std::printf("stat %s %.0f\n", kv.first.c_str(), kv.second);
     /* call index 1: ReverseSimulateRobots (SPCS:806) */

@@ -288,17 +288,22 @@ def test_planner_interface_sharded_over_device_lists(fks_lib, name):
     default (every visible device)."""
     base, *_ = _run(name, normals=(name == "linked"))
     assert base.returncode == 0, base.stderr
-    assert "devices 1 sharded 0" in base.stderr
+    assert "devices 1 sharded 0 over 1" in base.stderr
+    # PrepareKernels built the shape-specialised kernel at setup (a failed build would be
+    # reported here and fall back, same bytes)
+    assert " active 1 failed 0" in base.stderr, base.stderr
     for devices in ("0,0", "0,0,0", "all"):
         p, *_ = _run(name, normals=(name == "linked"), devices=devices, shard=1)
         assert p.returncode == 0, (devices, p.stderr)
         ndev = len(devices.split(",")) if devices != "all" else int(_capi.lib().fks_device_count())
-        assert f"devices {ndev} sharded {1 if ndev > 1 else 0}" in p.stderr, (devices, p.stderr)
+        assert f"devices {ndev} sharded {1 if ndev > 1 else 0} over {ndev}" in p.stderr, (devices, p.stderr)
+        assert " active 1 failed 0" in p.stderr, p.stderr
         assert p.stdout == base.stdout, devices
         assert p.normals == base.normals
-    # the automatic threshold (one device's resident waves) keeps these small batches whole
+    # the automatic threshold (twice one device's resident waves per device) keeps these small
+    # batches on the first device
     p, *_ = _run(name, devices="0,0")
-    assert p.returncode == 0 and "devices 2 sharded 0" in p.stderr, p.stderr
+    assert p.returncode == 0 and "devices 2 sharded 0 over 1" in p.stderr, p.stderr
 
 
 @pytest.mark.parametrize("name", ["linked", "se2", "se3"])

@@ -19,6 +19,8 @@
 #   sched:<wl>:<segs>:<heavy>  scheduling sweep (tools/sched_sweep.py; comma lists of segment lengths and
 #                      heavy thresholds, priority 1) -> <tag>_sched_<wl>.json
 #   torchrun1          bench.py through torch.distributed.run, world size 1 (RCCL) -> <tag>_torchrun_w1.json
+#   inproc:<devices>   bench.py --in-process over a device list (e.g. 0 or 0,0) with the strong-scaling
+#                      projection -> <tag>_inproc_<devices>.json
 #   round              suite smoke bench trace pmc others
 set -o pipefail
 TAG=$1
@@ -34,7 +36,7 @@ export FKS_SHAPEC=$PWD/fast_kinematic_simulator_amd/fks_shapec
 # (warm), so no compiler process starts under rocprofv3
 export FKS_KERNEL_CACHE=/tmp/fks_kernel_cache_$TAG
 warm() { timeout -k 10 300 "$@" > /dev/null 2>&1; }
-BP="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --pipeline-batches 0"
+BP="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --pipeline-batches 0 --no-projection"
 lib() { [ "$1" = L ] && echo $L || echo "$1"; }
 
 run_task() {
@@ -52,13 +54,13 @@ run_task() {
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_write -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_write.err &&
     timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/${TAG}_pmc_tcc -o bench -- $BP > /dev/null 2> $O/${TAG}_pmc_tcc.err ;;
   pmc:*)
-    w=${1#pmc:}; BW="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0 --workload $w"
+    w=${1#pmc:}; BW="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0 --no-projection --workload $w"
     warm $BW &&
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_${w}_fetch -o bench -- $BW > /dev/null 2> $O/${TAG}_pmc_${w}_fetch.err &&
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/${TAG}_pmc_${w}_write -o bench -- $BW > /dev/null 2> $O/${TAG}_pmc_${w}_write.err &&
     timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/${TAG}_pmc_${w}_tcc -o bench -- $BW > /dev/null 2> $O/${TAG}_pmc_${w}_tcc.err ;;
   valu)
-    B1="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0"
+    B1="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0 --no-projection"
     mkdir -p $O/${TAG}_valu
     warm $B1 &&
     timeout -s KILL 180 rocprofv3 --pmc VALUBusy --kernel-trace --output-format csv -d $O/${TAG}_valu/valubusy -o bench -- $B1 > /dev/null 2> $O/${TAG}_valu/valubusy.err &&
@@ -83,7 +85,7 @@ run_task() {
     rc=$?; unset FKS_LIB_PATH FKS_VARIANT_LIB; return $rc ;;
   mix:*)
     spec=${1#mix:}; w=${spec%%:*}; l=$(lib ${spec#*:}); n=$(basename $l .so); D=$O/${TAG}_mix_${w}_$n
-    BM="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0 --workload $w"
+    BM="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0 --no-projection --workload $w"
     export FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1
     warm $BM &&
     timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES --kernel-trace --output-format csv -d $D/mix -o m -- $BM > $D.mix.log 2>&1 &&
@@ -94,6 +96,7 @@ run_task() {
     spec=${1#sched:}; w=${spec%%:*}; rest=${spec#*:}; seg=${rest%%:*}; heavy=${rest#*:}
     np=""; [ "$w" = cfg4 -o "$w" = cfg5 ] && np="--particles 131072"
     timeout -k 10 600 python tools/sched_sweep.py --workload $w $np --segments $seg --heavy $heavy --prio 1 --json $O/${TAG}_sched_$w.json > $O/${TAG}_sched_$w.log 2>&1 ;;
+  inproc:*) d=${1#inproc:}; timeout -k 10 400 python bench.py --in-process --devices $d --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_inproc_${d//,/}.json 2> $O/${TAG}_inproc_${d//,/}.err ;;
   torchrun1) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_torchrun_w1.json 2> $O/${TAG}_torchrun_w1.err ;;
   round) for t in suite smoke bench trace pmc others; do run_task $t || return $?; done ;;
   *) echo "unknown task $1" >&2; return 2 ;;

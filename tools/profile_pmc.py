@@ -8,7 +8,9 @@ each its own `rocprofv3 --pmc ... --kernel-trace --output-format csv` run of
     python tools/profile_pmc.py <fetch> <write> <tcc> r04_cfg5 fks_simulate_linked_lean   # another kernel
 
 Only the headline kernel's summary (no kernel argument) is also written as latest_pmc.json,
-which bench.py reads for `roofline.traffic`.
+which bench.py reads for `roofline.traffic` — and only when the profile names the kernel and
+shape its own timed launches ran (`--shape t0-L8-...`, the bench line's specialization.shape)
+and the kernel sources it was built from (kernel_source_sha16, checked against the tree).
 
 HBM traffic per launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 bytes, averaged over the
 kernel's dispatches: MI355X_MICROARCH.md §HBM prescribes doubling FETCH_SIZE on gfx950
@@ -35,9 +37,31 @@ def counters(path, kernel=KERNEL):
     return vals
 
 
+def kernel_source_sha16():
+    """A hash of the kernel source and the headers it includes (build.EMBEDDED): a profile of
+    another kernel version is not quoted by bench.py."""
+    import hashlib
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from fast_kinematic_simulator_amd import build
+
+    h = hashlib.sha256()
+    for name, rel in build.EMBEDDED:
+        h.update(name.encode() + b"\0")
+        h.update(open(os.path.join(build.PKG, rel), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def main():
-    fetch_dir, write_dir, tcc_dir, tag = sys.argv[1:5]
-    kernel = sys.argv[5] if len(sys.argv) > 5 else KERNEL
+    argv = list(sys.argv[1:])
+    shape = None
+    if "--shape" in argv:
+        i = argv.index("--shape")
+        shape = argv[i + 1]
+        del argv[i:i + 2]
+    fetch_dir, write_dir, tcc_dir, tag = argv[:4]
+    kernel = argv[4] if len(argv) > 4 else KERNEL
     f = counters(fetch_dir, kernel)["FETCH_SIZE"]
     w = counters(write_dir, kernel)["WRITE_SIZE"]
     t = counters(tcc_dir, kernel)
@@ -46,7 +70,8 @@ def main():
     fetch_b = 2.0 * fetch_raw
     write_b = sum(w) / len(w) * 1024.0
     out = {
-        "kernel": kernel,
+        "kernel": f"{kernel} ({shape})" if shape else kernel,
+        "kernel_source_sha16": kernel_source_sha16(),
         "dispatches": len(f),
         "fetch_bytes_per_launch": fetch_b,
         "fetch_size_raw_bytes_per_launch": fetch_raw,

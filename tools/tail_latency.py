@@ -51,12 +51,14 @@ def main():
     wl = W.WORKLOADS[a.workload]()
     sim = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
     sim.set_robot(wl.robot)
+    # the library specialises by default: "off" must switch it off explicitly
+    sim.set_specialization(a.specialize == "on")
     if a.specialize == "on":
-        sim.set_specialization(True)
         sim.set_small_batch_kernel(False)
     run(sim, wl, wl.starts[:256], 0, dev)
     m, it, kms, ph = run(sim, wl, wl.starts, 0, dev)
-    out = {"workload": a.workload, "specialization": sim.specialization(), "batch_kernel_ms": kms, "particles": int(m.size), "alone": [],
+    out = {"workload": a.workload, "specialization": sim.specialization(), "batch_kernel": sim.launch_info()["last_kernel"],
+           "batch_kernel_ms": kms, "particles": int(m.size), "alone": [],
            "batch_phase_share": ({k: round(v / max(1, ph.get("particle", 0)), 4) for k, v in ph.items() if k not in COUNTS}
                                  if ph.get("control", 0) > 0 else None),
            "batch_phase_counts": {k: ph[k] for k in COUNTS if k in ph}}

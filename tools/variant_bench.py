@@ -23,7 +23,7 @@ def main():
     for spec in libs:
         lib, _, flag = spec.partition("+")
         env = dict(os.environ, FKS_LIB_PATH=os.path.abspath(lib), FKS_VARIANT_LIB="1")
-        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--pipeline-batches", "0", *extra]
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--pipeline-batches", "0", "--no-projection", *extra]
         if flag.startswith("env:"):
             name, _, value = flag[4:].partition("=")
             env[name] = value
