@@ -198,7 +198,7 @@ class SpecializationInfo(ctypes.Structure):
 
 
 class LaunchInfo(ctypes.Structure):
-    """fks_launch_info (ABI 8)"""
+    """fks_launch_info (ABI 9)"""
     _fields_ = [
         ("resident_waves", c_uint32),
         ("waves_per_group", c_uint32),
@@ -208,12 +208,13 @@ class LaunchInfo(ctypes.Structure):
         ("fk_pair", c_int32),
         ("lean", c_int32),
         ("last_kernel", c_int32),
-        ("reserved", c_int32),
+        ("last_check_kernel", c_int32),
     ]
 
     def as_dict(self):
         d = {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
         d["last_kernel"] = KERNEL_KINDS.get(d["last_kernel"], d["last_kernel"])
+        d["last_check_kernel"] = KERNEL_KINDS.get(d["last_check_kernel"], d["last_check_kernel"])
         return d
 
 

@@ -277,7 +277,8 @@ struct fks_context {
     bool fk_pair = false;             /* paired FK of free microsteps (fks_set_robot) */
     bool lean = false;                /* lean LDS block + lean kernels (fks_set_robot) */
     uint32_t standard_resident_waves = 0; /* resident waves of the non-lean layout (fks_get_launch_info) */
-    int32_t last_kernel = FKS_KERNEL_NONE; /* the simulation kernel of the last call */
+    int32_t last_kernel = FKS_KERNEL_NONE;       /* the simulation kernel of the last call */
+    int32_t last_check_kernel = FKS_KERNEL_NONE; /* the configuration-check kernel of the last check */
     double* d_seg_state = nullptr;
     uint32_t* d_seg_done = nullptr;
     size_t cap_seg_state = 0, cap_seg_done = 0;
@@ -288,7 +289,8 @@ struct fks_context {
     int32_t specialize = 1;
     bool spec_pending = false; /* robot set, its kernel not built yet (built at the first launch that runs it) */
     hipModule_t spec_module = nullptr;
-    hipFunction_t spec_fn = nullptr; /* fks_simulate_shaped of the current robot's shape */
+    hipFunction_t spec_fn = nullptr;       /* fks_simulate_shaped of the current robot's shape */
+    hipFunction_t spec_check_fn = nullptr; /* fks_check_configs_shaped (same module) */
     std::string spec_shape;
     double spec_seconds = 0.0;
     int32_t spec_from_cache = 0;
@@ -354,6 +356,7 @@ static void spec_release(fks_context* ctx) {
     }
     ctx->spec_module = nullptr;
     ctx->spec_fn = nullptr;
+    ctx->spec_check_fn = nullptr;
     ctx->spec_shape.clear();
     ctx->spec_seconds = 0.0;
     ctx->spec_from_cache = 0;
@@ -433,7 +436,8 @@ static fks_status spec_build(fks_context* ctx) {
      * (same launch bounds, same LDS block) is used only if it needs no more registers.  Its
      * count is read from the code object's metadata (the runtime's attribute query reports a
      * different quantity for module kernels than for the library's own) */
-    const int shaped_vgpr = fks_spec::metadata_uint(co->bytes, ".vgpr_count") + fks_spec::metadata_uint(co->bytes, ".agpr_count");
+    const int shaped_vgpr = fks_spec::kernel_metadata_uint(co->bytes, "fks_simulate_shaped", ".vgpr_count") +
+                            std::max(0, fks_spec::kernel_metadata_uint(co->bytes, "fks_simulate_shaped", ".agpr_count"));
     hipFuncAttributes gen{};
     if (hipFuncGetAttributes(&gen, reinterpret_cast<const void*>(kernel_for(ctx->R.type, false, ctx->lean))) != hipSuccess) gen.numRegs = 0;
     /* 512 VGPRs per SIMD lane, allocated in granules of 8 */
@@ -446,6 +450,10 @@ static fks_status spec_build(fks_context* ctx) {
     }
     ctx->spec_module = m;
     ctx->spec_fn = f;
+    /* the configuration check of the same shape, when the module carries it */
+    hipFunction_t fc = nullptr;
+    if (hipModuleGetFunction(&fc, m, "fks_check_configs_shaped") == hipSuccess) ctx->spec_check_fn = fc;
+    (void)hipGetLastError();
     ctx->spec_shape = fks_spec::shape_key(sh);
     ctx->spec_seconds = compiled ? co->compile_seconds : 0.0;
     ctx->spec_from_cache = compiled ? 0 : 1;
@@ -1396,9 +1404,26 @@ fks_status fks_check_config_collision_device(fks_context* ctx, const double* d_c
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, fksd::kCounterWords * sizeof(unsigned long long), s));
     const uint64_t groups_needed = (n + ctx->waves_per_group - 1) / ctx->waves_per_group;
     const uint32_t grid = (uint32_t)((groups_needed < (uint64_t)ctx->grid_groups) ? groups_needed : ctx->grid_groups);
+    /* a batch larger than the resident grid runs the robot's shape-specialised check (built
+     * here if the simulation has not built the module yet; a failure keeps the generic one) */
+    if (ctx->spec_pending && n > (uint64_t)ctx->grid_waves) {
+        ctx->spec_pending = false;
+        const std::string keep = ctx->last_error;
+        if (spec_prepare(ctx) != FKS_OK) ctx->last_error = keep + (keep.empty() ? "" : "; ") + ctx->last_error;
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+    }
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
-    hipLaunchKernelGGL(check_kernel_for(ctx->R.type), dim3(grid), dim3(64 * ctx->waves_per_group), ctx->lds_bytes, s,
-                       static_cast<const fksd::SimArgs*>(ctx->d_args));
+    if (ctx->spec_check_fn) {
+        const fksd::SimArgs* argp = ctx->d_args;
+        void* params[] = {&argp};
+        HIP_TRY(ctx, hipModuleLaunchKernel(ctx->spec_check_fn, grid, 1, 1, 64 * ctx->waves_per_group, 1, 1, (unsigned)ctx->lds_bytes,
+                                           s, params, nullptr));
+        ctx->last_check_kernel = FKS_KERNEL_SHAPED;
+    } else {
+        hipLaunchKernelGGL(check_kernel_for(ctx->R.type), dim3(grid), dim3(64 * ctx->waves_per_group), ctx->lds_bytes, s,
+                           static_cast<const fksd::SimArgs*>(ctx->d_args));
+        ctx->last_check_kernel = FKS_KERNEL_THROUGHPUT;
+    }
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_counters, ctx->d_counters, fksd::kCounterWords * sizeof(unsigned long long),
@@ -1844,6 +1869,7 @@ fks_status fks_get_launch_info(const fks_context* ctx, fks_launch_info* out) {
     out->fk_pair = ctx->fk_pair ? 1 : 0;
     out->lean = ctx->lean ? 1 : 0;
     out->last_kernel = ctx->last_kernel;
+    out->last_check_kernel = ctx->last_check_kernel;
     return FKS_OK;
 }
 

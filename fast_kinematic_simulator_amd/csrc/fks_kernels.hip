@@ -3241,9 +3241,19 @@ __device__ __forceinline__ void set_position(Sim& s, const double* src, double* 
 /* CheckSelfCollisions (SPCS:1324-1396) at extended cells of size `res`: true iff one
  * cell holds points of two geometries whose pair is disallowed (CheckPointsForSelfCollision,
  * SPCS:1277-1322).  Conservative per-geometry key boxes (one lane per geometry) reject
- * pairs; overlapping pairs compare exact keys. */
+ * pairs; overlapping pairs compare exact keys: a point of b can share a cell with a point of
+ * a only if its key lies in a's box (and the a point's in b's), so b's points in a's box are
+ * taken by ballot, their keys held in registers and broadcast one by one (readlane) to the
+ * lanes holding a's points in b's box — no memory round trip per comparison.  env_hit: the
+ * configuration already collides with the environment, so only the error bits of the key
+ * computation (which the reference's keying would raise) are still needed. */
+__device__ __forceinline__ int64_t readlane_i64(int64_t v, int lane) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict__ Ap, const double* shared, double* lds,
-                                                       double* scratch, int ln, const double* Tc, double res) {
+                                                       double* scratch, int ln, const double* Tc, double res, bool env_hit) {
     const SimArgs& A = *Ap;
     const RobotDev& R = A.R;
     double* box = lds + LAY(A).box;
@@ -3308,7 +3318,17 @@ __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict
             keys[3 * i + a] = k;
         }
     }
+    err = wave_or(err);
+    if (env_hit) return err << 1; /* collided either way: the pairs need not be compared */
     wsync();
+    auto in_box = [&](int i, int g) {
+        bool in = true;
+        for (int a = 0; a < 3; ++a) {
+            const double k = (double)keys[3 * i + a];
+            in = in && box[6 * g + a] <= k && k <= box[6 * g + 3 + a];
+        }
+        return in;
+    };
     bool hit = false;
     for (int k = 0; k < RDIM(R, npairs) && !wave_any(hit); ++k) {
         const int a = gp(R.pairs)[2 * k], b = gp(R.pairs)[2 * k + 1];
@@ -3317,13 +3337,82 @@ __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict
         if (!ov) continue;
         const int a0 = (int)gp(R.geom_off)[a], a1 = (int)gp(R.geom_off)[a + 1];
         const int b0 = (int)gp(R.geom_off)[b], b1 = (int)gp(R.geom_off)[b + 1];
-        for (int i = a0 + ln; i < a1; i += kWave) {
-            const int64_t kx = keys[3 * i], ky = keys[3 * i + 1], kz = keys[3 * i + 2];
-            for (int j = b0; j < b1 && !hit; ++j) hit = (keys[3 * j] == kx) && (keys[3 * j + 1] == ky) && (keys[3 * j + 2] == kz);
+        for (int j0 = b0; j0 < b1 && !wave_any(hit); j0 += kWave) {
+            const int j = j0 + ln;
+            const bool jin = j < b1 && in_box(j, a);
+            const int64_t bx = jin ? keys[3 * j] : 0, by = jin ? keys[3 * j + 1] : 0, bz = jin ? keys[3 * j + 2] : 0;
+            const uint64_t mb = __ballot(jin);
+            if (!mb) continue;
+            for (int i0 = a0; i0 < a1 && !wave_any(hit); i0 += kWave) {
+                const int i = i0 + ln;
+                const bool iin = i < a1 && in_box(i, b);
+                if (!wave_any(iin)) continue;
+                const int64_t ax = iin ? keys[3 * i] : 0, ay = iin ? keys[3 * i + 1] : 0, az = iin ? keys[3 * i + 2] : 0;
+                uint64_t m = mb;
+                bool h = false;
+                while (m) {
+                    const int t = __ffsll((unsigned long long)m) - 1;
+                    m &= m - 1ull;
+                    h = h || (ax == readlane_i64(bx, t) && ay == readlane_i64(by, t) && az == readlane_i64(bz, t));
+                }
+                hit = hit || (iin && h);
+            }
         }
     }
-    err = wave_or(err);
     return (err << 1) | (wave_any(hit) ? 1u : 0u);
+}
+
+/* CheckEnvironmentCollision (SPCS:921-981) for the batched configuration check: the
+ * nearest-cell values of NB rounds of points are gathered at once (one memory round trip for
+ * the whole robot at cfg3's 8 rounds, instead of one per pair of rounds), then examined in
+ * point order; EstimateDistance4d only where the nearest value cannot decide, as env_point.
+ * Bytes are counted up to the first colliding point, as the reference reads them. */
+template <int NB>
+__device__ __forceinline__ bool check_env_rounds(const SimArgs& A, const double* T, int ln, uint64_t* lane_bytes) {
+    const RobotDev& R = A.R;
+    const GridDev& g = A.sdf_g;
+    const double thr = A.thr_env;
+    const int P = RDIM(R, P);
+    for (int base = 0; base < P; base += NB * kWave) {
+        float d[NB];
+        uint32_t okm = 0; /* bit k: round k's point of this lane is in the grid */
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            const int i = base + k * kWave + ln;
+            d[k] = A.oob;
+            if (i < P) {
+                const D4 x = xform4(T + 12 * gp(R.point_link)[i], load_point(R, i));
+                int32_t idx[3];
+                if (grid_index(g, x, idx)) {
+                    d[k] = gp(A.sdf)[grid_brick(g, idx[0], idx[1], idx[2])];
+                    okm |= 1u << k;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            if (base + k * kWave >= P) break;
+            const int i = base + k * kWave + ln;
+            uint64_t b = ((okm >> k) & 1u) ? 4 : 0;
+            bool c = false;
+            if (i < P && (double)d[k] < thr) {
+                if ((double)d[k] < thr - g.res) {
+                    c = true;
+                } else {
+                    const D4 x = xform4(T + 12 * gp(R.point_link)[i], load_point(R, i));
+                    bool inb;
+                    c = estimate_distance(A, x, &inb, &b) < thr;
+                }
+            }
+            const uint64_t m = __ballot(c);
+            if (m) {
+                if (ln <= __ffsll((unsigned long long)m) - 1) *lane_bytes += b;
+                return true;
+            }
+            *lane_bytes += b;
+        }
+    }
+    return false;
 }
 
 /* batched CheckConfigCollision (SPCS:1398-1416): one wave per configuration,
@@ -3343,32 +3432,13 @@ __device__ __forceinline__ void check_configs(const SimArgs* __restrict__ args, 
     for (uint64_t c = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < A.n; c += stride) {
         set_position<RT>(s, A.starts + c * (uint64_t)RDIM(R, W), cfg);
         fk<RT>(s, cfg, T);
-        /* CheckEnvironmentCollision: pairs of 64-point rounds, bytes up to the first
-         * colliding point (its loop returns there) */
+        /* CheckEnvironmentCollision: bytes up to the first colliding point (its loop returns
+         * there), eight rounds' nearest-cell reads in flight at once */
         uint64_t lane_bytes = 0;
-        bool env = false;
-        for (int base = 0; base < RDIM(R, P) && !env; base += 2 * kWave) {
-            uint64_t b0 = 0, b1 = 0;
-            double S, G, C;
-            const bool c0 = env_point(A, T, base + ln, &b0, &S, &G, &C);
-            const bool c1 = env_point(A, T, base + kWave + ln, &b1, &S, &G, &C);
-            const uint64_t m0 = __ballot(c0), m1 = __ballot(c1);
-            if (m0) {
-                if (ln <= __ffsll((unsigned long long)m0) - 1) lane_bytes += b0;
-                env = true;
-            } else {
-                lane_bytes += b0;
-                if (m1) {
-                    if (ln <= __ffsll((unsigned long long)m1) - 1) lane_bytes += b1;
-                    env = true;
-                } else {
-                    lane_bytes += b1;
-                }
-            }
-        }
+        const bool env = check_env_rounds<8>(A, T, ln, &lane_bytes);
         uint32_t r = 0;
         if constexpr (RT == FKS_ROBOT_LINKED) {
-            if (RDIM(R, self_possible)) r = config_self_collision(args, s.shared(), s.lds(), s.scratch, ln, T, A.self_res);
+            if (RDIM(R, self_possible)) r = config_self_collision(args, s.shared(), s.lds(), s.scratch, ln, T, A.self_res, env);
         }
         const uint64_t bytes = wave_sum_u64(lane_bytes);
         if (ln == 0) {
@@ -3767,6 +3837,11 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_shaped(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
     simulate_particles<FKS_SHAPE_TYPE, false, false, FKS_SHAPE_LEAN != 0>(args, lds_mem);
+}
+/* the batched CheckConfigCollision of the same shape (same module, same LDS block) */
+extern "C" __global__ void FKS_KERNEL_ATTRS fks_check_configs_shaped(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    check_configs<FKS_SHAPE_TYPE>(args, lds_mem);
 }
 #else
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked(const SimArgs* __restrict__ args) {

@@ -57,6 +57,10 @@ std::shared_ptr<const CodeObject> code_object(const Shape& s, std::string* log, 
  * (MessagePack: the key string followed by a positive integer), e.g. ".vgpr_count"; -1 if
  * absent */
 int metadata_uint(const std::vector<char>& code_object, const char* key);
+/* the same field of the entry of kernel `name` (the module also carries the shaped
+ * configuration check): the first `key` after the entry's ".name" (the keys of a kernel's
+ * metadata map are emitted in sorted order, ".name" before ".sgpr_count" / ".vgpr_count") */
+int kernel_metadata_uint(const std::vector<char>& code_object, const char* name, const char* key);
 
 }  // namespace fks_spec
 

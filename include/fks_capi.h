@@ -456,7 +456,8 @@ typedef struct fks_launch_info {
     int32_t fk_pair;                         /* paired FK of free microsteps */
     int32_t lean;                            /* lean LDS block (skip-proof cache in scratch) */
     int32_t last_kernel;                     /* fks_kernel_kind of the last simulation call */
-    int32_t reserved;
+    int32_t last_check_kernel;               /* ABI 9: of the last batched CheckConfigCollision call
+                                                (FKS_KERNEL_THROUGHPUT: generic, FKS_KERNEL_SHAPED) */
 } fks_launch_info;
 fks_status fks_get_launch_info(const fks_context* ctx, fks_launch_info* out);
 /* Scheduling granularity of fks_forward_simulate*: when a batch holds more particles

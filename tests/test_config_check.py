@@ -166,3 +166,34 @@ def test_config_check_device_entry(fks_lib, oracle_lib):
         assert sim.last_call_counters()["particles"] == 2
     finally:
         sim.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,scale,n", [("cfg2", 8 / 4096, 12288), ("cfg3", 8 / 65536, 12288), ("cfg4", 64 / 1048576, 12288),
+                                          ("cfg5", 8 / 1048576, 6144)])
+def test_shaped_config_check_parity(fks_lib, oracle_lib, name, scale, n):
+    """A batch larger than the resident grid runs the robot's shape-specialised check
+    (fks_check_configs_shaped, built with the simulation kernel's module): bit-exact against
+    the oracle, collided flags, error bits and algorithmic bytes."""
+    import oracle
+    from fast_kinematic_simulator_amd import make_linked_simulator
+
+    wl = W.WORKLOADS[name](scale)
+    wl._env = W.SCENES[name](device=0)  # the GPU build: the host build's bytes, seconds faster at 512^3
+    env = wl.environment()
+    cfgs = _configs(wl, n, seed=13)
+    cfgs[1] = np.nan
+    sim = make_linked_simulator(env, wl.solver, wl.controller_frequency, wl.seed)
+    try:
+        sim.set_robot(wl.robot)
+        assert n > sim.launch_info()["resident_waves"]
+        for inflation in (0.0, 0.5):
+            g = sim.check_config_collisions(wl.robot, cfgs, inflation)
+            assert sim.launch_info()["last_check_kernel"] == "shaped", (sim.launch_info(), sim.specialization())
+            o = oracle.check_config_collision(env, wl.robot, wl.solver, cfgs, inflation)
+            bad = np.nonzero((g["collided"] != o["collided"]) | (g["error_flags"] != o["error_flags"]))[0]
+            assert len(bad) == 0, f"{name} inflation {inflation}: {len(bad)} of {n} differ, first {bad[:8]}"
+            assert sim.last_check_counters()["sdf_bytes"] == int(o["sdf_bytes"].sum())
+            assert 0 < int(g["collided"].sum()) < n
+    finally:
+        sim.close()
