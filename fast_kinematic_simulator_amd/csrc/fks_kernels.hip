@@ -3288,34 +3288,56 @@ __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict
         }
     }
     wsync();
-    bool any = false;
-    for (int k = ln; k < RDIM(R, npairs); k += kWave) {
-        const int a = gp(R.pairs)[2 * k], b = gp(R.pairs)[2 * k + 1];
-        bool ov = true;
-        for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
-        any = any || ov;
+    /* the geometries whose keys matter: those of overlapping pairs, and every geometry whose box
+     * is not finite.  A non-finite point (the only source of FKS_PARTICLE_ERR_KEY_RANGE, which
+     * the reference's keying of every point would raise) lies on a link with a non-finite box,
+     * so keying these gives the error bits of keying all points.  After an environment hit only
+     * the error bits are still needed. */
+    const uint64_t bad_geoms = __ballot(ln < RDIM(R, G) && bad);
+    uint64_t need = bad_geoms;
+    if (!env_hit) {
+        for (int k0 = 0; k0 < RDIM(R, npairs); k0 += kWave) {
+            const int k = k0 + ln;
+            int a = 0, b = 0;
+            bool ov = false;
+            if (k < RDIM(R, npairs)) {
+                a = gp(R.pairs)[2 * k];
+                b = gp(R.pairs)[2 * k + 1];
+                ov = true;
+                for (int i = 0; i < 3; ++i) ov = ov && (box[6 * a + i] <= box[6 * b + 3 + i]) && (box[6 * b + i] <= box[6 * a + 3 + i]);
+            }
+            uint64_t m = __ballot(ov);
+            while (m) {
+                const int bit = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1ull;
+                need |= (1ull << readlane_i32(a, bit)) | (1ull << readlane_i32(b, bit));
+            }
+        }
     }
-    if (!wave_any(any || bad)) return 0u;
-    /* exact keys of every point (LocationToExtendedGridIndex SPCS:1173-1181) */
+    if (!need) return 0u;
+    /* exact keys (LocationToExtendedGridIndex SPCS:1173-1181) of the needed geometries' points */
     int64_t* keys = reinterpret_cast<int64_t*>(scratch + SLAY(A).keys);
     uint32_t err = 0;
-    for (int i = ln; i < RDIM(R, P); i += kWave) {
-        const D4 x = xform4(Tc + 12 * (int)gp(R.point_link)[i], load_point(R, i));
-        const D4 g = xform4(A.env_g.inv, x);
-        const double q[3] = {g.x / res, g.y / res, g.z / res};
-        for (int a = 0; a < 3; ++a) {
-            int64_t k;
-            if (q[a] != q[a] || q[a] == __builtin_huge_val() || q[a] == -__builtin_huge_val()) {
-                err |= FKS_PARTICLE_ERR_KEY_RANGE;
-                k = 0;
-            } else if (q[a] >= 9.0e18) {
-                k = (int64_t)9000000000000000000ll;
-            } else if (q[a] <= -9.0e18) {
-                k = -(int64_t)9000000000000000000ll;
-            } else {
-                k = (int64_t)q[a];
+    for (uint64_t gm = need; gm; gm &= gm - 1ull) {
+        const int g0 = __ffsll((unsigned long long)gm) - 1;
+        for (int i = (int)gp(R.geom_off)[g0] + ln; i < (int)gp(R.geom_off)[g0 + 1]; i += kWave) {
+            const D4 x = xform4(Tc + 12 * (int)gp(R.point_link)[i], load_point(R, i));
+            const D4 g = xform4(A.env_g.inv, x);
+            const double q[3] = {g.x / res, g.y / res, g.z / res};
+            for (int a = 0; a < 3; ++a) {
+                int64_t k;
+                if (q[a] != q[a] || q[a] == __builtin_huge_val() || q[a] == -__builtin_huge_val()) {
+                    err |= FKS_PARTICLE_ERR_KEY_RANGE;
+                    k = 0;
+                } else if (q[a] >= 9.0e18) {
+                    k = (int64_t)9000000000000000000ll;
+                } else if (q[a] <= -9.0e18) {
+                    k = -(int64_t)9000000000000000000ll;
+                } else {
+                    k = (int64_t)q[a];
+                }
+                keys[3 * i + a] = k;
             }
-            keys[3 * i + a] = k;
         }
     }
     err = wave_or(err);

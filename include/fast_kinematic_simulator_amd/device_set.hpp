@@ -107,7 +107,7 @@ class DeviceSet {
     /* the particles each device must get before a batch takes it on (0: automatic =
      * kShardWavesPerDevice x the resident waves of devices[0] for the current robot; 1 shards
      * every batch of at least as many particles as devices over all of them) */
-    static constexpr uint64_t kShardWavesPerDevice = 2;
+    static constexpr uint64_t kShardWavesPerDevice = 3;
     void set_shard_threshold(uint64_t particles_per_device) { shard_threshold_ = particles_per_device; }
     uint64_t shard_threshold() const {
         if (shard_threshold_ > 0) return shard_threshold_;

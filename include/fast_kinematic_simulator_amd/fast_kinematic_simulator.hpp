@@ -349,7 +349,7 @@ class HipParticleContactSimulator : public simple_simulator_interface::Simulator
     fks_context* Context() const { return ctx_; }
     const std::vector<int32_t>& Devices() const { return dev_->devices(); }
     /* the particles each listed device must get before a batch is sharded over it (0:
-     * automatic = twice the resident waves of devices[0] for the current robot: a smaller shard
+     * automatic = three times the resident waves of devices[0] for the current robot: a smaller shard
      * is bounded by its slowest particle's chain); 1 shards every batch over all
      * of Devices() */
     void SetShardThreshold(uint64_t particles_per_device) { dev_->set_shard_threshold(particles_per_device); }

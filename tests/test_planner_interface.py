@@ -300,7 +300,7 @@ def test_planner_interface_sharded_over_device_lists(fks_lib, name):
         assert " active 1 failed 0" in p.stderr, p.stderr
         assert p.stdout == base.stdout, devices
         assert p.normals == base.normals
-    # the automatic threshold (twice one device's resident waves per device) keeps these small
+    # the automatic threshold (three times one device's resident waves per device) keeps these small
     # batches on the first device
     p, *_ = _run(name, devices="0,0")
     assert p.returncode == 0 and "devices 2 sharded 0 over 1" in p.stderr, p.stderr

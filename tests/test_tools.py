@@ -6,6 +6,7 @@ import json
 import os
 
 import numpy as np
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -72,3 +73,19 @@ def test_tail_pmc_summary(tmp_path):
     assert d["share_of_wave_cycles"]["waiting_on_memory_lds_smem (s_waitcnt)"] == 0.5
     assert d["cycles_per_instruction"] == round(3200 / 1600, 2)
     assert s["lone_per_resolver_iteration"]["VALU"] == 100.0
+
+
+@pytest.mark.gpu
+def test_precompile_kernels_fills_the_disk_cache(tmp_path):
+    """tools/precompile_kernels.py: the shapes of the named workloads are built
+    into FKS_KERNEL_CACHE on the GPU host, so a planner's first large call finds them there."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, FKS_KERNEL_CACHE=str(tmp_path / "cache"))
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "precompile_kernels.py"), "--workload", "cfg2"],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["active"] and not line["failed"] and line["shape"].startswith("t0-"), line
+    assert len(list((tmp_path / "cache").glob(line["shape"] + "-*.hsaco"))) == 1
