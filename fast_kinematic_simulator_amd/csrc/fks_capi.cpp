@@ -1227,6 +1227,7 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.skip_enabled = ctx->skip_enabled;
     a.skip_lplus = ctx->skip_lplus;
     a.skip_cmax = ctx->skip_cmax;
+    a.skip_wm_inv = ctx->skip_lplus > 0.0 ? (1.0 / (std::sqrt(3.0) * ctx->skip_lplus)) * (1.0 - 1e-12) : 0.0;
     a.R = ctx->R;
     a.S = ctx->params;
     a.dt = 1.0 / ctx->frequency;

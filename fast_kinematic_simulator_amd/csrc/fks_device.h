@@ -304,6 +304,7 @@ struct SimArgs {
     int32_t skip_enabled;
     int32_t skip_pad;
     double skip_lplus, skip_cmax;
+    double skip_wm_inv; /* 1 / (sqrt(3) * skip_lplus), rounded down (the travel watermark, FKS_WATERMARK) */
     RobotDev R;
     fks_solver_params S;
     double dt;               /* simulation_controller_interval_ = 1/frequency  (SPCS:427)   */

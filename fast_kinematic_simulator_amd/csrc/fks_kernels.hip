@@ -1112,6 +1112,43 @@ __device__ __forceinline__ void claim_fence() { __builtin_amdgcn_fence(__ATOMIC_
 constexpr uint32_t kSegClaimed = 0x80000000u; /* seg_done[p]: segment v is being run */
 enum { kSkipCheck = 1, kSkipCorrections = 2 };
 
+/* ---- the travel watermark (FKS_WATERMARK: linked shape builds of <= 8 rounds) ----
+ * A cheaper route to "every round of the environment check is provably free" for the common
+ * free microstep.  The wave keeps `travel`, an upper bound of the path length any robot point
+ * has covered since the particle's start: every microstep adds sum_d (|ustep_d| + noise bound_d)
+ * * lever_d (the actuator moves dof d by at most its clamped command plus the noise bound,
+ * UNC:77-90; clamping to the joint limits and wrapping only shorten it; lever_d as for the
+ * microstep-motion proof), every resolver correction sum_d |step_d| * lever_d.  A round's points
+ * have therefore moved at most travel - travel_r since the state cached at travel_r, and the
+ * check proof (round_proof, kSkipCheck) solved for the motion gives the largest motion slack_r
+ * it covers; rstate[15] holds travel_r + slack_r (refreshed whenever the per-round proof
+ * succeeds with a tighter bound: travel + slack_r - bm_r), and the watermark is their minimum.
+ * travel < watermark proves every round free with two LDS reads.  A new particle starts with no
+ * entries (-inf), except rounds no dof moves whose cached state is free (+inf: they never move).
+ * Misc slots: 6 travel, 7 the current step's per-microstep bound, 37 the watermark (NaN: to be
+ * recomputed from the entries by the next per-round proof). */
+#ifndef FKS_WATERMARK
+#define FKS_WATERMARK 0
+#endif
+#if FKS_WATERMARK && FKS_PAR_PROOF && defined(FKS_SHAPE_P) && FKS_SHAPE_TYPE == 0 && !FKS_NO_SKIP_PROOFS
+#define FKS_WM ((FKS_SHAPE_P + 63) / 64 <= 8)
+#else
+#define FKS_WM 0
+#endif
+enum { kMiscTravel = 6, kMiscStepBound = 7, kMiscWatermark = 37 };
+/* the largest motion (meters) of a round's points since its state st was cached that the check
+ * proof still covers: round_proof's two kSkipCheck routes solved for the bound b (cells),
+ * rounded down; -inf when neither route holds at b = 0 */
+__device__ __forceinline__ double round_slack_m(const SimArgs& A, double S, double G, double C) {
+    /* (d / lp - 2) / sqrt(3) with d = S / res - cmax - 1e-9; skip_wm_inv = 1 / (sqrt(3) lp) rounded
+     * down, 2 / sqrt(3) rounded up (lp >= 1e-6 whenever the proofs are enabled) */
+    const double d = S * A.sdf_g.inv_res - A.skip_cmax - 1e-9;
+    const double r1 = (d > 0.0) ? dmin(G - 1e-6, d * A.skip_wm_inv - 1.1547005383792517) : -__builtin_huge_val();
+    const double r2 = (S >= A.thr_env) ? C - 1e-9 : -__builtin_huge_val();
+    const double b = dmax(r1, r2);
+    return (b > 0.0) ? (b * (1.0 - 1e-6) - 1e-9) * A.sdf_g.res : -__builtin_huge_val();
+}
+
 /* (link, radius) of round r < 64 from the workgroup's LDS copy of R.rounds */
 __device__ __forceinline__ RoundDev lds_round(const Sim& s, int r) {
     RoundDev o;
@@ -1170,6 +1207,22 @@ __device__ __forceinline__ uint64_t skippable_rounds8(Sim& s, const double* T, i
     const uint64_t neq = __ballot(!eq);
     const bool still = ((neq >> (8 * r)) & 0xffull) == 0ull;
     const bool sk = usable && round_proof(A, st, bm, still, what);
+#if FKS_WM
+    if (what == kSkipCheck) {
+        /* refresh the proven rounds' watermark entries with the tight bound, then the minimum */
+        double entry = valid_r ? st[15] : __builtin_huge_val();
+        double* mw = s.lds() + LAY(A).misc;
+        if (FKS_WATERMARK == 1 && sk && e == 0 && entry != __builtin_huge_val()) {
+            const double fresh = mw[kMiscTravel] + (round_slack_m(A, st[12], st[13], st[14]) - bm);
+            if (fresh > entry) {
+                entry = fresh;
+                s.rstate[kRoundState * r + 15] = fresh;
+            }
+        }
+        const double w = wave_min((e == 0 || !valid_r) ? entry : __builtin_huge_val());
+        if (ln == 0) mw[kMiscWatermark] = w;
+    }
+#endif
     const uint64_t m = __ballot(sk && e == 0) & 0x0101010101010101ull;
     return (m * 0x0102040810204080ull) >> 56;
 }
@@ -1261,6 +1314,13 @@ __device__ __forceinline__ void round_update(Sim& s, int r, const double* T, dou
         st[12] = smin;
         st[13] = gmin;
         st[14] = cmin;
+#if FKS_WM && !(FKS_WM_OFF & 4)
+        /* a round no dof moves keeps a free state for good; any other is covered up to travel + slack */
+        double* mw = s.lds() + LAY(A).misc;
+        const bool fixed = gp(A.R.link_dof_mask)[rd.link] == 0ull;
+        st[15] = (fixed && smin >= A.thr_env) ? __builtin_huge_val() : mw[kMiscTravel] + round_slack_m(A, smin, gmin, cmin);
+        mw[kMiscWatermark] = __builtin_nan("");
+#endif
     }
 }
 
@@ -1368,6 +1428,10 @@ __device__ FKS_SHAPE_INLINE bool env_collision(Sim& s, const double* T) {
     uint64_t skip = skippable_rounds(s, T, kSkipCheck);
     asm volatile("" ::: "memory");
     skip &= skippable_rounds(s, T, kSkipCheck) | skip;
+#elif FKS_WM
+    /* travel below the watermark: every round free without the per-round proof */
+    const double* mw = s.lds() + LAY(A).misc;
+    const uint64_t skip = (mw[kMiscTravel] < mw[kMiscWatermark]) ? ~0ull : skippable_rounds(s, T, kSkipCheck);
 #else
     const uint64_t skip = skippable_rounds(s, T, kSkipCheck);
 #endif
@@ -2953,6 +3017,25 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
         const double bound = bfly_sum(0.0 + term);
         proven = !FKS_NO_SKIP_PROOFS && bound * (1.0 + 1e-6) + 1e-12 < A.allowed_micro;
     }
+#ifndef FKS_WM_OFF
+#define FKS_WM_OFF 0
+#endif
+#if FKS_WM && !(FKS_WM_OFF & 1)
+    {
+        /* the travel bound of one noisy microstep of this step: |clamped command| + noise bound
+         * per dof (UNC:77-90), through the lever arms; a sampled actuator has no such bound */
+        double nb = 0.0;
+        if (ln < D) {
+            const fks_dof_controller& ct = s.ctrl()[ln];
+            const double vmax = dabs(ct.velocity_limit);
+            nb = fks_control::actuator_noise_bound(clamp(ustep[ln], -vmax, vmax), dabs(ct.max_actuator_proportional_noise),
+                                                   dabs(ct.max_actuator_minimum_noise), vmax);
+        }
+        const double tw = (ln < D) ? (dabs(ustep[ln]) + nb) * gp(R.dof_lever)[ln] : 0.0;
+        const double B = R.sampled_mask ? __builtin_huge_val() : bfly_sum(0.0 + tw) * (1.0 + 1e-6) + 1e-12;
+        if (ln == 0) s.lds()[LAY(A).misc + kMiscStepBound] = B;
+    }
+#endif
     if (!proven) {
         apply_input<RT>(s, cfg, ustep, cfg_tmp, false, 0);
         fk<RT>(s, cfg_tmp, Ttmp);
@@ -3035,6 +3118,12 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                 fk<RT>(s, cfg, Tcur);
         }
         tock(s, FKS_PHASE_MICRO_FK, t0);
+#if FKS_WM
+        if (ln == 0) {
+            double* mw = s.lds() + LAY(A).misc;
+            mw[kMiscTravel] = mw[kMiscTravel] + mw[kMiscStepBound];
+        }
+#endif
         bool in_collision = check_collision<RT>(s, Tprev, Tcur, cfg);
         if (s.err) return 1;
         if (in_collision) pair_ready = false; /* the resolver reuses cfg_tmp / Ttmp */
@@ -3116,6 +3205,18 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                     wsync();
                     fk<RT>(s, cfg_act, Tcur);
                 }
+#if FKS_WM && !(FKS_WM_OFF & 2)
+                {
+                    /* the correction moved the robot by at most sum_d |step_d| * lever_d */
+                    const double* stp = applied ? x : real;
+                    const double tc = (ln < D) ? dabs(stp[ln]) * gp(R.dof_lever)[ln] : 0.0;
+                    const double inc = bfly_sum(0.0 + tc) * (1.0 + 1e-6) + 1e-12;
+                    if (ln == 0) {
+                        double* mw = s.lds() + LAY(A).misc;
+                        mw[kMiscTravel] = mw[kMiscTravel] + inc;
+                    }
+                }
+#endif
                 tock(s, FKS_PHASE_RESOLVE_APPLY, t0);
                 in_collision = check_collision<RT>(s, Tprev, Tcur, cfg_act);
                 if (s.err) return 1;
@@ -3457,10 +3558,16 @@ __device__ __forceinline__ void check_configs(const SimArgs* __restrict__ args, 
         /* CheckEnvironmentCollision: bytes up to the first colliding point (its loop returns
          * there), eight rounds' nearest-cell reads in flight at once */
         uint64_t lane_bytes = 0;
+#if defined(FKS_PROBE_CHECK_NO_ENV)
+        const bool env = false; /* A/B probe only: what the environment leg costs (results change) */
+#else
         const bool env = check_env_rounds<8>(A, T, ln, &lane_bytes);
+#endif
         uint32_t r = 0;
         if constexpr (RT == FKS_ROBOT_LINKED) {
+#if !defined(FKS_PROBE_CHECK_NO_SELF) /* A/B probe only: what the self-collision leg costs */
             if (RDIM(R, self_possible)) r = config_self_collision(args, s.shared(), s.lds(), s.scratch, ln, T, A.self_res, env);
+#endif
         }
         const uint64_t bytes = wave_sum_u64(lane_bytes);
         if (ln == 0) {
@@ -3557,6 +3664,9 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     s.rstate = LEAN ? s.scratch + SLAY(A).rstate : s.lds() + LAY(A).rstate;
     s.selfref = LEAN ? s.scratch + SLAY(A).selfref : s.lds() + LAY(A).selfref;
     if (s.lane() < RDIM(R, nrounds)) s.rstate[kRoundState * s.lane() + 12] = kInvalidRound;
+#if FKS_WM
+    if (s.lane() < RDIM(R, nrounds)) s.rstate[kRoundState * s.lane() + 15] = -__builtin_huge_val();
+#endif
     wsync();
     const int ln = s.lane();
     const int W = RDIM(R, W), D = RDIM(R, D);
@@ -3688,6 +3798,15 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             } else {
                 if (ln < 12) cfg[ln] = start[ln];
             }
+#if FKS_WM
+            /* a new particle: no travel, no watermark entries (except rounds that never move) */
+            if (ln < RDIM(R, nrounds) && s.rstate[kRoundState * ln + 15] != __builtin_huge_val())
+                s.rstate[kRoundState * ln + 15] = -__builtin_huge_val();
+            if (ln == 0) {
+                s.lds()[LAY(A).misc + kMiscTravel] = 0.0;
+                s.lds()[LAY(A).misc + kMiscWatermark] = __builtin_nan("");
+            }
+#endif
         } else {
             /* resume: configuration from out_q, controller state and per-particle totals
              * from seg_state (bit-exact: the step loop below recomputes FK at its start) */
@@ -3701,6 +3820,13 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             /* the particle's own skip-proof cache (the rounds' last full evaluations) */
             const int nrc = kRoundState * (RDIM(R, nrounds) < kWave ? RDIM(R, nrounds) : kWave);
             for (int e = ln; e < nrc; e += kWave) s.rstate[e] = load_coherent(st + 2 * D + 4 + e);
+#if FKS_WM
+            /* the particle's travel so far (its entries came back with the cache) */
+            if (ln == 0) {
+                s.lds()[LAY(A).misc + kMiscTravel] = load_coherent(st + 2 * D + 3);
+                s.lds()[LAY(A).misc + kMiscWatermark] = __builtin_nan("");
+            }
+#endif
         }
         wsync();
         double* Tcur = s.lds() + LAY(*s.A).Tcur;
@@ -3775,6 +3901,9 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                 store_coherent_u64(sw, (collided ? 1ull : 0ull) | (any_failed ? 2ull : 0ull));
                 store_coherent_u64(sw + 1, micro_total);
                 store_coherent_u64(sw + 2, resolver_total);
+#if FKS_WM
+                store_coherent(st + 2 * D + 3, s.lds()[LAY(A).misc + kMiscTravel]);
+#endif
             }
             const int nrc = kRoundState * (RDIM(R, nrounds) < kWave ? RDIM(R, nrounds) : kWave);
             for (int e = ln; e < nrc; e += kWave) store_coherent(st + 2 * D + 4 + e, s.rstate[e]);

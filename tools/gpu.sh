@@ -5,6 +5,7 @@
 #   suite              pytest -m gpu (whole suite)                  -> <tag>_pytest_gpu.log
 #   suitelib:<lib>     the same suite against a variant library  -> <tag>_pytest_gpu_<lib>.log
 #   tests:<file>       pytest -m gpu of one test file (tests/<file>.py) -> <tag>_pytest_<file>.log
+#   testslib:<file>:<lib>  the same against a variant library -> <tag>_pytest_<file>_<lib>.log
 #   smoke              __graft_entry__.smoke()                      -> <tag>_smoke.log
 #   bench[:cfgN]       bench.py (default workload, or --workload cfgN) -> <tag>_bench[_cfgN].json
 #   others             bench lines of cfg1 / cfg2 / cfg4 / cfg5
@@ -45,6 +46,7 @@ run_task() {
   suite) timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/${TAG}_pytest_gpu.log 2>&1 ;;
   suitelib:*) l=$(lib ${1#suitelib:}); FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/${TAG}_pytest_gpu_$(basename $l .so).log 2>&1 ;;
   tests:*) f=${1#tests:}; timeout -k 10 600 python -u -m pytest tests/$f.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/${TAG}_pytest_$f.log 2>&1 ;;
+  testslib:*) spec=${1#testslib:}; f=${spec%%:*}; l=$(lib ${spec#*:}); FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1 timeout -k 10 600 python -u -m pytest tests/$f.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/${TAG}_pytest_${f}_$(basename $l .so).log 2>&1 ;;
   smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1 ;;
   bench) timeout -k 10 400 python bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err ;;
   bench:*) w=${1#bench:}; timeout -k 10 300 python bench.py --workload $w --no-config-check > $O/${TAG}_bench_$w.json 2> $O/${TAG}_bench_$w.err ;;

@@ -36,7 +36,9 @@ def main():
         line = json.loads(p.stdout.strip().splitlines()[-1])
         print(json.dumps({"lib": os.path.basename(lib) + ("+" + flag if flag else ""), "value": line["value"], "kernel_ms": line["roofline"]["avg_kernel_ms"],
                           "frac": line["roofline"]["frac"], "error_particles": line["config"].get("error_particles"),
-                          "busy": line.get("wave_slots", {}).get("busy_fraction"), "phases": line.get("kernel_phases")}),
+                          "busy": line.get("wave_slots", {}).get("busy_fraction"), "phases": line.get("kernel_phases"),
+                          "config_check": (line.get("config_check") or {}).get("value"),
+                          "config_check_ms": (line.get("config_check") or {}).get("kernel_ms")}),
               flush=True)
 
 
