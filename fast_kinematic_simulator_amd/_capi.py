@@ -198,7 +198,7 @@ class SpecializationInfo(ctypes.Structure):
 
 
 class LaunchInfo(ctypes.Structure):
-    """fks_launch_info (ABI 9)"""
+    """fks_launch_info (ABI 10)"""
     _fields_ = [
         ("resident_waves", c_uint32),
         ("waves_per_group", c_uint32),
@@ -209,6 +209,8 @@ class LaunchInfo(ctypes.Structure):
         ("lean", c_int32),
         ("last_kernel", c_int32),
         ("last_check_kernel", c_int32),
+        ("cooperative_resident_particles", c_uint32),
+        ("cooperative_waves_per_particle", c_uint32),
     ]
 
     def as_dict(self):
@@ -218,7 +220,7 @@ class LaunchInfo(ctypes.Structure):
         return d
 
 
-KERNEL_KINDS = {0: "none", 1: "throughput", 2: "small_batch", 3: "shaped", 4: "traced", 5: "individual"}
+KERNEL_KINDS = {0: "none", 1: "throughput", 2: "small_batch", 3: "shaped", 4: "traced", 5: "individual", 6: "cooperative"}
 
 
 class Trace(ctypes.Structure):
@@ -321,6 +323,7 @@ PROTOTYPES = [
     ("fks_set_segment_steps", c_int32, [c_void_p, c_uint32]),
     ("fks_set_segment_policy", c_int32, [c_void_p, c_uint32, c_uint32]),
     ("fks_set_small_batch_kernel", c_int32, [c_void_p, c_int32]),
+    ("fks_set_cooperative_waves", c_int32, [c_void_p, c_int32]),
     ("fks_set_specialization", c_int32, [c_void_p, c_int32]),
     ("fks_get_launch_info", c_int32, [c_void_p, POINTER(LaunchInfo)]),
     ("fks_get_specialization", c_int32, [c_void_p, POINTER(SpecializationInfo)]),

@@ -39,6 +39,9 @@ extern "C" __global__ void fks_simulate_se3_traced(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_small(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se2_small(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_se3_small(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_linked_coop(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_se2_coop(const fksd::SimArgs* args);
+extern "C" __global__ void fks_simulate_se3_coop(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_lean(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_lean_indiv(const fksd::SimArgs* args);
 extern "C" __global__ void fks_simulate_linked_lean_traced(const fksd::SimArgs* args);
@@ -89,6 +92,16 @@ sim_kernel_t small_kernel_for(int robot_type) {
         case FKS_ROBOT_SE2: return fks_simulate_se2_small;
         case FKS_ROBOT_SE3: return fks_simulate_se3_small;
         default: return fks_simulate_linked_small;
+    }
+}
+
+/* the cooperative instantiation (one particle per workgroup) for batches of at most one
+ * particle per resident workgroup */
+sim_kernel_t coop_kernel_for(int robot_type) {
+    switch (robot_type) {
+        case FKS_ROBOT_SE2: return fks_simulate_se2_coop;
+        case FKS_ROBOT_SE3: return fks_simulate_se3_coop;
+        default: return fks_simulate_linked_coop;
     }
 }
 
@@ -243,6 +256,9 @@ struct fks_context {
     uint32_t grid_waves = 0;
     uint32_t waves_per_cu = 0;     /* resident waves per CU of the layout (LDS and registers) */
     uint32_t small_grid_waves = 0; /* resident waves of the small-batch kernel (0: none for this layout) */
+    uint32_t coop_particles = 0;   /* resident workgroups (particles) of the cooperative kernel (0: none) */
+    uint32_t coop_waves = 0;       /* its waves per workgroup */
+    size_t coop_lds_bytes = 0;
     uint32_t grid_groups = 0;
     uint32_t waves_per_group = fksd::kWavesPerGroup;
     size_t lds_bytes = 0;
@@ -274,6 +290,7 @@ struct fks_context {
     uint32_t heavy_priority = 1;
     int32_t individual_jacobians = 0; /* fks_set_individual_jacobians (SPCS:420-423) */
     int32_t small_batch = 1;          /* fks_set_small_batch_kernel */
+    int32_t cooperative = 0;          /* fks_set_cooperative_waves (opt-in: DESIGN.md §5.4) */
     bool fk_pair = false;             /* paired FK of free microsteps (fks_set_robot) */
     bool lean = false;                /* lean LDS block + lean kernels (fks_set_robot) */
     uint32_t standard_resident_waves = 0; /* resident waves of the non-lean layout (fks_get_launch_info) */
@@ -762,6 +779,28 @@ static fks_status launch_layout(fks_context* ctx, const fksd::RobotDev& R) {
             nk > 0)
             ctx->small_grid_waves = std::min<uint32_t>((uint32_t)(cus * nk) * wpg, ctx->grid_waves);
     }
+    /* the cooperative kernel: one wave's block plus the mailbox per workgroup, its workgroup
+     * size from its launch bound (a build's FKS_COOP_WAVES); each workgroup uses one wave's
+     * workspace, so at most grid_waves of them */
+    ctx->coop_particles = 0;
+    ctx->coop_waves = 0;
+    ctx->coop_lds_bytes = 0;
+    if (!lean && R.nrounds <= fksd::kCoopMaxRounds) {
+        const fksd::LdsLayout l = fksd::make_lds_layout(R.L, R.J, R.D, R.W, R.G, R.nrounds, pair);
+        const size_t cb = ((size_t)l.shared_total + l.total + fksd::kCoopBoxDoubles) * sizeof(double);
+        hipFuncAttributes fa{};
+        int nk = 0;
+        if (cb <= 160 * 1024 && hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(coop_kernel_for(R.type))) == hipSuccess &&
+            fa.maxThreadsPerBlock >= 128 &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nk, reinterpret_cast<const void*>(coop_kernel_for(R.type)),
+                                                         fa.maxThreadsPerBlock, cb) == hipSuccess &&
+            nk > 0) {
+            ctx->coop_waves = (uint32_t)fa.maxThreadsPerBlock / 64u;
+            ctx->coop_lds_bytes = cb;
+            ctx->coop_particles = std::min<uint32_t>((uint32_t)(cus * nk), ctx->grid_waves);
+        }
+    }
+    (void)hipGetLastError();
     ctx->scratch_per_wave = scratch_per_wave;
     return FKS_OK;
 }
@@ -1227,7 +1266,6 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
     a.skip_enabled = ctx->skip_enabled;
     a.skip_lplus = ctx->skip_lplus;
     a.skip_cmax = ctx->skip_cmax;
-    a.skip_wm_inv = ctx->skip_lplus > 0.0 ? (1.0 / (std::sqrt(3.0) * ctx->skip_lplus)) * (1.0 - 1e-12) : 0.0;
     a.R = ctx->R;
     a.S = ctx->params;
     a.dt = 1.0 / ctx->frequency;
@@ -1309,28 +1347,35 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
                                                                                   : ctx->grid_groups);
     /* a batch that fits the small-batch kernel's resident waves, whole particles, plain
      * simulation: that kernel (every particle has its wave from the start either way) */
-    const bool small = ctx->small_batch && !tr && !ctx->individual_jacobians && !ctx->lean && a.nseg == 1 &&
+    const bool coop = ctx->small_batch && ctx->cooperative && !tr && !ctx->individual_jacobians && !ctx->lean && a.nseg == 1 && n > 0 &&
+                      n <= (uint64_t)ctx->coop_particles;
+    const bool small = !coop && ctx->small_batch && !tr && !ctx->individual_jacobians && !ctx->lean && a.nseg == 1 &&
                        n <= (uint64_t)ctx->small_grid_waves;
     /* the plain throughput path runs the robot's shape-specialised kernel: built (or fetched
      * from a cache) here at the first such launch; a failure keeps the generic kernel and is
      * reported by fks_get_specialization / fks_get_last_error, not by this call */
-    if (ctx->spec_pending && !tr && !small && !ctx->individual_jacobians) {
+    if (ctx->spec_pending && !tr && !small && !coop && !ctx->individual_jacobians) {
         ctx->spec_pending = false;
         const std::string keep = ctx->last_error;
         if (spec_prepare(ctx) != FKS_OK) ctx->last_error = keep + (keep.empty() ? "" : "; ") + ctx->last_error;
         HIP_TRY(ctx, hipSetDevice(ctx->device));
     }
-    const bool shaped = ctx->spec_fn && !tr && !small && !ctx->individual_jacobians;
+    const bool shaped = ctx->spec_fn && !tr && !small && !coop && !ctx->individual_jacobians;
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
     ctx->last_kernel = tr ? FKS_KERNEL_TRACED
                           : (shaped ? FKS_KERNEL_SHAPED
-                                    : (small ? FKS_KERNEL_SMALL_BATCH : (ctx->individual_jacobians ? FKS_KERNEL_INDIVIDUAL : FKS_KERNEL_THROUGHPUT)));
+                                    : (coop ? FKS_KERNEL_COOPERATIVE
+                                            : (small ? FKS_KERNEL_SMALL_BATCH
+                                                     : (ctx->individual_jacobians ? FKS_KERNEL_INDIVIDUAL : FKS_KERNEL_THROUGHPUT))));
     if (shaped) {
         const fksd::SimArgs* argp = ctx->d_args;
         void* params[] = {&argp};
         HIP_TRY(ctx, hipModuleLaunchKernel(ctx->spec_fn, grid, 1, 1, 64 * ctx->waves_per_group, 1, 1, (unsigned)ctx->lds_bytes, s,
                                            params, nullptr));
         ctx->spec_launches++;
+    } else if (coop) {
+        hipLaunchKernelGGL(coop_kernel_for(ctx->R.type), dim3((uint32_t)n), dim3(64 * ctx->coop_waves), ctx->coop_lds_bytes, s,
+                           static_cast<const fksd::SimArgs*>(ctx->d_args));
     } else {
         hipLaunchKernelGGL(tr ? traced_kernel_for(ctx->R.type, ctx->lean)
                               : (small ? small_kernel_for(ctx->R.type) : kernel_for(ctx->R.type, ctx->individual_jacobians != 0, ctx->lean)),
@@ -1810,6 +1855,12 @@ fks_status fks_set_small_batch_kernel(fks_context* ctx, int32_t enabled) {
     return FKS_OK;
 }
 
+fks_status fks_set_cooperative_waves(fks_context* ctx, int32_t enabled) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    ctx->cooperative = enabled ? 1 : 0;
+    return FKS_OK;
+}
+
 fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_step, uint32_t heavy_priority) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
     if (heavy_resolver_per_step > 65536u) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "heavy_resolver_per_step > 65536");
@@ -1871,6 +1922,8 @@ fks_status fks_get_launch_info(const fks_context* ctx, fks_launch_info* out) {
     out->lean = ctx->lean ? 1 : 0;
     out->last_kernel = ctx->last_kernel;
     out->last_check_kernel = ctx->last_check_kernel;
+    out->cooperative_resident_particles = ctx->coop_particles;
+    out->cooperative_waves_per_particle = ctx->coop_waves;
     return FKS_OK;
 }
 

@@ -134,6 +134,26 @@ constexpr int kMaxWavesPerGroup = 8;
 /* the throughput kernels' register budget: amdgpu_waves_per_eu(FKS_WAVES_PER_EU) in
  * fks_kernels.hip, 5 waves per SIMD = 96 VGPRs */
 constexpr int kThroughputWavesPerEU = 5;
+/* cooperative small batches (fks_simulate_<family>_coop, fks_set_cooperative_waves): one
+ * particle per workgroup of kCoopWaves waves that share its point loops through a CoopBox
+ * behind the leader's LDS block; robots of up to kCoopMaxRounds 64-point rounds */
+constexpr int kCoopWaves = 8;
+constexpr int kMaxCoopWaves = 8;
+constexpr int kCoopMaxRounds = 16;
+struct CoopBox {
+    uint32_t cmd;
+    uint32_t self_nonempty;
+    uint32_t tc_off, tp_off, cfg_off; /* offsets (doubles) into the leader's LDS block */
+    uint32_t pad;
+    uint64_t work;                    /* the rounds handed out (bit r), taken in rank order */
+    uint64_t skip;                    /* corrections: the proven rounds (collect_corrections' skip mask) */
+    uint64_t cmask;                   /* environment: the rounds holding a colliding point */
+    uint32_t cnt[kCoopMaxRounds];     /* environment: a round's bytes as the sequential loop counts them;
+                                         corrections: its row count */
+    uint32_t err[kMaxCoopWaves];      /* corrections: each helper's error bits */
+    uint64_t selfk[kMaxCoopWaves];    /* corrections: each helper's self-corrected points */
+};
+constexpr uint32_t kCoopBoxDoubles = (uint32_t)((sizeof(CoopBox) + 7) / 8);
 struct LdsLayout {
     uint32_t joints, ctrl, base, dofj, gbox, gpairs, rounds, shared_total;
     uint32_t rstate, noise, noise_err, Tcur, Tprev, Ttmp, jm, cfg, cfg_work, cfg_res, cfg_prev, cfg_tmp, cfg_act, tgt, u,
@@ -304,7 +324,6 @@ struct SimArgs {
     int32_t skip_enabled;
     int32_t skip_pad;
     double skip_lplus, skip_cmax;
-    double skip_wm_inv; /* 1 / (sqrt(3) * skip_lplus), rounded down (the travel watermark, FKS_WATERMARK) */
     RobotDev R;
     fks_solver_params S;
     double dt;               /* simulation_controller_interval_ = 1/frequency  (SPCS:427)   */

@@ -1112,43 +1112,6 @@ __device__ __forceinline__ void claim_fence() { __builtin_amdgcn_fence(__ATOMIC_
 constexpr uint32_t kSegClaimed = 0x80000000u; /* seg_done[p]: segment v is being run */
 enum { kSkipCheck = 1, kSkipCorrections = 2 };
 
-/* ---- the travel watermark (FKS_WATERMARK: linked shape builds of <= 8 rounds) ----
- * A cheaper route to "every round of the environment check is provably free" for the common
- * free microstep.  The wave keeps `travel`, an upper bound of the path length any robot point
- * has covered since the particle's start: every microstep adds sum_d (|ustep_d| + noise bound_d)
- * * lever_d (the actuator moves dof d by at most its clamped command plus the noise bound,
- * UNC:77-90; clamping to the joint limits and wrapping only shorten it; lever_d as for the
- * microstep-motion proof), every resolver correction sum_d |step_d| * lever_d.  A round's points
- * have therefore moved at most travel - travel_r since the state cached at travel_r, and the
- * check proof (round_proof, kSkipCheck) solved for the motion gives the largest motion slack_r
- * it covers; rstate[15] holds travel_r + slack_r (refreshed whenever the per-round proof
- * succeeds with a tighter bound: travel + slack_r - bm_r), and the watermark is their minimum.
- * travel < watermark proves every round free with two LDS reads.  A new particle starts with no
- * entries (-inf), except rounds no dof moves whose cached state is free (+inf: they never move).
- * Misc slots: 6 travel, 7 the current step's per-microstep bound, 37 the watermark (NaN: to be
- * recomputed from the entries by the next per-round proof). */
-#ifndef FKS_WATERMARK
-#define FKS_WATERMARK 0
-#endif
-#if FKS_WATERMARK && FKS_PAR_PROOF && defined(FKS_SHAPE_P) && FKS_SHAPE_TYPE == 0 && !FKS_NO_SKIP_PROOFS
-#define FKS_WM ((FKS_SHAPE_P + 63) / 64 <= 8)
-#else
-#define FKS_WM 0
-#endif
-enum { kMiscTravel = 6, kMiscStepBound = 7, kMiscWatermark = 37 };
-/* the largest motion (meters) of a round's points since its state st was cached that the check
- * proof still covers: round_proof's two kSkipCheck routes solved for the bound b (cells),
- * rounded down; -inf when neither route holds at b = 0 */
-__device__ __forceinline__ double round_slack_m(const SimArgs& A, double S, double G, double C) {
-    /* (d / lp - 2) / sqrt(3) with d = S / res - cmax - 1e-9; skip_wm_inv = 1 / (sqrt(3) lp) rounded
-     * down, 2 / sqrt(3) rounded up (lp >= 1e-6 whenever the proofs are enabled) */
-    const double d = S * A.sdf_g.inv_res - A.skip_cmax - 1e-9;
-    const double r1 = (d > 0.0) ? dmin(G - 1e-6, d * A.skip_wm_inv - 1.1547005383792517) : -__builtin_huge_val();
-    const double r2 = (S >= A.thr_env) ? C - 1e-9 : -__builtin_huge_val();
-    const double b = dmax(r1, r2);
-    return (b > 0.0) ? (b * (1.0 - 1e-6) - 1e-9) * A.sdf_g.res : -__builtin_huge_val();
-}
-
 /* (link, radius) of round r < 64 from the workgroup's LDS copy of R.rounds */
 __device__ __forceinline__ RoundDev lds_round(const Sim& s, int r) {
     RoundDev o;
@@ -1207,22 +1170,6 @@ __device__ __forceinline__ uint64_t skippable_rounds8(Sim& s, const double* T, i
     const uint64_t neq = __ballot(!eq);
     const bool still = ((neq >> (8 * r)) & 0xffull) == 0ull;
     const bool sk = usable && round_proof(A, st, bm, still, what);
-#if FKS_WM
-    if (what == kSkipCheck) {
-        /* refresh the proven rounds' watermark entries with the tight bound, then the minimum */
-        double entry = valid_r ? st[15] : __builtin_huge_val();
-        double* mw = s.lds() + LAY(A).misc;
-        if (FKS_WATERMARK == 1 && sk && e == 0 && entry != __builtin_huge_val()) {
-            const double fresh = mw[kMiscTravel] + (round_slack_m(A, st[12], st[13], st[14]) - bm);
-            if (fresh > entry) {
-                entry = fresh;
-                s.rstate[kRoundState * r + 15] = fresh;
-            }
-        }
-        const double w = wave_min((e == 0 || !valid_r) ? entry : __builtin_huge_val());
-        if (ln == 0) mw[kMiscWatermark] = w;
-    }
-#endif
     const uint64_t m = __ballot(sk && e == 0) & 0x0101010101010101ull;
     return (m * 0x0102040810204080ull) >> 56;
 }
@@ -1314,13 +1261,6 @@ __device__ __forceinline__ void round_update(Sim& s, int r, const double* T, dou
         st[12] = smin;
         st[13] = gmin;
         st[14] = cmin;
-#if FKS_WM && !(FKS_WM_OFF & 4)
-        /* a round no dof moves keeps a free state for good; any other is covered up to travel + slack */
-        double* mw = s.lds() + LAY(A).misc;
-        const bool fixed = gp(A.R.link_dof_mask)[rd.link] == 0ull;
-        st[15] = (fixed && smin >= A.thr_env) ? __builtin_huge_val() : mw[kMiscTravel] + round_slack_m(A, smin, gmin, cmin);
-        mw[kMiscWatermark] = __builtin_nan("");
-#endif
     }
 }
 
@@ -1420,7 +1360,8 @@ __device__ __forceinline__ bool env_point(const SimArgs& A, const double* T, int
  * colliding point; algorithmic bytes are counted up to that point, as the reference
  * reads them (its loop returns at the first colliding point).  Provably-free rounds
  * are not read but still counted (4 B per point, all in bounds). */
-__device__ FKS_SHAPE_INLINE bool env_collision(Sim& s, const double* T) {
+template <bool GIVEN = false>
+__device__ FKS_SHAPE_INLINE bool env_collision(Sim& s, const double* T, const uint64_t given = 0) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
 #if defined(FKS_PROBE_PROOF_TWICE)
@@ -1428,12 +1369,8 @@ __device__ FKS_SHAPE_INLINE bool env_collision(Sim& s, const double* T) {
     uint64_t skip = skippable_rounds(s, T, kSkipCheck);
     asm volatile("" ::: "memory");
     skip &= skippable_rounds(s, T, kSkipCheck) | skip;
-#elif FKS_WM
-    /* travel below the watermark: every round free without the per-round proof */
-    const double* mw = s.lds() + LAY(A).misc;
-    const uint64_t skip = (mw[kMiscTravel] < mw[kMiscWatermark]) ? ~0ull : skippable_rounds(s, T, kSkipCheck);
 #else
-    const uint64_t skip = skippable_rounds(s, T, kSkipCheck);
+    const uint64_t skip = GIVEN ? given : skippable_rounds(s, T, kSkipCheck); /* GIVEN: the caller's proof */
 #endif
     /* every round proven free (the common microstep): the reference reads 4 bytes per
      * point and finds nothing; account those reads without walking the rounds */
@@ -1481,6 +1418,97 @@ __device__ FKS_SHAPE_INLINE bool env_collision(Sim& s, const double* T) {
         s.lane_bytes += b1;
     }
     return false;
+}
+
+/* ---- cooperative small batches (COOP waves per particle) ----
+ * A batch far smaller than the resident grid is the latency of its slowest particle, a chain
+ * of dependent memory round trips that one wave runs alone.  The cooperative kernels give each
+ * particle a workgroup of COOP waves: wave 0 (the leader) runs the particle as every other
+ * kernel does; where an environment check or a correction pass has two or more rounds left
+ * after the skip proofs, it hands them out, one per wave, through a mailbox (CoopBox) behind its
+ * LDS block, with a workgroup barrier to start them and one to collect them (a check with one
+ * round left runs as in the other kernels).  Results are the sequential loop's bit for bit:
+ * each round is evaluated by the same code, the first colliding point and the byte count of an
+ * environment check are resolved in round order by the leader, and correction rows are placed
+ * by a prefix sum of the rounds' row counts, in the sequential order. */
+#ifndef FKS_COOP_WAVES
+#define FKS_COOP_WAVES 8 /* fksd::kCoopWaves (the host reads a build's value from the kernel's launch bound) */
+#endif
+static_assert(FKS_COOP_WAVES >= 2 && FKS_COOP_WAVES <= kMaxCoopWaves, "cooperative workgroups hold 2..8 waves");
+enum { kCoopExit = 0, kCoopEnv = 1, kCoopCorr = 2 };
+__device__ __forceinline__ CoopBox* coop_box(const Sim& s) {
+    return reinterpret_cast<CoopBox*>(s.lds() + LAY(*s.A).total); /* behind the leader's block */
+}
+__device__ __forceinline__ void coop_sync() { __syncthreads(); }
+/* the k-th set bit of m (-1 if fewer) */
+__device__ __forceinline__ int nth_bit(uint64_t m, int k) {
+    for (int j = 0; j < k && m; ++j) m &= m - 1ull;
+    return m ? __ffsll((unsigned long long)m) - 1 : -1;
+}
+/* points of 64-point round r */
+__device__ __forceinline__ uint32_t round_points(int P, int r) {
+    const int left = P - r * kWave;
+    return (uint32_t)(left < kWave ? left : kWave);
+}
+
+/* wave w's share of a cooperative environment check: the work rounds of rank w, w + COOP, ... */
+template <int COOP>
+__device__ __forceinline__ void env_coop_share(Sim& s, CoopBox* box, int w) {
+    const SimArgs& A = *s.A;
+    const int ln = s.lane();
+    const double* T = s.lds() + box->tc_off;
+    const uint64_t work = box->work;
+    for (int k = w;; k += COOP) {
+        const int r = nth_bit(work, k);
+        if (r < 0) break;
+        uint64_t b = 0;
+        double S = __builtin_huge_val(), G = __builtin_huge_val(), C = __builtin_huge_val();
+        const bool c = env_point(A, T, r * kWave + ln, &b, &S, &G, &C);
+        round_update(s, r, T, S, G, C);
+        const uint64_t m = __ballot(c);
+        const int first = m ? __ffsll((unsigned long long)m) - 1 : kWave;
+        const uint64_t bytes = wave_sum_u64((ln <= first) ? b : 0ull);
+        if (ln == 0) {
+            box->cnt[r] = (uint32_t)bytes;
+            if (m) __hip_atomic_fetch_or(&box->cmask, 1ull << r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+/* CheckEnvironmentCollision (SPCS:921-981) over the particle's COOP waves (leader side): the
+ * verdict and the bytes of env_collision, the first colliding point in point order deciding
+ * both (its bytes go to lane 0: only their sum over the wave is ever read) */
+template <int COOP>
+__device__ FKS_SHAPE_INLINE bool env_collision_coop(Sim& s, const double* T) {
+    const SimArgs& A = *s.A;
+    const RobotDev& R = A.R;
+    const int nr = RDIM(R, nrounds);
+    const uint64_t skip = skippable_rounds(s, T, kSkipCheck);
+    const uint64_t all = (nr == kWave) ? ~0ull : ((1ull << nr) - 1ull);
+    const uint64_t work = all & ~skip;
+    if (__popcll(work) < 2) return env_collision<true>(s, T, skip);
+    CoopBox* box = coop_box(s);
+    if (s.lane() == 0) {
+        box->cmd = kCoopEnv;
+        box->tc_off = (uint32_t)(T - s.lds());
+        box->work = work;
+        box->cmask = 0;
+    }
+    coop_sync();
+    env_coop_share<COOP>(s, box, 0);
+    coop_sync();
+    const uint64_t cm = box->cmask;
+    const int rc = cm ? __ffsll((unsigned long long)cm) - 1 : nr - 1; /* the last round counted */
+    const uint64_t upto = (rc >= 63) ? ~0ull : ((2ull << rc) - 1ull);
+    /* proven rounds: 4 bytes per point (in bounds, as env_collision counts them) */
+    const uint64_t proven = all & skip & upto;
+    uint64_t bytes = 4ull * (uint64_t)__popcll(proven) * kWave;
+    if ((proven >> (nr - 1)) & 1ull) bytes -= 4ull * (uint64_t)(kWave - round_points(RDIM(R, P), nr - 1));
+    for (uint64_t m = work & upto; m; m &= m - 1ull) bytes += box->cnt[__ffsll((unsigned long long)m) - 1];
+    if (s.lane() == 0) s.lane_bytes += bytes;
+    count_event(s, FKS_PHASE_ENV_ROUNDS_SKIPPED, (uint64_t)__popcll(proven));
+    count_event(s, FKS_PHASE_ENV_ROUNDS_EVALUATED, (uint64_t)__popcll(work & upto));
+    return cm != 0ull;
 }
 
 /* ---------------- self-collision (SPCS:983-1275) ---------------- */
@@ -1944,10 +1972,14 @@ __device__ __noinline__ uint32_t self_collisions_exact(const SimArgs* __restrict
 }
 
 /* CheckCollision (SPCS:1418-1436) */
-template <int RT>
+template <int RT, int COOP = 0>
 __device__ FKS_SHAPE_INLINE bool check_collision(Sim& s, const double* Tp, const double* Tc, const double* q) {
     uint64_t t0 = tick();
-    const bool env = env_collision(s, Tc);
+    bool env;
+    if constexpr (COOP > 0)
+        env = env_collision_coop<COOP>(s, Tc);
+    else
+        env = env_collision(s, Tc);
     tock(s, FKS_PHASE_ENV_CHECK, t0);
     bool self = false;
     if constexpr (RT == FKS_ROBOT_LINKED) {
@@ -1981,9 +2013,11 @@ __device__ FKS_SHAPE_INLINE void joint_frames(Sim& s, const double* Tc) {
     wsync();
 }
 
-/* CollectPointCorrectionsAndJacobians (SPCS:1818-1939): rows written to scratch, returns R */
-template <int RT>
-__device__ FKS_SHAPE_INLINE uint32_t collect_corrections(Sim& s, const double* Tp, const double* Tc, const double* cfg) {
+/* CollectPointCorrectionsAndJacobians (SPCS:1818-1939): rows written to scratch, returns R
+ * (GIVEN: the caller has put the joint frames in LDS and proven the rounds in `given`) */
+template <int RT, bool GIVEN = false>
+__device__ FKS_SHAPE_INLINE uint32_t collect_corrections(Sim& s, const double* Tp, const double* Tc, const double* cfg,
+                                                         const uint64_t given = 0) {
     const SimArgs& A = *s.A;
     const RobotDev& R = A.R;
     const int ln = s.lane();
@@ -1994,13 +2028,13 @@ __device__ FKS_SHAPE_INLINE uint32_t collect_corrections(Sim& s, const double* T
     const FKS_GLOBAL double* corr = gp(s.scratch) + SL.corr;
     const FKS_GLOBAL double* flag = gp(s.scratch) + SL.flag;
     const uint32_t rc = ROWCAP(A);
-    joint_frames<RT>(s, Tc);
+    if constexpr (!GIVEN) joint_frames<RT>(s, Tc);
     const double* axw = s.lds() + LAY(*s.A).axis_w;
     const double* orw = s.lds() + LAY(*s.A).orig_w;
     uint32_t rows = 0;
     /* rounds that provably hold no corrected point: their EstimateDistance reads are
      * counted (28 B per point, in bounds) but not made */
-    const uint64_t skip = skippable_rounds(s, Tc, kSkipCorrections);
+    const uint64_t skip = GIVEN ? given : skippable_rounds(s, Tc, kSkipCorrections);
     for (int base = 0; base < RDIM(R, P); base += kWave) {
         const int i = base + ln;
         const int r = base / kWave;
@@ -2099,6 +2133,239 @@ __device__ FKS_SHAPE_INLINE uint32_t collect_corrections(Sim& s, const double* T
     }
     wsync();
     return rows * 3u;
+}
+
+/* one round of CollectPointCorrectionsAndJacobians (SPCS:1818-1939) for the cooperative
+ * pass: whether this lane's point gets a row, its correction and world position */
+template <int RT>
+__device__ __forceinline__ bool corr_coop_round(Sim& s, const double* Tp, const double* Tc, uint64_t skip, int r, D3* pc, D4* xc,
+                                                int* link, uint64_t* selfk) {
+    const SimArgs& A = *s.A;
+    const RobotDev& R = A.R;
+    const int ln = s.lane();
+    const int i = r * kWave + ln;
+    const bool skr = (skip >> r) & 1ull;
+    const FKS_GLOBAL double* corr = gp(s.scratch) + A.SL.corr;
+    const FKS_GLOBAL double* flag = gp(s.scratch) + A.SL.flag;
+    bool has = false;
+    *pc = D3{0.0, 0.0, 0.0};
+    *xc = D4{0.0, 0.0, 0.0, 0.0};
+    *link = 0;
+    if (skr && !s.self_nonempty) {
+        if (i < RDIM(R, P)) s.lane_bytes += 28;
+        return false;
+    }
+    if (i < RDIM(R, P)) {
+        const D4 p = load_point(R, i);
+        *link = gp(R.point_link)[i];
+        *xc = xform4(Tc + 12 * *link, p);
+        const bool has_self = s.self_nonempty && flag[i] != 0.0;
+        bool inb = false;
+        double est = 0.0;
+        if (skr)
+            s.lane_bytes += 28;
+        else
+            est = estimate_distance(A, *xc, &inb, &s.lane_bytes);
+        const bool has_env = (est < 0.0) && inb;
+        D3 ecorr{0.0, 0.0, 0.0};
+        if (has_env) {
+            const D4 xp = xform4(Tp + 12 * *link, p);
+            const D4 motion{xc->x - xp.x, xc->y - xp.y, xc->z - xp.z, xc->w - xp.w};
+            const D4 nm = safe_normal4(motion);
+            D3 raw;
+            const bool ok = lookup_normal(A, *xc, nm, &raw, &s.err, &s.lane_bytes);
+            if (!ok) s.err |= FKS_PARTICLE_ERR_NORMAL_OOB;
+            const D3 g = safe_normal3(raw);
+            const double pen = dabs(0.0 - est);
+            ecorr = D3{g.x * pen, g.y * pen, g.z * pen};
+        }
+        has = has_self || has_env;
+        if (has_self) *pc = D3{pc->x + corr[3 * i], pc->y + corr[3 * i + 1], pc->z + corr[3 * i + 2]};
+        if (has_env) *pc = D3{pc->x + ecorr.x, pc->y + ecorr.y, pc->z + ecorr.z};
+    }
+    if (s.self_nonempty) *selfk += (uint64_t)__popcll(__ballot(has && flag[i] != 0.0));
+    return has;
+}
+
+/* the row (3 values of b, 3 x D of J) of one corrected point at row index `row` (x 3) */
+template <int RT>
+__device__ __forceinline__ void corr_coop_row(Sim& s, const double* cfg, uint32_t row, const D3& pc, const D4& xc, int link) {
+    const SimArgs& A = *s.A;
+    const RobotDev& R = A.R;
+    const int D = RDIM(R, D);
+    const uint32_t rc = ROWCAP(A);
+    FKS_GLOBAL double* J = gpw(s.scratch) + A.SL.J;
+    FKS_GLOBAL double* bv = gpw(s.scratch) + A.SL.b;
+    bv[row + 0] = pc.x;
+    bv[row + 1] = pc.y;
+    bv[row + 2] = pc.z;
+    if constexpr (RT == FKS_ROBOT_LINKED) {
+        const double* axw = s.lds() + LAY(A).axis_w;
+        const double* orw = s.lds() + LAY(A).orig_w;
+        const uint64_t mask = gp(R.link_dof_mask)[link];
+        for (int d = 0; d < D; ++d) {
+            D3 col{0.0, 0.0, 0.0};
+            if ((mask >> d) & 1ull) {
+                const D3 aw{axw[3 * d], axw[3 * d + 1], axw[3 * d + 2]};
+                const int jt = s.joints()[s.dofj()[d]].type;
+                if (jt == FKS_JOINT_PRISMATIC) {
+                    col = aw;
+                } else {
+                    col = cross(aw, D3{xc.x - orw[3 * d], xc.y - orw[3 * d + 1], xc.z - orw[3 * d + 2]});
+                }
+                col = D3{0.0 + col.x, 0.0 + col.y, 0.0 + col.z};
+            }
+            J[(uint64_t)d * rc + row + 0] = col.x;
+            J[(uint64_t)d * rc + row + 1] = col.y;
+            J[(uint64_t)d * rc + row + 2] = col.z;
+        }
+    } else if constexpr (RT == FKS_ROBOT_SE2) {
+        J[0 * rc + row + 0] = 0.0 + 1.0;
+        J[0 * rc + row + 1] = 0.0;
+        J[0 * rc + row + 2] = 0.0;
+        J[1 * rc + row + 0] = 0.0;
+        J[1 * rc + row + 1] = 0.0 + 1.0;
+        J[1 * rc + row + 2] = 0.0;
+        const D3 c2 = cross(D3{0.0, 0.0, 1.0}, D3{xc.x - cfg[0], xc.y - cfg[1], xc.z - 0.0});
+        J[2 * rc + row + 0] = 0.0 + c2.x;
+        J[2 * rc + row + 1] = 0.0 + c2.y;
+        J[2 * rc + row + 2] = 0.0 + c2.z;
+    } else {
+        const D3 d{xc.x - cfg[3], xc.y - cfg[7], xc.z - cfg[11]};
+        for (int a = 0; a < 3; ++a) {
+            const D3 axis{cfg[a], cfg[4 + a], cfg[8 + a]};
+            J[(uint64_t)a * rc + row + 0] = 0.0 + axis.x;
+            J[(uint64_t)a * rc + row + 1] = 0.0 + axis.y;
+            J[(uint64_t)a * rc + row + 2] = 0.0 + axis.z;
+            const D3 c = cross(axis, d);
+            J[(uint64_t)(3 + a) * rc + row + 0] = 0.0 + c.x;
+            J[(uint64_t)(3 + a) * rc + row + 1] = 0.0 + c.y;
+            J[(uint64_t)(3 + a) * rc + row + 2] = 0.0 + c.z;
+        }
+    }
+}
+
+/* wave w's share of a cooperative correction pass: the work rounds of rank w, w + COOP, ...
+ * (at most two each, the pass's rounds beyond 2 x COOP are not handed out): their row counts
+ * are published, and after the barrier their rows written at the prefix sum of the counts of
+ * the work rounds before them; returns the total row count (the same in every wave) */
+template <int RT, int COOP>
+__device__ __forceinline__ uint32_t corr_coop_share(Sim& s, CoopBox* box, int w, uint64_t* selfk) {
+    const int ln = s.lane();
+    const double* Tc = s.lds() + box->tc_off;
+    const double* Tp = s.lds() + box->tp_off;
+    const double* cfg = s.lds() + box->cfg_off;
+    const uint64_t skip = box->skip;
+    const uint64_t work = box->work;
+    const int r0 = nth_bit(work, w), r1 = nth_bit(work, w + COOP);
+    D3 pc0, pc1;
+    D4 xc0, xc1;
+    int l0 = 0, l1 = 0;
+    bool h0 = false, h1 = false;
+    if (r0 >= 0) h0 = corr_coop_round<RT>(s, Tp, Tc, skip, r0, &pc0, &xc0, &l0, selfk);
+    if (r1 >= 0) h1 = corr_coop_round<RT>(s, Tp, Tc, skip, r1, &pc1, &xc1, &l1, selfk);
+    const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
+    if (ln == 0) {
+        if (r0 >= 0) box->cnt[r0] = (uint32_t)__popcll(m0);
+        if (r1 >= 0) box->cnt[r1] = (uint32_t)__popcll(m1);
+    }
+    coop_sync();
+    uint32_t before0 = 0, before1 = 0, total = 0;
+    for (uint64_t m = work; m; m &= m - 1ull) {
+        const int r = __ffsll((unsigned long long)m) - 1;
+        const uint32_t c = box->cnt[r];
+        if (r < r0) before0 += c;
+        if (r < r1) before1 += c;
+        total += c;
+    }
+    const uint64_t below = (1ull << ln) - 1ull;
+    if (h0) corr_coop_row<RT>(s, cfg, (before0 + (uint32_t)__popcll(m0 & below)) * 3u, pc0, xc0, l0);
+    if (h1) corr_coop_row<RT>(s, cfg, (before1 + (uint32_t)__popcll(m1 & below)) * 3u, pc1, xc1, l1);
+    return total;
+}
+
+/* CollectPointCorrectionsAndJacobians (SPCS:1818-1939) over the particle's COOP waves
+ * (leader side): the rows collect_corrections writes, in its order; returns R.  The work
+ * rounds are those collect_corrections evaluates (a proven round is still read for its
+ * self-collision flags); a pass with fewer than two, or more than 2 x COOP, runs as there. */
+template <int RT, int COOP>
+__device__ FKS_SHAPE_INLINE uint32_t collect_corrections_coop(Sim& s, const double* Tp, const double* Tc, const double* cfg) {
+    const int nr = RDIM(s.A->R, nrounds);
+    const uint64_t all = (nr == kWave) ? ~0ull : ((1ull << nr) - 1ull);
+    joint_frames<RT>(s, Tc);
+    const uint64_t skip = skippable_rounds(s, Tc, kSkipCorrections);
+    const uint64_t work = s.self_nonempty ? all : (all & ~skip);
+    const int nw = __popcll(work);
+    if (nw < 2 || nw > 2 * COOP) return collect_corrections<RT, true>(s, Tp, Tc, cfg, skip);
+    count_event(s, FKS_PHASE_CORR_ROUNDS_SKIPPED, (uint64_t)__popcll(skip & all));
+    count_event(s, FKS_PHASE_CORR_ROUNDS_EVALUATED, (uint64_t)(nr - __popcll(skip & all)));
+    /* the rounds nobody evaluates: 28 bytes per point, as collect_corrections counts them */
+    const uint64_t idle = all & ~work;
+    uint64_t bytes = 28ull * (uint64_t)__popcll(idle) * kWave;
+    if ((idle >> (nr - 1)) & 1ull) bytes -= 28ull * (uint64_t)(kWave - round_points(RDIM(s.A->R, P), nr - 1));
+    if (s.lane() == 0) s.lane_bytes += bytes;
+    CoopBox* box = coop_box(s);
+    if (s.lane() == 0) {
+        box->cmd = kCoopCorr;
+        box->tc_off = (uint32_t)(Tc - s.lds());
+        box->tp_off = (uint32_t)(Tp - s.lds());
+        box->cfg_off = (uint32_t)(cfg - s.lds());
+        box->work = work;
+        box->skip = skip;
+        box->self_nonempty = s.self_nonempty ? 1u : 0u;
+    }
+    coop_sync();
+    uint64_t selfk = 0;
+    const uint32_t rows = corr_coop_share<RT, COOP>(s, box, 0, &selfk);
+    coop_sync();
+    uint32_t e = 0;
+#pragma unroll
+    for (int w = 1; w < COOP; ++w) {
+        e |= box->err[w];
+        selfk += box->selfk[w];
+    }
+    s.err |= e;
+    if (s.self_nonempty && s.lane() == 0) self_counters(s)[1] += selfk;
+    return rows * 3u;
+}
+
+/* the helper waves of a cooperative workgroup: the leader's share of each loop it hands out,
+ * until it posts kCoopExit; their byte counts go to the call's counters at the end */
+template <int RT, int COOP>
+__device__ __noinline__ void coop_helper(const SimArgs* __restrict__ args, double* lds_mem, int w) {
+    const SimArgs& A = *args;
+    Sim s;
+    s.A = args;
+    s.lds_block = lds_mem + LAY(A).shared_total;
+    s.scratch = A.scratch + (uint64_t)blockIdx.x * A.scratch_per_wave;
+    s.lane_v = lane_id();
+    s.rstate = s.lds() + LAY(A).rstate;
+    s.selfref = s.lds() + LAY(A).selfref;
+    s.lane_bytes = 0;
+    s.err = 0;
+    s.self_nonempty = false;
+    CoopBox* box = coop_box(s);
+    for (;;) {
+        coop_sync();
+        const uint32_t cmd = box->cmd;
+        if (cmd == kCoopExit) break;
+        if (cmd == kCoopEnv) {
+            env_coop_share<COOP>(s, box, w);
+        } else {
+            s.err = 0;
+            s.self_nonempty = box->self_nonempty != 0u;
+            uint64_t selfk = 0;
+            (void)corr_coop_share<RT, COOP>(s, box, w, &selfk);
+            const uint32_t e = wave_or(s.err);
+            if (s.lane() == 0) {
+                box->err[w] = e;
+                box->selfk[w] = selfk;
+            }
+        }
+        coop_sync();
+    }
+    const uint64_t bytes = wave_sum_u64(s.lane_bytes);
+    if (s.lane() == 0 && bytes) atomicAdd(A.counters + kCntSdfBytes, (unsigned long long)bytes);
 }
 
 /* value of column `k` (wave-uniform, runtime) of this lane's register row */
@@ -2961,7 +3228,7 @@ __device__ __noinline__ void individual_jacobians_solve(Sim& s, uint32_t Rn, dou
  * IND: the individual-Jacobian solve (SPCS:1966-1988) is compiled into a kernel of its
  * own, so the default stacked-Jacobian kernel does not carry it; the traced kernels
  * (not on the hot path) read the choice at run time. */
-template <int RT, bool TR, bool IND>
+template <int RT, bool TR, bool IND, int COOP = 0>
 __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg, double* res_cfg, bool allow_contacts, bool* out_collided,
                             bool* out_failed, double*& Tcur, double*& Tprev) {
     const SimArgs& A = *s.A;
@@ -3017,25 +3284,6 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
         const double bound = bfly_sum(0.0 + term);
         proven = !FKS_NO_SKIP_PROOFS && bound * (1.0 + 1e-6) + 1e-12 < A.allowed_micro;
     }
-#ifndef FKS_WM_OFF
-#define FKS_WM_OFF 0
-#endif
-#if FKS_WM && !(FKS_WM_OFF & 1)
-    {
-        /* the travel bound of one noisy microstep of this step: |clamped command| + noise bound
-         * per dof (UNC:77-90), through the lever arms; a sampled actuator has no such bound */
-        double nb = 0.0;
-        if (ln < D) {
-            const fks_dof_controller& ct = s.ctrl()[ln];
-            const double vmax = dabs(ct.velocity_limit);
-            nb = fks_control::actuator_noise_bound(clamp(ustep[ln], -vmax, vmax), dabs(ct.max_actuator_proportional_noise),
-                                                   dabs(ct.max_actuator_minimum_noise), vmax);
-        }
-        const double tw = (ln < D) ? (dabs(ustep[ln]) + nb) * gp(R.dof_lever)[ln] : 0.0;
-        const double B = R.sampled_mask ? __builtin_huge_val() : bfly_sum(0.0 + tw) * (1.0 + 1e-6) + 1e-12;
-        if (ln == 0) s.lds()[LAY(A).misc + kMiscStepBound] = B;
-    }
-#endif
     if (!proven) {
         apply_input<RT>(s, cfg, ustep, cfg_tmp, false, 0);
         fk<RT>(s, cfg_tmp, Ttmp);
@@ -3118,13 +3366,7 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                 fk<RT>(s, cfg, Tcur);
         }
         tock(s, FKS_PHASE_MICRO_FK, t0);
-#if FKS_WM
-        if (ln == 0) {
-            double* mw = s.lds() + LAY(A).misc;
-            mw[kMiscTravel] = mw[kMiscTravel] + mw[kMiscStepBound];
-        }
-#endif
-        bool in_collision = check_collision<RT>(s, Tprev, Tcur, cfg);
+        bool in_collision = check_collision<RT, COOP>(s, Tprev, Tcur, cfg);
         if (s.err) return 1;
         if (in_collision) pair_ready = false; /* the resolver reuses cfg_tmp / Ttmp */
         trace_config<TR>(s, cfg, micro, FKS_TRACE_POST_ACTION);
@@ -3149,7 +3391,11 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                 const int ln = s.lane();
                 s.resolver_count++;
                 t0 = tick();
-                uint32_t Rn = collect_corrections<RT>(s, Tprev, Tcur, cfg_act);
+                uint32_t Rn;
+                if constexpr (COOP > 0)
+                    Rn = collect_corrections_coop<RT, COOP>(s, Tprev, Tcur, cfg_act);
+                else
+                    Rn = collect_corrections<RT>(s, Tprev, Tcur, cfg_act);
                 s.lsq_rows += Rn;
                 s.err = wave_or(s.err);
                 tock(s, FKS_PHASE_CORRECTIONS, t0);
@@ -3205,20 +3451,8 @@ __device__ FKS_SHAPE_INLINE int resolve_step(Sim& s, const double* particle_cfg,
                     wsync();
                     fk<RT>(s, cfg_act, Tcur);
                 }
-#if FKS_WM && !(FKS_WM_OFF & 2)
-                {
-                    /* the correction moved the robot by at most sum_d |step_d| * lever_d */
-                    const double* stp = applied ? x : real;
-                    const double tc = (ln < D) ? dabs(stp[ln]) * gp(R.dof_lever)[ln] : 0.0;
-                    const double inc = bfly_sum(0.0 + tc) * (1.0 + 1e-6) + 1e-12;
-                    if (ln == 0) {
-                        double* mw = s.lds() + LAY(A).misc;
-                        mw[kMiscTravel] = mw[kMiscTravel] + inc;
-                    }
-                }
-#endif
                 tock(s, FKS_PHASE_RESOLVE_APPLY, t0);
-                in_collision = check_collision<RT>(s, Tprev, Tcur, cfg_act);
+                in_collision = check_collision<RT, COOP>(s, Tprev, Tcur, cfg_act);
                 if (s.err) return 1;
                 trace_config<TR>(s, cfg_act, micro, FKS_TRACE_RESOLVER_STEP);
                 iters++;
@@ -3416,15 +3650,23 @@ __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict
         }
     }
     if (!need) return 0u;
-    /* exact keys (LocationToExtendedGridIndex SPCS:1173-1181) of the needed geometries' points */
+    /* exact keys (LocationToExtendedGridIndex SPCS:1173-1181: trunc of the quotient by `res`) of
+     * the needed geometries' points.  The quotient is taken as a product with 1/res unless an
+     * integer lies within 8 ulp of it (then the division): the product is within 2.5 ulp of the
+     * correctly rounded quotient, so away from integers both truncate alike */
     int64_t* keys = reinterpret_cast<int64_t*>(scratch + SLAY(A).keys);
     uint32_t err = 0;
+    const double inv = 1.0 / res;
+    auto quotient = [&](double v) {
+        const double r = v * inv;
+        return (dabs(r) < 4.0e15 && dabs(r - __builtin_rint(r)) > dabs(r) * 0x1p-49) ? r : v / res;
+    };
     for (uint64_t gm = need; gm; gm &= gm - 1ull) {
         const int g0 = __ffsll((unsigned long long)gm) - 1;
         for (int i = (int)gp(R.geom_off)[g0] + ln; i < (int)gp(R.geom_off)[g0 + 1]; i += kWave) {
             const D4 x = xform4(Tc + 12 * (int)gp(R.point_link)[i], load_point(R, i));
             const D4 g = xform4(A.env_g.inv, x);
-            const double q[3] = {g.x / res, g.y / res, g.z / res};
+            const double q[3] = {quotient(g.x), quotient(g.y), quotient(g.z)};
             for (int a = 0; a < 3; ++a) {
                 int64_t k;
                 if (q[a] != q[a] || q[a] == __builtin_huge_val() || q[a] == -__builtin_huge_val()) {
@@ -3460,6 +3702,38 @@ __device__ __noinline__ uint32_t config_self_collision(const SimArgs* __restrict
         if (!ov) continue;
         const int a0 = (int)gp(R.geom_off)[a], a1 = (int)gp(R.geom_off)[a + 1];
         const int b0 = (int)gp(R.geom_off)[b], b1 = (int)gp(R.geom_off)[b + 1];
+        if (a1 - a0 <= kWave && b1 - b0 <= kWave) {
+            /* one chunk each (every robot here: <= 64 points per geometry): both sides' keys in
+             * one memory round trip */
+            const int j = b0 + ln, i = a0 + ln;
+            int64_t bx = 0, by = 0, bz = 0, ax = 0, ay = 0, az = 0;
+            if (j < b1) {
+                bx = keys[3 * j];
+                by = keys[3 * j + 1];
+                bz = keys[3 * j + 2];
+            }
+            if (i < a1) {
+                ax = keys[3 * i];
+                ay = keys[3 * i + 1];
+                az = keys[3 * i + 2];
+            }
+            auto in_box_k = [&](int64_t kx, int64_t ky, int64_t kz, int g) {
+                return box[6 * g] <= (double)kx && (double)kx <= box[6 * g + 3] && box[6 * g + 1] <= (double)ky &&
+                       (double)ky <= box[6 * g + 4] && box[6 * g + 2] <= (double)kz && (double)kz <= box[6 * g + 5];
+            };
+            const bool jin = j < b1 && in_box_k(bx, by, bz, a);
+            const bool iin = i < a1 && in_box_k(ax, ay, az, b);
+            uint64_t m = __ballot(jin);
+            if (!m || !wave_any(iin)) continue;
+            bool h = false;
+            while (m) {
+                const int t = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1ull;
+                h = h || (ax == readlane_i64(bx, t) && ay == readlane_i64(by, t) && az == readlane_i64(bz, t));
+            }
+            hit = hit || (iin && h);
+            continue;
+        }
         for (int j0 = b0; j0 < b1 && !wave_any(hit); j0 += kWave) {
             const int j = j0 + ln;
             const bool jin = j < b1 && in_box(j, a);
@@ -3621,7 +3895,7 @@ __device__ __forceinline__ void kinematics(const SimArgs* __restrict__ args, dou
     }
 }
 
-template <int RT, bool TR, bool IND = false, bool LEAN = false>
+template <int RT, bool TR, bool IND = false, bool LEAN = false, int COOP = 0>
 __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ args, double* lds_mem) {
     const SimArgs& A = *args;
     const RobotDev& R = A.R;
@@ -3651,12 +3925,19 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             shared[LAY(A).rounds + 2 * t] = (double)rd.link;
             shared[LAY(A).rounds + 2 * t + 1] = rd.radius;
         }
-        __syncthreads(); /* the only workgroup barrier: waves run independently afterwards */
+        __syncthreads(); /* the only workgroup barrier: waves run independently afterwards (except COOP's) */
+    }
+    if constexpr (COOP > 0) {
+        /* one particle per workgroup: wave 0 runs it, the others help with its point loops */
+        if (wave != 0) {
+            coop_helper<RT, COOP>(args, lds_mem, wave);
+            return;
+        }
     }
     Sim s;
     s.A = args;
     s.lds_block = lds_mem + LAY(A).shared_total + (uint64_t)wave * LAY(A).total;
-    s.scratch = A.scratch + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)wave) * A.scratch_per_wave;
+    s.scratch = A.scratch + ((uint64_t)blockIdx.x * (COOP > 0 ? 1u : (blockDim.x >> 6)) + (uint64_t)wave) * A.scratch_per_wave;
     s.lane_v = lane_id();
     /* skip-proof cache of the first 64 rounds (the skip masks are 64-bit; later rounds are always
      * read): in the wave's LDS block, or in its scratch for a lean block (fixed per kernel, so
@@ -3664,9 +3945,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     s.rstate = LEAN ? s.scratch + SLAY(A).rstate : s.lds() + LAY(A).rstate;
     s.selfref = LEAN ? s.scratch + SLAY(A).selfref : s.lds() + LAY(A).selfref;
     if (s.lane() < RDIM(R, nrounds)) s.rstate[kRoundState * s.lane() + 12] = kInvalidRound;
-#if FKS_WM
-    if (s.lane() < RDIM(R, nrounds)) s.rstate[kRoundState * s.lane() + 15] = -__builtin_huge_val();
-#endif
     wsync();
     const int ln = s.lane();
     const int W = RDIM(R, W), D = RDIM(R, D);
@@ -3745,6 +4023,11 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                     for (int k = 0; k < FKS_NUM_PHASES; ++k)
                         if (s.phase()[k]) atomicAdd(A.counters + kPhaseBase + k, (unsigned long long)s.phase()[k]);
                 }
+                if constexpr (COOP > 0) {
+                    /* release the helpers (every wave of the workgroup meets this barrier last) */
+                    if (ln == 0) coop_box(s)->cmd = kCoopExit;
+                    coop_sync();
+                }
                 break;
             }
             if (!run) continue; /* segment already run, being run, or left to the wave finishing its predecessor */
@@ -3798,15 +4081,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             } else {
                 if (ln < 12) cfg[ln] = start[ln];
             }
-#if FKS_WM
-            /* a new particle: no travel, no watermark entries (except rounds that never move) */
-            if (ln < RDIM(R, nrounds) && s.rstate[kRoundState * ln + 15] != __builtin_huge_val())
-                s.rstate[kRoundState * ln + 15] = -__builtin_huge_val();
-            if (ln == 0) {
-                s.lds()[LAY(A).misc + kMiscTravel] = 0.0;
-                s.lds()[LAY(A).misc + kMiscWatermark] = __builtin_nan("");
-            }
-#endif
         } else {
             /* resume: configuration from out_q, controller state and per-particle totals
              * from seg_state (bit-exact: the step loop below recomputes FK at its start) */
@@ -3820,13 +4094,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             /* the particle's own skip-proof cache (the rounds' last full evaluations) */
             const int nrc = kRoundState * (RDIM(R, nrounds) < kWave ? RDIM(R, nrounds) : kWave);
             for (int e = ln; e < nrc; e += kWave) s.rstate[e] = load_coherent(st + 2 * D + 4 + e);
-#if FKS_WM
-            /* the particle's travel so far (its entries came back with the cache) */
-            if (ln == 0) {
-                s.lds()[LAY(A).misc + kMiscTravel] = load_coherent(st + 2 * D + 3);
-                s.lds()[LAY(A).misc + kMiscWatermark] = __builtin_nan("");
-            }
-#endif
         }
         wsync();
         double* Tcur = s.lds() + LAY(*s.A).Tcur;
@@ -3845,7 +4112,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
             wsync();
             tock(s, FKS_PHASE_CONTROL, t0);
             bool rc = false, rf = false;
-            const int status = resolve_step<RT, TR, IND>(s, cfg, res_cfg, A.allow_contacts != 0, &rc, &rf, Tcur, Tprev);
+            const int status = resolve_step<RT, TR, IND, COOP>(s, cfg, res_cfg, A.allow_contacts != 0, &rc, &rf, Tcur, Tprev);
             s.err = wave_or(s.err);
             if (status != 0 || s.err) {
                 ended = true;
@@ -3901,9 +4168,6 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                 store_coherent_u64(sw, (collided ? 1ull : 0ull) | (any_failed ? 2ull : 0ull));
                 store_coherent_u64(sw + 1, micro_total);
                 store_coherent_u64(sw + 2, resolver_total);
-#if FKS_WM
-                store_coherent(st + 2 * D + 3, s.lds()[LAY(A).misc + kMiscTravel]);
-#endif
             }
             const int nrc = kRoundState * (RDIM(R, nrounds) < kWave ? RDIM(R, nrounds) : kWave);
             for (int e = ln; e < nrc; e += kWave) store_coherent(st + 2 * D + 4 + e, s.rstate[e]);
@@ -4025,6 +4289,23 @@ extern "C" __global__ void FKS_SMALL_KERNEL_ATTRS fks_simulate_se2_small(const S
 extern "C" __global__ void FKS_SMALL_KERNEL_ATTRS fks_simulate_se3_small(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
     simulate_particles<FKS_ROBOT_SE3, false>(args, lds_mem);
+}
+
+/* cooperative small batches (fks_set_cooperative_waves): one particle per workgroup of
+ * FKS_COOP_WAVES waves, whose environment checks and correction passes are shared out over
+ * them (COOP above); for batches up to one particle per workgroup slot */
+#define FKS_COOP_KERNEL_ATTRS __launch_bounds__(64 * FKS_COOP_WAVES) __attribute__((amdgpu_waves_per_eu(2)))
+extern "C" __global__ void FKS_COOP_KERNEL_ATTRS fks_simulate_linked_coop(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_LINKED, false, false, false, FKS_COOP_WAVES>(args, lds_mem);
+}
+extern "C" __global__ void FKS_COOP_KERNEL_ATTRS fks_simulate_se2_coop(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_SE2, false, false, false, FKS_COOP_WAVES>(args, lds_mem);
+}
+extern "C" __global__ void FKS_COOP_KERNEL_ATTRS fks_simulate_se3_coop(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_ROBOT_SE3, false, false, false, FKS_COOP_WAVES>(args, lds_mem);
 }
 
 /* simulate_with_individual_jacobians = true (SPCS:420, 1629; fks_set_individual_jacobians) */

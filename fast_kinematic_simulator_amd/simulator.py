@@ -162,6 +162,13 @@ class HipParticleContactSimulator:
         (fks_set_small_batch_kernel; default on).  Results do not depend on it."""
         _capi.check(self._lib.fks_set_small_batch_kernel(self._ctx, 1 if enabled else 0), self._ctx, "small batch kernel")
 
+    def set_cooperative_waves(self, enabled: bool = True):
+        """Batches of at most launch_info()["cooperative_resident_particles"] particles run one
+        particle per workgroup, its environment checks and correction passes shared over the
+        workgroup's waves (fks_set_cooperative_waves; default off: slower on the measured
+        workloads).  Results do not depend on it."""
+        _capi.check(self._lib.fks_set_cooperative_waves(self._ctx, 1 if enabled else 0), self._ctx, "cooperative waves")
+
     def set_specialization(self, enabled=True):
         """Run the plain throughput simulation of this robot (and of every robot set later) on a
         kernel compiled at run time for its shape (fks_set_specialization: hiprtc, cached per

@@ -68,8 +68,10 @@ extern "C" {
  * 8: shape specialisation, launch info
  * 9: specialisation modes (FKS_SPECIALIZE_NO_PROOFS validation kernel), build failures in
  *    fks_specialization_info (failed, message), fks_multi_set_active_devices, pinned per-device
- *    staging in fks_multi_* */
-#define FKS_ABI_VERSION 9
+ *    staging in fks_multi_*
+ * 10: cooperative small batches (fks_set_cooperative_waves, FKS_KERNEL_COOPERATIVE, launch
+ *    info cooperative_*) */
+#define FKS_ABI_VERSION 10
 
 typedef enum {
     FKS_OK = 0,
@@ -444,7 +446,8 @@ typedef enum {
     FKS_KERNEL_SMALL_BATCH = 2,  /* fks_simulate_<family>_small (fks_set_small_batch_kernel) */
     FKS_KERNEL_SHAPED = 3,       /* the robot-shape-specialised kernel (fks_set_specialization) */
     FKS_KERNEL_TRACED = 4,       /* fks_simulate_<family>[_lean]_traced */
-    FKS_KERNEL_INDIVIDUAL = 5    /* fks_simulate_<family>[_lean]_indiv (fks_set_individual_jacobians) */
+    FKS_KERNEL_INDIVIDUAL = 5,   /* fks_simulate_<family>[_lean]_indiv (fks_set_individual_jacobians) */
+    FKS_KERNEL_COOPERATIVE = 6   /* ABI 10: fks_simulate_<family>_coop (fks_set_cooperative_waves) */
 } fks_kernel_kind;
 /* The launch layout fks_set_robot chose (ABI 8; diagnostic, no reference counterpart). */
 typedef struct fks_launch_info {
@@ -458,6 +461,8 @@ typedef struct fks_launch_info {
     int32_t last_kernel;                     /* fks_kernel_kind of the last simulation call */
     int32_t last_check_kernel;               /* ABI 9: of the last batched CheckConfigCollision call
                                                 (FKS_KERNEL_THROUGHPUT: generic, FKS_KERNEL_SHAPED) */
+    uint32_t cooperative_resident_particles; /* ABI 10: the cooperative kernel's grid (0: not for this robot) */
+    uint32_t cooperative_waves_per_particle; /* ABI 10: its waves per particle (workgroup) */
 } fks_launch_info;
 fks_status fks_get_launch_info(const fks_context* ctx, fks_launch_info* out);
 /* Scheduling granularity of fks_forward_simulate*: when a batch holds more particles
@@ -488,6 +493,17 @@ fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_
  * (a planner's typical call: cfg1, 32 particles, 10 % shorter).  0 = always the
  * throughput kernel. */
 fks_status fks_set_small_batch_kernel(fks_context* ctx, int32_t enabled);
+/* Cooperative small batches (ABI 10; no reference counterpart, results are bit-identical
+ * either way; opt-in, default 0): with `enabled` a plain simulation call of at most
+ * fks_launch_info.cooperative_resident_particles particles (one per workgroup slot: 256 CUs
+ * x the kernel's occupancy; same exclusions as the small-batch kernel, robots of at most
+ * 1024 points) runs each particle on a workgroup of cooperative_waves_per_particle waves: one
+ * runs the particle, and every environment check and correction pass is shared out over all
+ * of them, 64-point rounds each.  Takes precedence over the small-batch kernel;
+ * fks_set_small_batch_kernel(ctx, 0) turns both off.  Measured on cfg3's heaviest particles
+ * alone it is 5-10 % SLOWER than the small-batch kernel (about three rounds per check are left
+ * after the skip proofs, too few to share), hence off by default. */
+fks_status fks_set_cooperative_waves(fks_context* ctx, int32_t enabled);
 /* SimpleParticleContactSimulator(..., simulate_with_individual_jacobians, ...) (SPCS:420-423,
  * 1629): 0 = ComputeResolverCorrectionStepStackedJacobian (SPCS:1990-1998; what the factories
  * FKS.cpp:22,45,68 hard-wire, the default), 1 = ComputeResolverCorrectionStepIndividualJacobians

@@ -8,7 +8,7 @@ COUNTER_KEYS = ("microsteps", "resolver_iterations", "controller_steps", "sdf_by
 
 
 def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, first_particle_id=0, sim=None,
-             individual_jacobians=False, segment_steps=None, small_batch_kernel=None, specialize=False):
+             individual_jacobians=False, segment_steps=None, small_batch_kernel=None, specialize=False, cooperative=None):
     import oracle
     from fast_kinematic_simulator_amd import make_linked_simulator
 
@@ -25,6 +25,8 @@ def run_both(wl, starts=None, targets=None, allow_contacts=None, call_index=0, f
         sim.set_segment_steps(segment_steps)
     if small_batch_kernel is not None:
         sim.set_small_batch_kernel(small_batch_kernel)
+    if cooperative is not None:
+        sim.set_cooperative_waves(cooperative)
     if specialize:
         # the robot-shape-specialised throughput kernel (fks_set_specialization); small batches
         # would otherwise run the small-batch kernel

@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol(fks_lib):
 def test_abi_basics(fks_lib):
     from fast_kinematic_simulator_amd import _capi, get_default_solver_parameters
 
-    assert fks_lib.fks_abi_version() == 9
+    assert fks_lib.fks_abi_version() == 10
     assert fks_lib.fks_status_string(0) == b"ok"
     p = _capi.SolverParams()
     assert fks_lib.fks_default_solver_params(ctypes.byref(p)) == 0

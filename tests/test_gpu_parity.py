@@ -24,17 +24,18 @@ def test_selftest_math(fks_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("small_batch_kernel", [True, False])
+@pytest.mark.parametrize("kernel", ["cooperative", "small_batch", "throughput"])
 @pytest.mark.parametrize("name,scale", CASES)
-def test_forward_parity(fks_lib, oracle_lib, name, scale, small_batch_kernel):
+def test_forward_parity(fks_lib, oracle_lib, name, scale, kernel):
     """Batches this small run the low-occupancy instantiation by default
-    (fks_set_small_batch_kernel); both kernels must match the oracle."""
+    (fks_set_small_batch_kernel), or, opted in, the cooperative kernel (a workgroup per
+    particle, fks_set_cooperative_waves); all three kernels must match the oracle."""
     wl = W.WORKLOADS[name](scale)
-    g, o = run_both(wl, small_batch_kernel=small_batch_kernel)
+    g, o = run_both(wl, small_batch_kernel=kernel != "throughput", cooperative=kernel == "cooperative")
     print(name, mismatch_report(g, o), g["launch"])
     # the kernel the call ran is the one the parameter asks for (a failed occupancy query would
-    # leave the small-batch grid empty and run the throughput kernel both times)
-    assert g["launch"]["last_kernel"] == ("small_batch" if small_batch_kernel else "throughput"), g["launch"]
+    # leave the small-batch grids empty and run the throughput kernel every time)
+    assert g["launch"]["last_kernel"] == kernel, g["launch"]
     assert_identical(g, o)
     assert_counters_identical(g, o)
 

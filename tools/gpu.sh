@@ -16,6 +16,9 @@
 #   ab:<wl>:<libs>     interleaved bench.py of comma-separated libraries (each may carry +flag;
 #                      "L" = the product library) on workload <wl>  -> <tag>_ab_<wl>.log
 #   tail:<wl>:<lib>    heaviest particles alone + phase shares (tools/tail_latency.py) -> <tag>_tail_<wl>_<lib>.json
+#   tailsmall:<wl>:<lib>  the same, the lone particles on the one-wave small-batch kernel
+#                      -> <tag>_tailsmall_<wl>_<lib>.json
+#   tailcoop:<wl>:<lib>   the same, the lone particles on the cooperative kernel -> <tag>_tailcoop_<wl>_<lib>.json
 #   tailpmc:<wl>:<lib> instruction-mix and wait counters of the batch and the heaviest particle
 #                      alone (three --pmc passes over tools/tail_latency.py --top 1) -> <tag>_tailpmc_<wl>_<lib>/
 #   sched:<wl>:<segs>:<heavy>  scheduling sweep (tools/sched_sweep.py; comma lists of segment lengths and
@@ -78,6 +81,10 @@ run_task() {
   tail:*)
     spec=${1#tail:}; w=${spec%%:*}; l=$(lib ${spec#*:}); n=$(basename $l .so)
     FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1 timeout -k 10 400 python tools/tail_latency.py --workload $w --top 3 --json $O/${TAG}_tail_${w}_$n.json > $O/${TAG}_tail_${w}_$n.log 2>&1 ;;
+  tailsmall:*|tailcoop:*)
+    kind=${1%%:*}; spec=${1#*:}; w=${spec%%:*}; l=$(lib ${spec#*:}); n=$(basename $l .so)
+    lone=small; [ $kind = tailcoop ] && lone=cooperative
+    FKS_LIB_PATH=$PWD/$l FKS_VARIANT_LIB=1 timeout -k 10 400 python tools/tail_latency.py --workload $w --top 3 --lone $lone --json $O/${TAG}_${kind}_${w}_$n.json > $O/${TAG}_${kind}_${w}_$n.log 2>&1 ;;
   tailpmc:*)
     spec=${1#tailpmc:}; w=${spec%%:*}; l=$(lib ${spec#*:}); n=$(basename $l .so); D=$O/${TAG}_tailpmc_${w}_$n
     T1="python3 tools/tail_latency.py --workload $w --top 1"

@@ -45,7 +45,10 @@ def main():
     ap.add_argument("--top", type=int, default=3)
     ap.add_argument("--json", default="")
     ap.add_argument("--specialize", choices=("on", "off"), default="on",
-                    help="the robot-shape-specialised kernel (the lone particles then skip the small-batch kernel)")
+                    help="the robot-shape-specialised kernel for the batch (and for lone particles with --lone throughput)")
+    ap.add_argument("--lone", choices=("throughput", "small", "cooperative"), default="throughput",
+                    help="the kernel of the lone particles: the batch's, the one-wave small-batch kernel, or the "
+                         "cooperative kernel (a workgroup per particle)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     wl = W.WORKLOADS[a.workload]()
@@ -53,10 +56,11 @@ def main():
     sim.set_robot(wl.robot)
     # the library specialises by default: "off" must switch it off explicitly
     sim.set_specialization(a.specialize == "on")
-    if a.specialize == "on":
-        sim.set_small_batch_kernel(False)
+    sim.set_small_batch_kernel(False)
     run(sim, wl, wl.starts[:256], 0, dev)
     m, it, kms, ph = run(sim, wl, wl.starts, 0, dev)
+    sim.set_small_batch_kernel(a.lone != "throughput")
+    sim.set_cooperative_waves(a.lone == "cooperative")
     out = {"workload": a.workload, "specialization": sim.specialization(), "batch_kernel": sim.launch_info()["last_kernel"],
            "batch_kernel_ms": kms, "particles": int(m.size), "alone": [],
            "batch_phase_share": ({k: round(v / max(1, ph.get("particle", 0)), 4) for k, v in ph.items() if k not in COUNTS}
@@ -66,7 +70,8 @@ def main():
         i = int(i)
         m1, it1, k1, ph1 = run(sim, wl, wl.starts[i:i + 1], i, dev)
         tot = max(1, ph1.get("particle", 0))
-        out["alone"].append({"particle": i, "microsteps": int(m1[0]), "resolver_iterations": int(it1[0]), "kernel_ms": k1,
+        out["alone"].append({"particle": i, "kernel": sim.launch_info()["last_kernel"], "microsteps": int(m1[0]),
+                             "resolver_iterations": int(it1[0]), "kernel_ms": k1,
                              "same_as_in_batch": bool(m1[0] == m[i] and it1[0] == it[i]),
                              "us_per_resolver_iteration_upper": 1e3 * k1 / max(int(it1[0]), 1),
                              "phase_share": ({k: round(v / tot, 4) for k, v in ph1.items() if k not in COUNTS}
