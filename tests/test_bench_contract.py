@@ -44,6 +44,20 @@ def test_bench_json_line():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode,kind", [("off", "throughput"), ("on", "shaped")])
+def test_bench_specialize_flag_is_what_runs(mode, kind):
+    """`--specialize off` times the generic kernel and `on` the shaped one, and the line names
+    the kernel the timed launches actually ran (fks_get_launch_info), not the flag"""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--particles", "8192", "--steps", "1", "--warmup", "1",
+                        "--no-cpu-baseline", "--no-config-check", "--no-projection", "--pipeline-batches", "0",
+                        "--specialize", mode], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.strip()][-1])
+    assert d["roofline"]["kernel_kind"] == kind, d["roofline"]
+    assert d["roofline"]["kernel"].startswith("fks_simulate_shaped" if mode == "on" else "fks_simulate_linked"), d["roofline"]
+
+
+@pytest.mark.gpu
 def test_bench_under_torchrun():
     """The driver's multi-GPU launch (torchrun, one rank per GPU, RCCL process group,
     outcome gather, max-over-ranks timing) at the world size one GPU allows."""

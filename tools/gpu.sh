@@ -12,6 +12,8 @@
 #   trace              rocprofv3 --kernel-trace --stats of bench.py -> <tag>_trace/
 #   pmc                FETCH_SIZE / WRITE_SIZE / TCC hit+miss, one --pmc pass each -> <tag>_pmc_*/
 #   pmc:<wl>           the same three passes on another workload  -> <tag>_pmc_<wl>_*/
+#   counters           rocprofv3 --list-avail                        -> <tag>_counters.txt
+#   icache             instruction-cache, instruction-wait and LDS-conflict counters, one pass -> <tag>_icache/
 #   valu               VALUBusy / VALUUtilization / SQ issue counters, one pass each -> <tag>_valu/
 #   ab:<wl>:<libs>     interleaved bench.py of comma-separated libraries (each may carry +flag;
 #                      "L" = the product library) on workload <wl>  -> <tag>_ab_<wl>.log
@@ -73,6 +75,12 @@ run_task() {
     timeout -s KILL 180 rocprofv3 --pmc VALUBusy --kernel-trace --output-format csv -d $O/${TAG}_valu/valubusy -o bench -- $B1 > /dev/null 2> $O/${TAG}_valu/valubusy.err &&
     timeout -s KILL 180 rocprofv3 --pmc VALUUtilization --kernel-trace --output-format csv -d $O/${TAG}_valu/valuutil -o bench -- $B1 > /dev/null 2> $O/${TAG}_valu/valuutil.err &&
     timeout -s KILL 180 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $O/${TAG}_valu/issue -o bench -- $B1 > /dev/null 2> $O/${TAG}_valu/issue.err ;;
+  counters) timeout -k 10 120 rocprofv3 --list-avail > $O/${TAG}_counters.txt 2>&1 ;;
+  icache)
+    B1="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-check --pipeline-batches 0 --no-projection"
+    mkdir -p $O/${TAG}_icache
+    warm $B1 &&
+    timeout -s KILL 180 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_IFETCH SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $O/${TAG}_icache/ic -o bench -- $B1 > /dev/null 2> $O/${TAG}_icache/ic.err ;;
   ab:*)
     spec=${1#ab:}; w=${spec%%:*}; libs=${spec#*:}; args=()
     for x in ${libs//,/ }; do args+=("$(lib ${x%%+*})${x#${x%%+*}}"); done
