@@ -153,10 +153,11 @@ def config_check_bench(sim, wl, dev, n=1 << 20, reps=3, cpu_sample=16384, thread
 def kernel_name(kind: str, robot_type: int, spec) -> str:
     """The simulation kernel the last timed launch ran (fks_get_launch_info's last_kernel),
     not the one the flags asked for."""
-    if kind == "shaped":
-        return "fks_simulate_shaped (" + (spec["shape"] if spec else "?") + ")"
+    if kind in ("shaped", "shaped_small_batch"):
+        name = "fks_simulate_shaped" if kind == "shaped" else "fks_simulate_shaped_small"
+        return name + " (" + (spec["shape"] if spec else "?") + ")"
     base = KERNELS.get(robot_type, "fks_simulate")
-    return {"throughput": base, "small_batch": base + "_small"}.get(kind, f"{base} ({kind})")
+    return {"throughput": base, "small_batch": base + "_small", "cooperative": base + "_coop"}.get(kind, f"{base} ({kind})")
 
 
 def kernel_source_sha16() -> str:

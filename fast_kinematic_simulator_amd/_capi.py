@@ -220,7 +220,8 @@ class LaunchInfo(ctypes.Structure):
         return d
 
 
-KERNEL_KINDS = {0: "none", 1: "throughput", 2: "small_batch", 3: "shaped", 4: "traced", 5: "individual", 6: "cooperative"}
+KERNEL_KINDS = {0: "none", 1: "throughput", 2: "small_batch", 3: "shaped", 4: "traced", 5: "individual", 6: "cooperative",
+                7: "shaped_small_batch"}
 
 
 class Trace(ctypes.Structure):

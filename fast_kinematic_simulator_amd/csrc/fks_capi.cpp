@@ -308,6 +308,7 @@ struct fks_context {
     hipModule_t spec_module = nullptr;
     hipFunction_t spec_fn = nullptr;       /* fks_simulate_shaped of the current robot's shape */
     hipFunction_t spec_check_fn = nullptr; /* fks_check_configs_shaped (same module) */
+    hipFunction_t spec_small_fn = nullptr; /* fks_simulate_shaped_small (same module, non-lean shapes) */
     std::string spec_shape;
     double spec_seconds = 0.0;
     int32_t spec_from_cache = 0;
@@ -374,6 +375,7 @@ static void spec_release(fks_context* ctx) {
     ctx->spec_module = nullptr;
     ctx->spec_fn = nullptr;
     ctx->spec_check_fn = nullptr;
+    ctx->spec_small_fn = nullptr;
     ctx->spec_shape.clear();
     ctx->spec_seconds = 0.0;
     ctx->spec_from_cache = 0;
@@ -470,6 +472,14 @@ static fks_status spec_build(fks_context* ctx) {
     /* the configuration check of the same shape, when the module carries it */
     hipFunction_t fc = nullptr;
     if (hipModuleGetFunction(&fc, m, "fks_check_configs_shaped") == hipSuccess) ctx->spec_check_fn = fc;
+    /* ... and the small-batch kernel, used when it needs no more registers than two waves per
+     * SIMD leave (the generic small-batch kernel's grid is the one launched) */
+    hipFunction_t fs = nullptr;
+    if (!ctx->lean && hipModuleGetFunction(&fs, m, "fks_simulate_shaped_small") == hipSuccess) {
+        const int v = fks_spec::kernel_metadata_uint(co->bytes, "fks_simulate_shaped_small", ".vgpr_count") +
+                      std::max(0, fks_spec::kernel_metadata_uint(co->bytes, "fks_simulate_shaped_small", ".agpr_count"));
+        if (v > 0 && v <= 256) ctx->spec_small_fn = fs;
+    }
     (void)hipGetLastError();
     ctx->spec_shape = fks_spec::shape_key(sh);
     ctx->spec_seconds = compiled ? co->compile_seconds : 0.0;
@@ -1361,9 +1371,13 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
         HIP_TRY(ctx, hipSetDevice(ctx->device));
     }
     const bool shaped = ctx->spec_fn && !tr && !small && !coop && !ctx->individual_jacobians;
+    /* a small batch runs the shape's small-batch kernel once the robot's module is built (it is
+     * never built for a small batch: robots only ever simulated in small batches cost no compile) */
+    const bool shaped_small = small && ctx->spec_fn && ctx->spec_small_fn;
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
     ctx->last_kernel = tr ? FKS_KERNEL_TRACED
                           : (shaped ? FKS_KERNEL_SHAPED
+                                    : shaped_small ? FKS_KERNEL_SHAPED_SMALL_BATCH
                                     : (coop ? FKS_KERNEL_COOPERATIVE
                                             : (small ? FKS_KERNEL_SMALL_BATCH
                                                      : (ctx->individual_jacobians ? FKS_KERNEL_INDIVIDUAL : FKS_KERNEL_THROUGHPUT))));
@@ -1372,6 +1386,12 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
         void* params[] = {&argp};
         HIP_TRY(ctx, hipModuleLaunchKernel(ctx->spec_fn, grid, 1, 1, 64 * ctx->waves_per_group, 1, 1, (unsigned)ctx->lds_bytes, s,
                                            params, nullptr));
+        ctx->spec_launches++;
+    } else if (shaped_small) {
+        const fksd::SimArgs* argp = ctx->d_args;
+        void* params[] = {&argp};
+        HIP_TRY(ctx, hipModuleLaunchKernel(ctx->spec_small_fn, grid, 1, 1, 64 * ctx->waves_per_group, 1, 1, (unsigned)ctx->lds_bytes,
+                                           s, params, nullptr));
         ctx->spec_launches++;
     } else if (coop) {
         hipLaunchKernelGGL(coop_kernel_for(ctx->R.type), dim3((uint32_t)n), dim3(64 * ctx->coop_waves), ctx->coop_lds_bytes, s,

@@ -4258,6 +4258,16 @@ extern "C" __global__ void FKS_KERNEL_ATTRS fks_check_configs_shaped(const SimAr
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];
     check_configs<FKS_SHAPE_TYPE>(args, lds_mem);
 }
+#if !FKS_SHAPE_LEAN
+/* the small-batch instantiation of the same shape (two waves per SIMD; see
+ * fks_simulate_<family>_small below), for calls that fit its resident waves once the module
+ * is built */
+extern "C" __global__ void __launch_bounds__(64 * kMaxWavesPerGroup) __attribute__((amdgpu_waves_per_eu(2)))
+fks_simulate_shaped_small(const SimArgs* __restrict__ args) {
+    extern __shared__ __attribute__((aligned(16))) double lds_mem[];
+    simulate_particles<FKS_SHAPE_TYPE, false>(args, lds_mem);
+}
+#endif
 #else
 extern "C" __global__ void FKS_KERNEL_ATTRS fks_simulate_linked(const SimArgs* __restrict__ args) {
     extern __shared__ __attribute__((aligned(16))) double lds_mem[];

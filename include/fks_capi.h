@@ -70,7 +70,7 @@ extern "C" {
  *    fks_specialization_info (failed, message), fks_multi_set_active_devices, pinned per-device
  *    staging in fks_multi_*
  * 10: cooperative small batches (fks_set_cooperative_waves, FKS_KERNEL_COOPERATIVE, launch
- *    info cooperative_*) */
+ *    info cooperative_*), the shape-specialised small-batch kernel (FKS_KERNEL_SHAPED_SMALL_BATCH) */
 #define FKS_ABI_VERSION 10
 
 typedef enum {
@@ -447,7 +447,9 @@ typedef enum {
     FKS_KERNEL_SHAPED = 3,       /* the robot-shape-specialised kernel (fks_set_specialization) */
     FKS_KERNEL_TRACED = 4,       /* fks_simulate_<family>[_lean]_traced */
     FKS_KERNEL_INDIVIDUAL = 5,   /* fks_simulate_<family>[_lean]_indiv (fks_set_individual_jacobians) */
-    FKS_KERNEL_COOPERATIVE = 6   /* ABI 10: fks_simulate_<family>_coop (fks_set_cooperative_waves) */
+    FKS_KERNEL_COOPERATIVE = 6,  /* ABI 10: fks_simulate_<family>_coop (fks_set_cooperative_waves) */
+    FKS_KERNEL_SHAPED_SMALL_BATCH = 7 /* ABI 10: the shape-specialised module's small-batch kernel
+                                         (a small batch once the robot's module is built) */
 } fks_kernel_kind;
 /* The launch layout fks_set_robot chose (ABI 8; diagnostic, no reference counterpart). */
 typedef struct fks_launch_info {

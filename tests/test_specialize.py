@@ -73,6 +73,28 @@ def test_specialized_kernel_parity(fks_lib, oracle_lib, name, scale):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name,scale", [c for c in SPEC_CASES if c[0] != "cfg5"])
+def test_shaped_small_batch_kernel_parity(fks_lib, oracle_lib, name, scale):
+    """Once a robot's module is built, a batch that fits the small-batch grid runs the module's
+    small-batch kernel (fks_simulate_shaped_small; lean shapes have none): oracle-exact"""
+    from fast_kinematic_simulator_amd import make_linked_simulator
+
+    wl = getattr(W, name)(scale)
+    sim = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
+    try:
+        sim.set_robot(wl.robot)
+        sim.set_specialization(True)  # builds the module now
+        assert sim.specialization()["active"], sim.specialization()
+        g, o = run_both(wl, sim=sim, call_index=4)
+        print(name, mismatch_report(g, o), g["launch"])
+        assert g["launch"]["last_kernel"] == "shaped_small_batch", g["launch"]
+        assert_identical(g, o)
+        assert_counters_identical(g, o)
+    finally:
+        sim.close()
+
+
+@pytest.mark.gpu
 def test_specialized_segmented_cfg3(fks_lib, oracle_lib):
     """Segment hand-over through the specialised kernel (segments of 3 controller steps)."""
     wl = W.cfg3(64 / 65536)
