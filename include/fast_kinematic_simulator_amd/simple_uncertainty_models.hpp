@@ -144,39 +144,53 @@ inline size_t GetMatchingBin(const JointUncertaintySampleModel& bins, const doub
     throw std::out_of_range("GetMatchingBin: value " + std::to_string(commanded_velocity) + " is not in any bin");
 }
 
-/* UNC:156-222: (commanded velocity, velocity error) CSV rows into num_bins bins splitting
- * [-actuator_limit, actuator_limit] evenly (the outer two open to -inf / +inf), each bin
- * downsampled to bin_elements items with `rng` */
+namespace unc_detail {
+/* the model file's rows, each `commanded velocity, velocity error` (blank lines skipped) */
+inline std::vector<std::pair<double, double>> read_error_rows(const std::string& path) {
+    std::ifstream file(path);
+    if (!file) throw std::runtime_error("LoadModel: cannot read " + path);
+    std::vector<std::pair<double, double>> rows;
+    for (std::string text; std::getline(file, text);) {
+        if (text.empty()) continue;
+        std::vector<double> cells;
+        std::stringstream fields(text);
+        for (std::string field; std::getline(fields, field, ',');) cells.push_back(std::stod(field));
+        if (cells.size() != 2) throw std::runtime_error("LoadModel: rows are `commanded velocity, velocity error`");
+        rows.emplace_back(cells[0], cells[1]);
+    }
+    return rows;
+}
+/* the upper edge of each of `count` bins over [-limit, limit]: the width accumulated from -limit
+ * one bin at a time (the reference's edges, bit for bit), the last edge open (+inf) */
+inline std::vector<double> bin_upper_edges(const double limit, const uint32_t count) {
+    const double width = (limit * 2.0) / (double)count;
+    std::vector<double> upper(count);
+    double edge = -limit;
+    for (uint32_t k = 0; k < count; k++) {
+        edge = edge + width;
+        upper[k] = (k + 1 >= count) ? std::numeric_limits<double>::infinity() : edge;
+    }
+    return upper;
+}
+}  // namespace unc_detail
+
+/* UNC:156-222: the (commanded velocity, velocity error) rows of `model_file` sorted into
+ * num_bins bins over [-actuator_limit, actuator_limit] (the outer two open to -inf / +inf),
+ * each bin then downsampled to bin_elements entries with `rng` */
 template <typename RNG>
 inline std::shared_ptr<JointUncertaintySampleModel> LoadModel(const std::string& model_file, const double actuator_limit,
                                                               const uint32_t num_bins, const uint32_t bin_elements, RNG& rng) {
-    std::ifstream indata(model_file);
-    if (!indata) throw std::runtime_error("LoadModel: cannot read " + model_file);
-    std::string line;
-    std::vector<std::pair<double, double>> raw_data;
-    while (std::getline(indata, line)) {
-        if (line.empty()) continue;
-        std::stringstream line_stream(line);
-        std::string cell;
-        std::vector<double> line_data;
-        while (std::getline(line_stream, cell, ',')) line_data.push_back(std::stod(cell));
-        if (line_data.size() != 2) throw std::runtime_error("LoadModel: rows are `commanded velocity, velocity error`");
-        raw_data.emplace_back(line_data[0], line_data[1]);
+    const std::vector<std::pair<double, double>> rows = unc_detail::read_error_rows(model_file);
+    const std::vector<double> upper = unc_detail::bin_upper_edges(actuator_limit, num_bins);
+    auto model = std::make_shared<JointUncertaintySampleModel>();
+    model->reserve(num_bins);
+    for (uint32_t k = 0; k < num_bins; k++) {
+        const double lower = (k == 0) ? -std::numeric_limits<double>::infinity() : upper[k - 1];
+        model->emplace_back(std::make_pair(lower, upper[k]), std::vector<double>());
     }
-    std::shared_ptr<JointUncertaintySampleModel> bins(new JointUncertaintySampleModel());
-    const double bin_size = (actuator_limit * 2.0) / (double)num_bins;
-    double previous_bin_upper = -actuator_limit;
-    for (size_t idx = 0; idx < num_bins; idx++) {
-        double bin_lower = previous_bin_upper;
-        if (idx == 0) bin_lower = -std::numeric_limits<double>::infinity();
-        double bin_upper = previous_bin_upper + bin_size;
-        if (idx >= (num_bins - 1)) bin_upper = std::numeric_limits<double>::infinity();
-        previous_bin_upper = bin_upper;
-        bins->push_back(std::make_pair(std::make_pair(bin_lower, bin_upper), std::vector<double>()));
-    }
-    for (const auto& data_pair : raw_data) (*bins)[GetMatchingBin(*bins, data_pair.first)].second.push_back(data_pair.second);
-    for (auto& bin_contents : *bins) bin_contents.second = DownsampleBin(bin_contents.second, bin_elements, rng);
-    return bins;
+    for (const std::pair<double, double>& row : rows) (*model)[GetMatchingBin(*model, row.first)].second.push_back(row.second);
+    for (auto& bin : *model) bin.second = DownsampleBin(bin.second, bin_elements, rng);
+    return model;
 }
 /* reproducible bins: the downsampling generator seeded with `seed` */
 inline std::shared_ptr<JointUncertaintySampleModel> LoadModel(const std::string& model_file, const double actuator_limit,
