@@ -323,6 +323,7 @@ PROTOTYPES = [
     ("fks_get_launch_geometry", c_int32, [c_void_p, POINTER(c_uint32), POINTER(c_uint64)]),
     ("fks_set_segment_steps", c_int32, [c_void_p, c_uint32]),
     ("fks_set_segment_policy", c_int32, [c_void_p, c_uint32, c_uint32]),
+    ("fks_set_segment_heavy_relative", c_int32, [c_void_p, c_uint32]),
     ("fks_set_small_batch_kernel", c_int32, [c_void_p, c_int32]),
     ("fks_set_cooperative_waves", c_int32, [c_void_p, c_int32]),
     ("fks_set_specialization", c_int32, [c_void_p, c_int32]),

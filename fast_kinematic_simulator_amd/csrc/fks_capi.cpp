@@ -109,10 +109,14 @@ using fksd::GridDev;
 /* controller steps per segment when a batch outnumbers the resident waves: short
  * enough that a contact-heavy particle progresses from the start of the launch, long
  * enough that the hand-over (resting state + one FK) costs < 1 % */
-constexpr uint32_t kDefaultSegmentSteps = 14; /* re-swept in round 2: profiles/r02ar_sched_sweep_*.json */
+constexpr uint32_t kDefaultSegmentSteps = 14; /* re-swept in round 6: profiles/r06p_sched_ab_cfg*.json */
 /* a segment averaging this many resolver iterations per controller step is
- * contact-heavy: its wave keeps the particle (the cfg3 batch averages 0.65) */
+ * contact-heavy: its wave keeps the particle (the cfg3 batch averages 0.65) ... */
 constexpr uint32_t kHeavyResolverPerStep = 2;
+/* ... if it also has at least this many times the batch's mean resolver iterations per
+ * segment so far: a batch where most segments resolve contacts (cfg5) carries only its
+ * outliers */
+constexpr uint32_t kHeavyRelative = 3;
 using fksd::JointDev;
 using fksd::RobotDev;
 
@@ -288,6 +292,7 @@ struct fks_context {
     uint32_t segment_steps = 0; /* 0 = automatic (kDefaultSegmentSteps) */
     uint32_t heavy_per_step = kHeavyResolverPerStep; /* fks_set_segment_policy */
     uint32_t heavy_priority = 1;
+    uint32_t heavy_relative = kHeavyRelative; /* fks_set_segment_heavy_relative */
     int32_t individual_jacobians = 0; /* fks_set_individual_jacobians (SPCS:420-423) */
     int32_t small_batch = 1;          /* fks_set_small_batch_kernel */
     int32_t cooperative = 0;          /* fks_set_cooperative_waves (opt-in: DESIGN.md §5.4) */
@@ -1323,6 +1328,8 @@ static fks_status simulate_device(fks_context* ctx, const double* d_starts, uint
         const uint64_t heavy = (uint64_t)ctx->heavy_per_step * k;
         a.seg_heavy_resolver = (uint32_t)std::min<uint64_t>(heavy, 0xffffffffull);
         a.seg_heavy_prio = ctx->heavy_priority;
+        /* the relative test's running sums pack 24 bits of segments: off for larger batches */
+        a.seg_heavy_rel = ((uint64_t)n * a.nseg < (1ull << 24)) ? ctx->heavy_relative : 0u;
     }
     if (a.nseg > 1) {
         const size_t words = (size_t)n * a.seg_stride;
@@ -1878,6 +1885,13 @@ fks_status fks_set_small_batch_kernel(fks_context* ctx, int32_t enabled) {
 fks_status fks_set_cooperative_waves(fks_context* ctx, int32_t enabled) {
     if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
     ctx->cooperative = enabled ? 1 : 0;
+    return FKS_OK;
+}
+
+fks_status fks_set_segment_heavy_relative(fks_context* ctx, uint32_t times_mean) {
+    if (!ctx) return FKS_ERR_INVALID_ARGUMENT;
+    if (times_mean > 64u) return fail(ctx, FKS_ERR_INVALID_ARGUMENT, "times_mean must be at most 64");
+    ctx->heavy_relative = times_mean;
     return FKS_OK;
 }
 

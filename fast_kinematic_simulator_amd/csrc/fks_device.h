@@ -365,7 +365,9 @@ struct SimArgs {
     uint32_t seg_stride;          /* doubles per particle in seg_state */
     uint32_t seg_heavy_resolver;  /* resolver iterations that mark a segment contact-heavy (0: off) */
     uint32_t seg_heavy_prio;      /* waves carrying a heavy particle raise their issue priority */
-    uint32_t seg_pad;
+    uint32_t seg_heavy_rel;       /* ... and, when nonzero, at least this many times the batch's mean resolver
+                                   * iterations per segment so far (the running sums in counters[kSchedWord]:
+                                   * 40 bits of iterations over 24 bits of segments) */
     double* scratch;
     uint64_t scratch_per_wave; /* doubles */
     uint32_t row_cap;          /* 3 * P */
@@ -411,7 +413,10 @@ enum {
  * particle queue in the counter buffer; order = FKS_PHASE_* in fks_capi.h */
 enum {
     kPhaseBase = kNumCounters + 2,
-    kCounterWords = kPhaseBase + FKS_NUM_PHASES
+    /* the running sums of the relative heavy-segment test (SimArgs.seg_heavy_rel), on a cache line
+     * of their own (not the ticket counter's) */
+    kSchedWord = ((kPhaseBase + FKS_NUM_PHASES + 15) / 16) * 16,
+    kCounterWords = kSchedWord + 1
 };
 
 }  // namespace fksd

@@ -3963,6 +3963,7 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
     if (ln < kWaveTotals) s.totals()[ln] = 0;
     s.lane_bytes = 0;
     if (ln < 2) self_counters(s)[ln] = 0;
+    if (ln == 0) *reinterpret_cast<uint64_t*>(s.lds() + LAY(*s.A).misc + 6) = 0; /* relative heavy test: pending sums */
     /* timestamps are folded into their LDS sums at once (end - start = (0 - start) + end),
      * so none stays live across the particle loop */
     if (ln == 0) s.phase()[FKS_PHASE_WAVE_RESIDENCY] = 0ull - __builtin_amdgcn_s_memrealtime();
@@ -4211,11 +4212,32 @@ __device__ __forceinline__ void simulate_particles(const SimArgs* __restrict__ a
                 __hip_atomic_store(A.seg_done + local, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 publish_fence(); /* the store is visible before the ticket counter is read (Dekker with the holder) */
                 uint32_t cont = 0;
+                /* a contact-heavy segment (many resolver iterations) keeps its wave: the
+                 * particle's next segment is claimed at once instead of waiting for its
+                 * ticket, so the longest particles are not paced by the round-robin */
+                bool heavy = !ended && A.seg_heavy_resolver != 0 && s.resolver_count >= A.seg_heavy_resolver;
+                if (A.seg_heavy_rel) {
+                    /* relative to the batch: in a contact-heavy batch (its mean so far at or above
+                     * the absolute threshold: most segments resolve contacts) only the outliers
+                     * are carried.  The wave sums its segments in LDS (misc + 6) and adds them to
+                     * the batch's running sums when it has 16 or a candidate needs the mean */
+                    uint64_t* pend = reinterpret_cast<uint64_t*>(s.lds() + LAY(*s.A).misc + 6);
+                    const uint64_t mine = *pend + (((uint64_t)s.resolver_count << 24) | 1ull);
+                    unsigned long long* sums = A.counters + kSchedWord;
+                    if (heavy) {
+                        const uint64_t prior = __hip_atomic_fetch_add(sums, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint64_t segs = prior & 0xffffffull, iters = prior >> 24;
+                        heavy = segs < 256u || iters < (uint64_t)A.seg_heavy_resolver * segs ||
+                                (uint64_t)s.resolver_count * segs >= (uint64_t)A.seg_heavy_rel * iters;
+                        *pend = 0;
+                    } else if ((mine & 0xffffffull) >= 16u) {
+                        (void)__hip_atomic_fetch_add(sums, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        *pend = 0;
+                    } else {
+                        *pend = mine;
+                    }
+                }
                 if (!ended) {
-                    /* a contact-heavy segment (many resolver iterations) keeps its wave: the
-                     * particle's next segment is claimed at once instead of waiting for its
-                     * ticket, so the longest particles are not paced by the round-robin */
-                    const bool heavy = A.seg_heavy_resolver != 0 && s.resolver_count >= A.seg_heavy_resolver;
                     const uint64_t next_ticket = (seg + 1) * A.n + local;
                     const uint64_t issued =
                         heavy ? ~0ull : __hip_atomic_load(A.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -157,6 +157,11 @@ class HipParticleContactSimulator:
         _capi.check(self._lib.fks_set_segment_policy(self._ctx, int(heavy_resolver_per_step), int(heavy_priority)), self._ctx,
                     "segment policy")
 
+    def set_segment_heavy_relative(self, times_mean: int = 3):
+        """A heavy segment must also exceed times_mean x the batch's running mean resolver
+        iterations per segment (fks_set_segment_heavy_relative; 0 = off).  Results do not depend on it."""
+        _capi.check(self._lib.fks_set_segment_heavy_relative(self._ctx, int(times_mean)), self._ctx, "segment heavy relative")
+
     def set_small_batch_kernel(self, enabled: bool = True):
         """Batches that fit the low-occupancy instantiation's resident waves run it
         (fks_set_small_batch_kernel; default on).  Results do not depend on it."""

@@ -70,7 +70,8 @@ extern "C" {
  *    fks_specialization_info (failed, message), fks_multi_set_active_devices, pinned per-device
  *    staging in fks_multi_*
  * 10: cooperative small batches (fks_set_cooperative_waves, FKS_KERNEL_COOPERATIVE, launch
- *    info cooperative_*), the shape-specialised small-batch kernel (FKS_KERNEL_SHAPED_SMALL_BATCH) */
+ *    info cooperative_*), the shape-specialised small-batch kernel (FKS_KERNEL_SHAPED_SMALL_BATCH),
+ *    fks_set_segment_heavy_relative */
 #define FKS_ABI_VERSION 10
 
 typedef enum {
@@ -487,6 +488,12 @@ fks_status fks_set_segment_steps(fks_context* ctx, uint32_t controller_steps);
  *     2 = also 1 for particles that fell behind the round-robin).
  * The priority is reset to 0 at the start of every segment a wave claims. */
 fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_step, uint32_t heavy_priority);
+/* ABI 10: once the batch's mean resolver iterations per finished segment reaches the absolute
+ * threshold (a contact-heavy batch), a heavy segment must also have at least `times_mean` times
+ * that mean (the kernel keeps the running sums; default 3, 0 = the absolute test alone, at most
+ * 64; off for batches of 2^24 or more particle-segments).  Results are bit-identical for every
+ * value. */
+fks_status fks_set_segment_heavy_relative(fks_context* ctx, uint32_t times_mean);
 /* Small batches (ABI 7; no reference counterpart, results are bit-identical either way):
  * with `enabled` (the default) a plain simulation call whose particles all fit the
  * resident waves of a low-occupancy instantiation (two waves per SIMD, no register

@@ -68,6 +68,8 @@ def test_argument_validation(fks_lib):
     assert fks_lib.fks_set_segment_steps(None, 10) == 1
     assert fks_lib.fks_set_segment_policy(None, 2, 1) == 1
     assert fks_lib.fks_set_small_batch_kernel(None, 1) == 1
+    assert fks_lib.fks_set_segment_heavy_relative(None, 3) == 1
+    assert fks_lib.fks_set_cooperative_waves(None, 1) == 1
     assert fks_lib.fks_set_individual_jacobians(None, 1) == 1
     waves, lds = ctypes.c_uint32(0), ctypes.c_uint64(0)
     assert fks_lib.fks_get_launch_geometry(None, ctypes.byref(waves), ctypes.byref(lds)) == 1

@@ -23,8 +23,8 @@
 #   tailcoop:<wl>:<lib>   the same, the lone particles on the cooperative kernel -> <tag>_tailcoop_<wl>_<lib>.json
 #   tailpmc:<wl>:<lib> instruction-mix and wait counters of the batch and the heaviest particle
 #                      alone (three --pmc passes over tools/tail_latency.py --top 1) -> <tag>_tailpmc_<wl>_<lib>/
-#   sched:<wl>:<segs>:<heavy>  scheduling sweep (tools/sched_sweep.py; comma lists of segment lengths and
-#                      heavy thresholds, priority 1) -> <tag>_sched_<wl>.json
+#   sched:<wl>:<segs>:<heavy>[:<rel>]  scheduling sweep (tools/sched_sweep.py; comma lists of segment lengths,
+#                      heavy thresholds and relative factors (default 3), priority 1) -> <tag>_sched_<wl>.json
 #   torchrun1          bench.py through torch.distributed.run, world size 1 (RCCL) -> <tag>_torchrun_w1.json
 #   inproc:<devices>   bench.py --in-process over a device list (e.g. 0 or 0,0) with the strong-scaling
 #                      projection -> <tag>_inproc_<devices>.json
@@ -112,9 +112,10 @@ run_task() {
     timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $D/more -o m -- $BM > $D.more.log 2>&1
     rc=$?; unset FKS_LIB_PATH FKS_VARIANT_LIB; return $rc ;;
   sched:*)
-    spec=${1#sched:}; w=${spec%%:*}; rest=${spec#*:}; seg=${rest%%:*}; heavy=${rest#*:}
+    spec=${1#sched:}; w=${spec%%:*}; rest=${spec#*:}; seg=${rest%%:*}; rest=${rest#*:}; heavy=${rest%%:*}; rel=3
+    [ "$rest" != "$heavy" ] && rel=${rest#*:}
     np=""; [ "$w" = cfg4 -o "$w" = cfg5 ] && np="--particles 131072"
-    timeout -k 10 600 python tools/sched_sweep.py --workload $w $np --segments $seg --heavy $heavy --prio 1 --json $O/${TAG}_sched_$w.json > $O/${TAG}_sched_$w.log 2>&1 ;;
+    timeout -k 10 600 python tools/sched_sweep.py --workload $w $np --segments $seg --heavy $heavy --prio 1 --rel $rel --json $O/${TAG}_sched_$w.json > $O/${TAG}_sched_$w.log 2>&1 ;;
   inproc:*) d=${1#inproc:}; timeout -k 10 400 python bench.py --in-process --devices $d --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_inproc_${d//,/}.json 2> $O/${TAG}_inproc_${d//,/}.err ;;
   torchrun1) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_torchrun_w1.json 2> $O/${TAG}_torchrun_w1.err ;;
   round) for t in suite smoke bench trace pmc others; do run_task $t || return $?; done ;;

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--segments", default="5,10,20")
     ap.add_argument("--heavy", default="1,2,4,65536")
     ap.add_argument("--prio", default="0,1,2")
+    ap.add_argument("--rel", default="3", help="fks_set_segment_heavy_relative values (0 = off)")
     ap.add_argument("--json", default="")
     ap.add_argument("--particles", type=int, default=0, help="batch size (default: the workload's base count)")
     a = ap.parse_args()
@@ -52,11 +53,13 @@ def main():
 
     run()
     rows = []
-    for seg, heavy, prio in itertools.product(*[[int(v) for v in x.split(",")] for x in (a.segments, a.heavy, a.prio)]):
+    for seg, heavy, prio, rel in itertools.product(*[[int(v) for v in x.split(",")] for x in (a.segments, a.heavy, a.prio, a.rel)]):
         sim.set_segment_steps(seg)
         sim.set_segment_policy(heavy, prio)
+        sim.set_segment_heavy_relative(rel)
         ms = min(run(), run())
-        rows.append({"segment_steps": seg, "heavy_resolver_per_step": heavy, "heavy_priority": prio, "kernel_ms": ms})
+        rows.append({"segment_steps": seg, "heavy_resolver_per_step": heavy, "heavy_priority": prio, "heavy_relative": rel,
+                     "kernel_ms": ms})
         print(json.dumps(rows[-1]), flush=True)
     best = min(rows, key=lambda r: r["kernel_ms"])
     print("best", json.dumps(best))
