@@ -85,6 +85,36 @@ def test_segmented_parity(fks_lib, oracle_lib, name, scale, segment_steps):
 
 
 @pytest.mark.gpu
+def test_scheduling_policy_never_changes_results(fks_lib):
+    """The heavy-segment policy (absolute and batch-relative thresholds, issue priority) only
+    decides which wave runs a segment when: a contact-heavy batch (cfg5, 2,048 particles in
+    7-step segments, so the relative test binds) gives the same bytes under every setting"""
+    from fast_kinematic_simulator_amd import make_linked_simulator
+
+    wl = W.cfg5(2048 / 1048576)
+    sim = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
+    try:
+        sim.set_segment_steps(7)
+        runs = []
+        for heavy, prio, rel in ((2, 1, 3), (2, 1, 0), (65536, 0, 0), (1, 2, 1)):
+            sim.set_segment_policy(heavy, prio)
+            sim.set_segment_heavy_relative(rel)
+            sim.set_call_index(1)
+            sim.reset_statistics()
+            r = sim.forward_simulate_arrays(wl.robot, wl.starts, wl.targets, wl.allow_contacts)
+            r["counters"] = {k: sim.last_call_counters()[k] for k in ("microsteps", "resolver_iterations", "sdf_bytes")}
+            r["statistics"] = sim.get_statistics()
+            runs.append(r)
+        for r in runs[1:]:
+            for k in ("positions", "collided", "microsteps", "resolver_iterations", "error_flags"):
+                assert np.array_equal(r[k], runs[0][k]), k
+            assert r["counters"] == runs[0]["counters"] and r["statistics"] == runs[0]["statistics"]
+        assert runs[0]["counters"]["resolver_iterations"] > 0
+    finally:
+        sim.close()
+
+
+@pytest.mark.gpu
 def test_segmented_early_stops(fks_lib, oracle_lib):
     """allow_contacts = false ends particles mid-segment (SPCS:904-909): later
     segments of an ended particle are skipped, its outputs stay those of the stop."""
