@@ -87,6 +87,38 @@ def test_empty_batches(fks_lib):
         assert t["positions"].shape == (0, 3) and buf.num_steps.shape == (0,)
         # the context still works afterwards
         assert_identical(*run_both(wl, sim=sim))
+        # ... and every small-batch kernel takes an empty batch too: the cooperative one, and the
+        # module's own once the robot's module is built
+        sim.set_cooperative_waves(True)
+        assert sim.forward_simulate_arrays(wl.robot, np.zeros((0, 3)), wl.targets, True)["positions"].shape == (0, 3)
+        sim.set_cooperative_waves(False)
+        sim.set_specialization(True)
+        assert sim.forward_simulate_arrays(wl.robot, np.zeros((0, 3)), wl.targets, True)["positions"].shape == (0, 3)
+        assert_identical(*run_both(wl, sim=sim))
+        assert sim.launch_info()["last_kernel"] == "shaped_small_batch"
+    finally:
+        sim.close()
+
+
+@pytest.mark.gpu
+def test_small_batch_grid_boundary(fks_lib):
+    """A batch of exactly the small-batch grid runs the module's small-batch kernel, one particle
+    more the throughput kernel: the shared particles' outcomes are the same bytes"""
+    wl = W.cfg2()
+    sim = make_linked_simulator(wl.environment(), wl.solver, wl.controller_frequency, wl.seed)
+    try:
+        sim.set_robot(wl.robot)
+        sim.set_specialization(True)
+        n = sim.launch_info()["small_batch_resident_waves"]
+        assert 0 < n < len(wl.starts)
+        sim.set_call_index(2)
+        a = sim.forward_simulate_arrays(wl.robot, wl.starts[:n], wl.targets, True)
+        assert sim.launch_info()["last_kernel"] == "shaped_small_batch"
+        sim.set_call_index(2)
+        b = sim.forward_simulate_arrays(wl.robot, wl.starts[:n + 1], wl.targets, True)
+        assert sim.launch_info()["last_kernel"] == "shaped"
+        for k in ("positions", "collided", "microsteps", "resolver_iterations", "error_flags"):
+            assert np.array_equal(a[k], b[k][:n]), k
     finally:
         sim.close()
 
