@@ -291,7 +291,7 @@ struct fks_context {
     /* controller-step segments: resting particle state between segments */
     uint32_t segment_steps = 0; /* 0 = automatic (kDefaultSegmentSteps) */
     uint32_t heavy_per_step = kHeavyResolverPerStep; /* fks_set_segment_policy */
-    uint32_t heavy_priority = 1;
+    uint32_t heavy_priority = 2; /* round 6: cfg5 -2 %, cfg3 / cfg4 equal (profiles/r06prio_*.json) */
     uint32_t heavy_relative = kHeavyRelative; /* fks_set_segment_heavy_relative */
     int32_t individual_jacobians = 0; /* fks_set_individual_jacobians (SPCS:420-423) */
     int32_t small_batch = 1;          /* fks_set_small_batch_kernel */

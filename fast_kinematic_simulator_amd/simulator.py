@@ -151,7 +151,7 @@ class HipParticleContactSimulator:
         0 = automatic).  Results do not depend on it."""
         _capi.check(self._lib.fks_set_segment_steps(self._ctx, int(controller_steps)), self._ctx, "segment steps")
 
-    def set_segment_policy(self, heavy_resolver_per_step: int = 2, heavy_priority: int = 1):
+    def set_segment_policy(self, heavy_resolver_per_step: int = 2, heavy_priority: int = 2):
         """Scheduling policy of segmented batches (fks_set_segment_policy): contact-heavy
         segments keep their wave and raise its issue priority.  Results do not depend on it."""
         _capi.check(self._lib.fks_set_segment_policy(self._ctx, int(heavy_resolver_per_step), int(heavy_priority)), self._ctx,

@@ -484,8 +484,8 @@ fks_status fks_set_segment_steps(fks_context* ctx, uint32_t controller_steps);
  *     particle's next segment instead of returning it to the round-robin (0 = off;
  *     default 2; at most 65536);
  *   heavy_priority: issue priority (s_setprio 0..2) of a wave carrying a contact-heavy
- *     particle (default 1 = raised to 2 for heavy segments only; 0 = never raised;
- *     2 = also 1 for particles that fell behind the round-robin).
+ *     particle (1 = raised to 2 for heavy segments only; 0 = never raised; 2, the default
+ *     since ABI 10 = also 1 for particles that fell behind the round-robin).
  * The priority is reset to 0 at the start of every segment a wave claims. */
 fks_status fks_set_segment_policy(fks_context* ctx, uint32_t heavy_resolver_per_step, uint32_t heavy_priority);
 /* ABI 10: once the batch's mean resolver iterations per finished segment reaches the absolute
